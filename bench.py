@@ -1,0 +1,211 @@
+#!/usr/bin/env python
+"""Throughput of the FlockingRelative-v0 env step on MI355X, in agent-steps/s.
+
+One "step" = one batched FlockingRelativeEnv.step() over all of this GPU's envs
+(dynamics + compute_helpers + instant_cost, reference flocking_relative.py:91-147),
+with the dense (N,N) float32 network, (N,6) state_values and rewards left in HBM.
+Workload (BASELINE.json configs[1]): N=1024 agents x 256 envs per GPU, synthetic
+random-init swarms, float32 actions U(-1,1) resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Multi-GPU: the env batch is sharded (256 envs per rank, weak scaling, no exchange on
+the step path); per-env rewards are all-gathered with RCCL on a side stream after
+each step (the metrics path). torch.distributed (gloo, CPU) is used only for the
+rendezvous, barriers and the max-over-ranks time; it never touches the GPU.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gym-flock_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def step_bytes(n):
+    """Algorithmic HBM bytes of one env-step: read x (float64,
+    32N) + u (float32, 8N); write x (32N), state_values (float32, 24N), network
+    (float32, 4N^2) and the reward (8)."""
+    return 4 * n * n + 96 * n + 8
+
+
+def cpu_baseline(n_agents, seconds):
+    """The oracle's NumPy step (one core) on env 0 of the same synthetic workload."""
+    from oracle import flocking as orc
+    from gym_flock.init_states import synthetic_state
+
+    x = synthetic_state(n_agents, 0)
+    rs = np.random.RandomState(1234)
+    u = rs.uniform(-1, 1, size=(n_agents, 2)).astype(np.float32)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        out = orc.step(x, u)
+        x = out["x"]
+        steps += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and steps >= 3) or steps >= 100000:
+            break
+    return {"value": n_agents * steps / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": "oracle/flocking.py step() (NumPy, float64, 1 thread) on 1 env of N=%d for "
+                      "%d steps (%.1f s); same synthetic init and float32 actions as the GPU run"
+                      % (n_agents, steps, el)}
+
+
+def load_traffic(n_agents, n_envs):
+    """Per-launch HBM bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE,
+    gfx950 correction) for this workload, committed under profiles/; None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get("%dx%d" % (n_agents, n_envs))
+        return None if e is None else float(e["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n-agents", type=int, default=1024)
+    ap.add_argument("--n-envs", type=int, default=256, help="envs per GPU")
+    ap.add_argument("--metrics-every", type=int, default=1, help="reward all-gather period (N>1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-controller-line", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # CPU (gloo) only: rendezvous, barrier, max
+        dist.init_process_group("gloo")
+
+    from gym_flock.shard import RcclRewardGather
+    from gym_flock.vec import VecFlockingRelative
+
+    N, B, K, W = args.n_agents, args.n_envs, args.steps, args.warmup
+    t_setup = time.perf_counter()
+    env = VecFlockingRelative(B, N, device=local_rank, env_offset=rank * B)
+    env.reset(seed=0)
+    u = np.random.RandomState(1234 + rank).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    env.set_actions(u)
+    gather = None
+    if world > 1:
+        uid = [env.h.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        gather = RcclRewardGather(env.h, world, rank, uid[0])
+    log("setup %.1fs: N=%d B=%d per GPU, world=%d" % (time.perf_counter() - t_setup, N, B, world))
+
+    def run(k, with_ctrl=False):
+        for s in range(k):
+            if with_ctrl:
+                env.step(expert=True, controller=True)
+            else:
+                env.step(resident=True)
+            if gather is not None and (s + 1) % args.metrics_every == 0:
+                gather.issue()
+
+    def barrier():
+        env.sync()
+        if dist is not None:
+            dist.barrier()
+
+    run(W)
+    barrier()
+    env.h.timing_start()
+    t0 = time.perf_counter()
+    run(K)
+    env.sync()
+    t1 = time.perf_counter()
+    kernel_ms, launches = env.h.timing_stop()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    extra = {}
+    if gather is not None:
+        allr = gather.result()
+        mine = env.rewards()
+        extra["gathered_rewards_ok"] = bool(np.array_equal(allr[rank * B:(rank + 1) * B], mine))
+
+    # closed-loop step + fused controller (u = previous controller output), same workload
+    if not args.no_controller_line:
+        env.reset(seed=0)
+        env.controller()
+        run(min(W, 5), with_ctrl=True)
+        barrier()
+        t2 = time.perf_counter()
+        run(K, with_ctrl=True)
+        env.sync()
+        t3 = time.perf_counter()
+        barrier()
+        ec = t3 - t2
+        if dist is not None:
+            import torch
+            t = torch.tensor([ec], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ec = float(t.item())
+        extra["step_with_controller"] = {"value": world * B * N * K / ec, "unit": "agent-steps/s",
+                                         "ms_per_step": 1e3 * ec / K}
+
+    if rank == 0:
+        value = world * B * N * K / elapsed
+        bytes_launch = B * step_bytes(N)
+        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+        traffic = load_traffic(N, B)
+        line = {
+            "metric": "agent-steps/sec (N_agents×N_envs×steps/s), FlockingRelative N=1024",
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": 1e3 * elapsed / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (random-init swarms, SURVEY.md §8d; float32 actions U(-1,1) resident in HBM)",
+            "config": {"workload": "FlockingRelative-v0 step(), N=%d agents x %d envs per GPU "
+                                   "(BASELINE.json configs[1])" % (N, B),
+                       "n_agents": N, "envs_per_gpu": B, "global_envs": world * B,
+                       "outputs": "network (N,N) f32 + state_values (N,6) f32 + reward, in HBM",
+                       "parallelism": "env-sharded dp%d, RCCL reward all-gather" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "flock_step_kernel<DYN,f32 u>", "kernel_ms": kernel_ms,
+                         "launches_timed": launches, "algorithmic_bytes_per_launch": bytes_launch},
+        }
+        line.update(extra)
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline (oracle, 1 core, ~%.0fs)..." % args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    env.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

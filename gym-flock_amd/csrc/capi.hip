@@ -1,0 +1,596 @@
+// C-ABI of libgymflock.so (include/gymflock.h): handle lifecycle, device buffers,
+// stream-ordered launches, host transfers, RCCL metrics path and error reporting.
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "flock_internal.h"
+#include "gymflock.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int fail_hip(const char* what, hipError_t e) {
+  return fail(GF_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define GF_HIP(expr)                                        \
+  do {                                                      \
+    hipError_t e_ = (expr);                                 \
+    if (e_ != hipSuccess) return fail_hip(#expr, e_);       \
+  } while (0)
+
+constexpr int kRewardSlots = 8;  // reward ring: step t writes slot t % 8
+
+}  // namespace
+
+struct fe_handle {
+  fe_config cfg{};
+  hipStream_t stream = nullptr;
+  hipStream_t comm_stream = nullptr;
+  double* x[2] = {nullptr, nullptr};
+  int cur = 0;
+  void* u = nullptr;                    // (B,N,2) up to float64
+  double* ctrl[2] = {nullptr, nullptr};
+  int ccur = 0;
+  float* sv = nullptr;
+  float* net = nullptr;
+  double* reward_ring = nullptr;        // kRewardSlots x B
+  int rslot = 0;
+  int32_t* knn_idx = nullptr;
+  float* knn_obs = nullptr;
+  double* vel_diffs = nullptr;
+  double* min_dists = nullptr;
+  int32_t* degree = nullptr;
+  int u_resident_f64 = -1;              // dtype of the resident actions (-1: none)
+  bool has_state = false, has_ctrl = false, has_obs = false, has_knn = false;
+  int R = 0, T = 0, bpe = 0;
+  size_t BN = 0;
+  // kernel timing (bench roofline)
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  // RCCL metrics path
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  double* gather = nullptr;             // kRewardSlots x nranks x B
+  hipEvent_t step_ev = nullptr;
+  hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
+  hipEvent_t ag_ev[kRewardSlots] = {};
+  bool ag_pending[kRewardSlots] = {};
+  int last_gather = -1;
+};
+
+namespace {
+
+int use_dev(const fe_handle* h) {
+  GF_HIP(hipSetDevice(h->cfg.device));
+  return GF_OK;
+}
+
+template <class T>
+int dalloc(T** p, size_t count) {
+  if (count == 0) {
+    *p = nullptr;
+    return GF_OK;
+  }
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+  if (e != hipSuccess) return fail(GF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return GF_OK;
+}
+
+void release(fe_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->cfg.device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
+  if (h->comm) ncclCommDestroy(h->comm);
+  void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
+                  h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  for (hipEvent_t e : h->ev) hipEventDestroy(e);
+  if (h->step_ev) hipEventDestroy(h->step_ev);
+  if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
+  for (hipEvent_t e : h->ag_ev)
+    if (e) hipEventDestroy(e);
+  if (h->stream) hipStreamDestroy(h->stream);
+  if (h->comm_stream) hipStreamDestroy(h->comm_stream);
+  delete h;
+}
+
+int check_env(const fe_handle* h, int env) {
+  if (env >= h->cfg.n_envs) return fail(GF_EINVAL, "env index out of range");
+  return GF_OK;
+}
+
+double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h->cfg.n_envs; }
+
+// Advance the reward ring before a launch that writes rewards; if an all-gather may
+// still be reading that slot, order the stream behind it (a device-side wait).
+int next_reward_slot(fe_handle* h) {
+  h->rslot = (h->rslot + 1) % kRewardSlots;
+  if (h->ag_pending[h->rslot]) {
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ag_ev[h->rslot], 0));
+    h->ag_pending[h->rslot] = false;
+  }
+  return GF_OK;
+}
+
+gf::StepArgs base_args(fe_handle* h) {
+  gf::StepArgs a{};
+  a.dt = h->cfg.dt;
+  a.action_scalar = h->cfg.action_scalar;
+  a.cr = h->cfg.comm_radius;
+  a.cr2 = h->cfg.comm_radius * h->cfg.comm_radius;
+  a.dt_f = static_cast<float>(h->cfg.dt);
+  a.as_f = static_cast<float>(h->cfg.action_scalar);
+  a.N = h->cfg.n_agents;
+  a.B = h->cfg.n_envs;
+  a.R = h->R;
+  a.T = h->T;
+  a.bpe = h->bpe;
+  a.mean_pooling = h->cfg.mean_pooling;
+  a.centralized = h->cfg.centralized;
+  return a;
+}
+
+int timed_launch(fe_handle* h, const gf::StepArgs& a, bool dyn, bool uf64, bool ctrl) {
+  if (h->timing) {
+    if (h->ev_used + 2 > h->ev.size()) {
+      for (int k = 0; k < 64; ++k) {
+        hipEvent_t e;
+        GF_HIP(hipEventCreate(&e));
+        h->ev.push_back(e);
+      }
+    }
+    GF_HIP(hipEventRecord(h->ev[h->ev_used], h->stream));
+  }
+  hipError_t e = gf::launch_step(a, dyn, uf64, ctrl, h->stream);
+  if (e != hipSuccess) return fail_hip("flock_step_kernel launch", e);
+  if (h->timing) {
+    GF_HIP(hipEventRecord(h->ev[h->ev_used + 1], h->stream));
+    h->ev_used += 2;
+  }
+  return GF_OK;
+}
+
+int launch_knn_cur(fe_handle* h) {
+  gf::KnnArgs k{};
+  k.x = h->x[h->cur];
+  k.idx = h->knn_idx;
+  k.obs = h->knn_obs;
+  k.N = h->cfg.n_agents;
+  k.B = h->cfg.n_envs;
+  k.K = h->cfg.n_neighbors;
+  hipError_t e = gf::launch_knn(k, h->stream);
+  if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
+  h->has_knn = true;
+  return GF_OK;
+}
+
+int d2h(fe_handle* h, void* dst, const void* src, size_t bytes) {
+  GF_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fe_last_error(void) { return g_err.c_str(); }
+int fe_abi_version(void) { return GF_ABI_VERSION; }
+
+int fe_create(const fe_config* cfg, fe_handle** out) {
+  if (!cfg || !out) return fail(GF_EINVAL, "null argument");
+  *out = nullptr;
+  if (cfg->n_agents < 1 || cfg->n_envs < 1) return fail(GF_EINVAL, "n_agents and n_envs must be >= 1");
+  if (cfg->n_neighbors < 0 || cfg->n_neighbors > cfg->n_agents)
+    return fail(GF_EINVAL, "n_neighbors must be in [0, n_agents] (the reference indexes argsort columns)");
+  if (cfg->n_neighbors > 0) {
+    static const int ok[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16};
+    bool found = false;
+    for (int k : ok) found |= (k == cfg->n_neighbors);
+    if (!found) return fail(GF_EINVAL, "n_neighbors must be one of 1-8, 10, 12, 16");
+  }
+  if (!(cfg->comm_radius > 0) || !(cfg->action_scalar != 0)) return fail(GF_EINVAL, "bad comm_radius/action_scalar");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return fail(GF_EHIP, "no HIP device available (libgymflock needs an MI355X)");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(GF_EINVAL, "device ordinal out of range");
+
+  fe_handle* h = new fe_handle();
+  h->cfg = *cfg;
+  const size_t B = cfg->n_envs, N = cfg->n_agents;
+  h->BN = B * N;
+  h->R = gf::step_rows_per_block(cfg->n_agents);
+  h->T = gf::step_tile(cfg->n_agents);
+  h->bpe = (cfg->n_agents + h->R - 1) / h->R;
+  if ((size_t)h->bpe * B > 0x7fffffff) {
+    delete h;
+    return fail(GF_EINVAL, "grid too large");
+  }
+  int rc = GF_OK;
+  if ((e = hipSetDevice(cfg->device)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) {
+    release(h);
+    return fail_hip("stream create", e);
+  }
+  if ((rc = dalloc(&h->x[0], h->BN * 4)) || (rc = dalloc(&h->x[1], h->BN * 4)) ||
+      (rc = dalloc(reinterpret_cast<double**>(&h->u), h->BN * 2)) || (rc = dalloc(&h->ctrl[0], h->BN * 2)) ||
+      (rc = dalloc(&h->ctrl[1], h->BN * 2)) || (rc = dalloc(&h->sv, h->BN * 6)) ||
+      (rc = dalloc(&h->net, h->BN * N)) || (rc = dalloc(&h->reward_ring, (size_t)kRewardSlots * B)) ||
+      (rc = dalloc(&h->knn_idx, h->BN * cfg->n_neighbors)) ||
+      (rc = dalloc(&h->knn_obs, h->BN * 4 * cfg->n_neighbors))) {
+    release(h);
+    return rc;
+  }
+  if ((e = hipEventCreateWithFlags(&h->h2d_ev, hipEventDisableTiming)) != hipSuccess) {
+    release(h);
+    return fail_hip("event create", e);
+  }
+  if ((e = hipMemsetAsync(h->reward_ring, 0, sizeof(double) * kRewardSlots * B, h->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
+    release(h);
+    return fail_hip("init", e);
+  }
+  *out = h;
+  return GF_OK;
+}
+
+int fe_destroy(fe_handle* h) {
+  release(h);
+  return GF_OK;
+}
+
+int fe_get_config(const fe_handle* h, fe_config* out) {
+  if (!h || !out) return fail(GF_EINVAL, "null argument");
+  *out = h->cfg;
+  return GF_OK;
+}
+
+int fe_set_state(fe_handle* h, const double* x) {
+  if (!h || !x) return fail(GF_EINVAL, "null argument");
+  if (int rc = use_dev(h)) return rc;
+  GF_HIP(hipMemcpyAsync(h->x[h->cur], x, h->BN * 4 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  h->has_state = true;
+  h->has_ctrl = h->has_obs = h->has_knn = false;
+  return GF_OK;
+}
+
+int fe_set_state_env(fe_handle* h, int env, const double* x) {
+  if (!h || !x || env < 0) return fail(GF_EINVAL, "bad argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (int rc = use_dev(h)) return rc;
+  const size_t n = (size_t)h->cfg.n_agents * 4;
+  GF_HIP(hipMemcpyAsync(h->x[h->cur] + env * n, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  h->has_state = true;
+  h->has_ctrl = h->has_obs = h->has_knn = false;
+  return GF_OK;
+}
+
+int fe_get_state(fe_handle* h, double* x) {
+  if (!h || !x) return fail(GF_EINVAL, "null argument");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  if (int rc = use_dev(h)) return rc;
+  return d2h(h, x, h->x[h->cur], h->BN * 4 * sizeof(double));
+}
+
+int fe_get_state_env(fe_handle* h, int env, double* x) {
+  if (!h || !x || env < 0) return fail(GF_EINVAL, "bad argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  if (int rc = use_dev(h)) return rc;
+  const size_t n = (size_t)h->cfg.n_agents * 4;
+  return d2h(h, x, h->x[h->cur] + env * n, n * sizeof(double));
+}
+
+int fe_compute_helpers(fe_handle* h, int flags) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  if (int rc = use_dev(h)) return rc;
+  const bool ctrl = flags & FE_WITH_CONTROLLER;
+  if (int rc = next_reward_slot(h)) return rc;
+  gf::StepArgs a = base_args(h);
+  a.x_in = h->x[h->cur];
+  a.state_values = (flags & FE_NO_STATE_VALUES) ? nullptr : h->sv;
+  a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
+  a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
+  a.reward = cur_reward(h);
+  if (int rc = timed_launch(h, a, false, false, ctrl)) return rc;
+  if (ctrl) {
+    h->ccur ^= 1;
+    h->has_ctrl = true;
+  }
+  h->has_obs = true;
+  if ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0)
+    if (int rc = launch_knn_cur(h)) return rc;
+  return GF_OK;
+}
+
+int fe_step(fe_handle* h, const void* u, int flags) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set (call fe_set_state first)");
+  if (int rc = use_dev(h)) return rc;
+  const bool ctrl = flags & FE_WITH_CONTROLLER;
+  bool uf64 = flags & FE_U_F64;
+  const void* up = nullptr;
+  if (flags & FE_U_EXPERT) {
+    if (!h->has_ctrl) return fail(GF_ESTATE, "FE_U_EXPERT needs a previous controller output");
+    up = h->ctrl[h->ccur];
+    uf64 = true;
+  } else if (flags & FE_U_RESIDENT) {
+    if (h->u_resident_f64 < 0) return fail(GF_ESTATE, "FE_U_RESIDENT needs fe_set_actions first");
+    up = h->u;
+    uf64 = h->u_resident_f64 == 1;
+  } else if (!u) {
+    return fail(GF_EINVAL, "null action pointer");
+  } else if (flags & FE_U_DEVICE) {
+    up = u;
+  } else {
+    GF_HIP(hipMemcpyAsync(h->u, u, h->BN * 2 * (uf64 ? 8 : 4), hipMemcpyHostToDevice, h->stream));
+    GF_HIP(hipEventRecord(h->h2d_ev, h->stream));
+    up = h->u;
+    h->u_resident_f64 = -1;  // the buffer now holds this call's actions
+  }
+  if (int rc = next_reward_slot(h)) return rc;
+  gf::StepArgs a = base_args(h);
+  a.x_in = h->x[h->cur];
+  a.x_out = h->x[h->cur ^ 1];
+  a.u = up;
+  a.state_values = (flags & FE_NO_STATE_VALUES) ? nullptr : h->sv;
+  a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
+  a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
+  a.reward = cur_reward(h);
+  if (int rc = timed_launch(h, a, true, uf64, ctrl)) return rc;
+  h->cur ^= 1;
+  if (ctrl) h->ccur ^= 1;
+  h->has_ctrl = ctrl;
+  h->has_obs = true;
+  h->has_knn = false;
+  if ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0)
+    if (int rc = launch_knn_cur(h)) return rc;
+  // the host action buffer is borrowed only for this call: wait for its copy, not the step
+  if (!(flags & (FE_U_DEVICE | FE_U_EXPERT | FE_U_RESIDENT))) GF_HIP(hipEventSynchronize(h->h2d_ev));
+  return GF_OK;
+}
+
+int fe_set_actions(fe_handle* h, const void* u, int f64) {
+  if (!h || !u) return fail(GF_EINVAL, "null argument");
+  if (int rc = use_dev(h)) return rc;
+  GF_HIP(hipMemcpyAsync(h->u, u, h->BN * 2 * (f64 ? 8 : 4), hipMemcpyHostToDevice, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  h->u_resident_f64 = f64 ? 1 : 0;
+  return GF_OK;
+}
+
+int fe_controller(fe_handle* h, int centralized, double* u_out) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  if (int rc = use_dev(h)) return rc;
+  gf::StepArgs a = base_args(h);
+  if (centralized >= 0) a.centralized = centralized ? 1 : 0;
+  a.x_in = h->x[h->cur];
+  a.ctrl_out = h->ctrl[h->ccur ^ 1];
+  hipError_t e = gf::launch_step(a, false, false, true, h->stream);
+  if (e != hipSuccess) return fail_hip("controller launch", e);
+  h->ccur ^= 1;
+  h->has_ctrl = true;
+  if (u_out) return d2h(h, u_out, h->ctrl[h->ccur], h->BN * 2 * sizeof(double));
+  return GF_OK;
+}
+
+int fe_get_stats(fe_handle* h, int env, double* vel_diffs, double* min_dists) {
+  return fe_get_stats_ex(h, env, vel_diffs, min_dists, nullptr);
+}
+
+int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists, int32_t* degree) {
+  if (!h || env < 0) return fail(GF_EINVAL, "bad argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  if (int rc = use_dev(h)) return rc;
+  if (!h->vel_diffs) {
+    if (int rc = dalloc(&h->vel_diffs, h->BN)) return rc;
+    if (int rc = dalloc(&h->min_dists, h->BN)) return rc;
+    if (int rc = dalloc(&h->degree, h->BN)) return rc;
+  }
+  gf::StatsArgs s{h->x[h->cur], h->vel_diffs, h->min_dists, h->degree,
+                  h->cfg.comm_radius * h->cfg.comm_radius, h->cfg.n_agents, h->cfg.n_envs};
+  hipError_t e = gf::launch_stats(s, h->stream);
+  if (e != hipSuccess) return fail_hip("stats launch", e);
+  const size_t N = h->cfg.n_agents;
+  if (vel_diffs) GF_HIP(hipMemcpyAsync(vel_diffs, h->vel_diffs + env * N, N * 8, hipMemcpyDeviceToHost, h->stream));
+  if (min_dists) GF_HIP(hipMemcpyAsync(min_dists, h->min_dists + env * N, N * 8, hipMemcpyDeviceToHost, h->stream));
+  if (degree) GF_HIP(hipMemcpyAsync(degree, h->degree + env * N, N * 4, hipMemcpyDeviceToHost, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int fe_get_state_values(fe_handle* h, int env, float* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (int rc = use_dev(h)) return rc;
+  const size_t n = (size_t)h->cfg.n_agents * 6;
+  return env < 0 ? d2h(h, dst, h->sv, h->BN * 6 * 4) : d2h(h, dst, h->sv + env * n, n * 4);
+}
+
+int fe_get_network(fe_handle* h, int env, float* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (int rc = use_dev(h)) return rc;
+  const size_t n = (size_t)h->cfg.n_agents * h->cfg.n_agents;
+  return env < 0 ? d2h(h, dst, h->net, h->BN * h->cfg.n_agents * 4) : d2h(h, dst, h->net + env * n, n * 4);
+}
+
+int fe_get_network_rows(fe_handle* h, int env, int row0, int nrows, float* dst) {
+  if (!h || !dst || env < 0 || row0 < 0 || nrows < 0 || row0 + nrows > h->cfg.n_agents)
+    return fail(GF_EINVAL, "bad argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (int rc = use_dev(h)) return rc;
+  const size_t N = h->cfg.n_agents;
+  return d2h(h, dst, h->net + (env * N + row0) * N, (size_t)nrows * N * 4);
+}
+
+int fe_get_controls(fe_handle* h, int env, double* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_ctrl) return fail(GF_ESTATE, "no controller output");
+  if (int rc = use_dev(h)) return rc;
+  const size_t n = (size_t)h->cfg.n_agents * 2;
+  const double* src = h->ctrl[h->ccur];
+  return env < 0 ? d2h(h, dst, src, h->BN * 2 * 8) : d2h(h, dst, src + env * n, n * 8);
+}
+
+int fe_get_rewards(fe_handle* h, double* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (!h->has_obs) return fail(GF_ESTATE, "no step computed yet");
+  if (int rc = use_dev(h)) return rc;
+  return d2h(h, dst, cur_reward(h), (size_t)h->cfg.n_envs * 8);
+}
+
+int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (int rc = check_env(h, env)) return rc;
+  if (h->cfg.n_neighbors <= 0) return fail(GF_EINVAL, "handle created with n_neighbors = 0");
+  if (int rc = use_dev(h)) return rc;
+  if (!h->has_knn) {
+    if (!h->has_state) return fail(GF_ESTATE, "state not set");
+    if (int rc = launch_knn_cur(h)) return rc;
+  }
+  const size_t K = h->cfg.n_neighbors, N = h->cfg.n_agents;
+  const size_t off = env < 0 ? 0 : env * N;
+  const size_t cnt = env < 0 ? h->BN : N;
+  if (idx) GF_HIP(hipMemcpyAsync(idx, h->knn_idx + off * K, cnt * K * 4, hipMemcpyDeviceToHost, h->stream));
+  if (obs) GF_HIP(hipMemcpyAsync(obs, h->knn_obs + off * 4 * K, cnt * 4 * K * 4, hipMemcpyDeviceToHost, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int fe_device_buffers(fe_handle* h, fe_buffers* out) {
+  if (!h || !out) return fail(GF_EINVAL, "null argument");
+  out->x = h->x[h->cur];
+  out->state_values = h->sv;
+  out->network = h->net;
+  out->controls = h->ctrl[h->ccur];
+  out->rewards = cur_reward(h);
+  out->knn_idx = h->knn_idx;
+  out->knn_obs = h->knn_obs;
+  out->stream = h->stream;
+  return GF_OK;
+}
+
+int fe_sync(fe_handle* h) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (int rc = use_dev(h)) return rc;
+  GF_HIP(hipStreamSynchronize(h->stream));
+  if (h->comm_stream) GF_HIP(hipStreamSynchronize(h->comm_stream));
+  return GF_OK;
+}
+
+int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (int rc = use_dev(h)) return rc;
+  if (enable == 1) {
+    GF_HIP(hipStreamSynchronize(h->stream));
+    h->ev_used = 0;
+    h->timing = true;
+    return GF_OK;
+  }
+  GF_HIP(hipStreamSynchronize(h->stream));
+  double tot = 0;
+  for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
+    float ms = 0;
+    GF_HIP(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
+    tot += ms;
+  }
+  const int64_t n = (int64_t)(h->ev_used / 2);
+  if (avg_ms) *avg_ms = n ? tot / n : 0.0;
+  if (launches) *launches = n;
+  if (enable == 0) h->timing = false;
+  return GF_OK;
+}
+
+// ------------------------------------------------------------------ RCCL metrics path
+int fe_comm_unique_id(uint8_t id[128]) {
+  if (!id) return fail(GF_EINVAL, "null argument");
+  ncclUniqueId uid;
+  ncclResult_t r = ncclGetUniqueId(&uid);
+  if (r != ncclSuccess) return fail(GF_ECOMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  static_assert(sizeof(uid) == 128, "ncclUniqueId size");
+  std::memcpy(id, &uid, 128);
+  return GF_OK;
+}
+
+int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
+  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(GF_EINVAL, "bad argument");
+  if (h->comm) return fail(GF_ESTATE, "communicator already initialised");
+  if (int rc = use_dev(h)) return rc;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  ncclResult_t r = ncclCommInitRank(&h->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    h->comm = nullptr;
+    return fail(GF_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  h->nranks = nranks;
+  h->rank = rank;
+  GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
+  GF_HIP(hipEventCreateWithFlags(&h->step_ev, hipEventDisableTiming));
+  for (auto& e : h->ag_ev) GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (int rc = dalloc(&h->gather, (size_t)kRewardSlots * nranks * h->cfg.n_envs)) return rc;
+  return GF_OK;
+}
+
+int fe_allgather_rewards(fe_handle* h) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->comm) return fail(GF_ESTATE, "fe_comm_init not called");
+  if (int rc = use_dev(h)) return rc;
+  const int s = h->rslot;
+  const size_t B = h->cfg.n_envs;
+  GF_HIP(hipEventRecord(h->step_ev, h->stream));
+  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
+  ncclResult_t r = ncclAllGather(cur_reward(h), h->gather + (size_t)s * h->nranks * B, B, ncclFloat64, h->comm,
+                                 h->comm_stream);
+  if (r != ncclSuccess) return fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  GF_HIP(hipEventRecord(h->ag_ev[s], h->comm_stream));
+  h->ag_pending[s] = true;
+  h->last_gather = s;
+  return GF_OK;
+}
+
+int fe_get_gathered_rewards(fe_handle* h, double* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (h->last_gather < 0) return fail(GF_ESTATE, "no all-gather issued");
+  if (int rc = use_dev(h)) return rc;
+  const size_t n = (size_t)h->nranks * h->cfg.n_envs;
+  GF_HIP(hipEventSynchronize(h->ag_ev[h->last_gather]));
+  GF_HIP(hipMemcpy(dst, h->gather + (size_t)h->last_gather * n, n * 8, hipMemcpyDeviceToHost));
+  return GF_OK;
+}
+
+int fe_comm_destroy(fe_handle* h) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (h->comm) {
+    if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
+    ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+  }
+  return GF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// Internal interface between the C-ABI (capi.hip) and the kernels (flock_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gf {
+
+constexpr int kThreads = 256;   // 4 wave64s per workgroup
+constexpr int kTileMax = 1024;  // agents staged per LDS tile (32 KiB of float64 state)
+
+// One batched hot-path launch. Pointers are device pointers; all per-env arrays
+// are [B][N][...] contiguous.
+struct StepArgs {
+  const double* x_in;     // (B,N,4) state before the step
+  double* x_out;          // (B,N,4) state after the step (DYN only)
+  const void* u;          // (B,N,2) float or double actions (DYN only)
+  float* state_values;    // (B,N,6) or nullptr
+  float* network;         // (B,N,N) or nullptr
+  double* ctrl_out;       // (B,N,2) or nullptr (CTRL only)
+  double* reward;         // (B) or nullptr
+  double dt, action_scalar, cr, cr2;
+  float dt_f, as_f;
+  int N, B;
+  int R;                  // rows per workgroup (power of two, 4..64)
+  int T;                  // agents per LDS tile (multiple of 64)
+  int bpe;                // workgroups per env = ceil(N / R)
+  int mean_pooling, centralized;
+};
+
+struct KnnArgs {
+  const double* x;        // (B,N,4) current state
+  int32_t* idx;           // (B,N,K)
+  float* obs;             // (B,N,4K)
+  int N, B, K;
+};
+
+struct StatsArgs {
+  const double* x;        // (B,N,4)
+  double* vel_diffs;      // (B,N)
+  double* min_dists;      // (B,N)
+  int32_t* degree;        // (B,N) neighbours with r2 < comm_radius^2
+  double cr2;
+  int N, B;
+};
+
+// Launch-geometry helpers shared by host and tests.
+int step_rows_per_block(int N);
+int step_tile(int N);
+size_t step_lds_bytes(int N, int R, int T, bool ctrl);
+
+hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
+hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
+
+}  // namespace gf

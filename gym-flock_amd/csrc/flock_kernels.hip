@@ -1,0 +1,492 @@
+// HIP kernels (gfx950 / CDNA4) for gym-flock's FlockingRelative-v0 / Flocking-v0 step.
+//
+// Reference (paths relative to the reference root):
+//   gym_flock/envs/flocking/flocking_relative.py  step :91-109, compute_helpers :111-134,
+//     get_stats :136-143, instant_cost :145-147, controller/potential_grad :194-226
+//   gym_flock/envs/flocking/flocking.py            get_observation :20-25 (k nearest)
+//
+// The reference materialises several (N,N,{4,6}) float64 temporaries per step. Here
+// one launch does the whole step for B envs: each 256-thread workgroup owns R rows
+// (agents i) of one env, stages the env's agents through LDS in tiles of up to 1024,
+// and produces
+//   - adjacency bits for its rows (wave64 ballots of r2 < comm_radius^2) kept in LDS,
+//   - the neighbour features / controller gradients, evaluated only for the pairs
+//     whose bit is set (lane per (row, word-slice), iterating set bits),
+//   - the dense mean-pooled (N,N) network rows as 16-byte coalesced stores.
+// The dense network write (4*N^2 bytes per env) is the roofline: the kernel is HBM
+// write bound, not MFMA work.
+//
+// Numerics: the pair path is float64 with -ffp-contract=off so every r2 is the
+// reference's bit pattern (dx*dx + dy*dy, two roundings then a sum); adjacency is
+// therefore bit-exact, and features differ from NumPy only by summation order.
+#include "flock_internal.h"
+
+#include <float.h>
+#include <limits.h>
+
+namespace gf {
+
+namespace {
+
+struct __attribute__((aligned(16))) St {
+  double px, py, vx, vy;
+};
+
+// Workgroup -> (env, row block) with all row blocks of an env on one XCD
+// (blocks b and b+8 share an XCD under round-robin dispatch; speed only).
+__device__ __forceinline__ int xcd_remap(int bid, int G) {
+  const int xcd = bid & 7, q = G >> 3, r = G & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Deterministic workgroup sum: butterfly inside each wave, then the 4 wave totals in
+// a fixed tree. Every thread returns the same bits.
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// State of agent `g` (flat index b*N + j) after the double-integrator update of
+// flocking_relative.py:96-105, in the reference's operation order. With a float32 u
+// the action terms are float32 arithmetic (NumPy keeps u*10.0, *dt, *0.5 in float32)
+// and are widened when added to the float64 state.
+template <bool DYN, bool UF64>
+__device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
+  const double2* xp = reinterpret_cast<const double2*>(a.x_in) + 2 * g;
+  const double2 p = xp[0], v = xp[1];
+  St s{p.x, p.y, v.x, v.y};
+  if constexpr (DYN) {
+    if constexpr (UF64) {
+      const double2 u = reinterpret_cast<const double2*>(a.u)[g];
+      const double ux = u.x * a.action_scalar, uy = u.y * a.action_scalar;
+      s.px = (p.x + v.x * a.dt) + ((ux * a.dt) * a.dt) * 0.5;
+      s.py = (p.y + v.y * a.dt) + ((uy * a.dt) * a.dt) * 0.5;
+      s.vx = v.x + ux * a.dt;
+      s.vy = v.y + uy * a.dt;
+    } else {
+      const float2 u = reinterpret_cast<const float2*>(a.u)[g];
+      const float ux = u.x * a.as_f, uy = u.y * a.as_f;
+      const float apx = ((ux * a.dt_f) * a.dt_f) * 0.5f;
+      const float apy = ((uy * a.dt_f) * a.dt_f) * 0.5f;
+      s.px = (p.x + v.x * a.dt) + static_cast<double>(apx);
+      s.py = (p.y + v.y * a.dt) + static_cast<double>(apy);
+      s.vx = v.x + static_cast<double>(ux * a.dt_f);
+      s.vy = v.y + static_cast<double>(uy * a.dt_f);
+    }
+  }
+  return s;
+}
+
+__device__ __forceinline__ double clip10(double v) {  // np.clip(v, -10, 10); NaN stays NaN
+  return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v);
+}
+
+// ---------------------------------------------------------------------------------
+// The fused step: DYN = apply dynamics (step) or not (compute_helpers on the current
+// state: reset / standalone controller), UF64 = action dtype, CTRL = also controller().
+template <bool DYN, bool UF64, bool CTRL>
+__global__ __launch_bounds__(kThreads) void flock_step_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, R = a.R, T = a.T;
+  const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
+  const int Wt = T >> 6;         // words per row of one tile
+  St* tile = reinterpret_cast<St*>(smem);
+  St* rows = tile + T;
+  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);
+  uint64_t* nearb = adj + (size_t)R * Wn;
+  double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)R * Wt : 0));
+  float* inv = reinterpret_cast<float*>(red + 8);
+
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = L / a.bpe;
+  const int i0 = (L - b * a.bpe) * R;
+  const int nrows = min(R, N - i0);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const size_t env0 = (size_t)b * N;
+
+  // rows owned by this workgroup (post-update state)
+  for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64>(a, env0 + i0 + r);
+
+  // feature-pass thread mapping: S word-slices per row
+  const int S = kThreads / R;
+  const int fr = tid / S, fs = tid - fr * S;
+  const bool frow = fr < nrows;
+  double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
+  double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
+  St me{0, 0, 0, 0};
+
+  for (int j0 = 0; j0 < N; j0 += T) {
+    const int tc = min(T, N - j0);
+    __syncthreads();  // previous tile fully consumed; rows[] visible on first pass
+    for (int t = tid; t < tc; t += kThreads) {
+      const St s = load_state<DYN, UF64>(a, env0 + j0 + t);
+      tile[t] = s;
+      svx += s.vx;
+      svy += s.vy;
+    }
+    if (j0 == 0 && frow) me = rows[fr];
+    __syncthreads();
+
+    // pass 1: adjacency (and controller "near") bits, lane = column j, loop over rows
+    const int nch = (tc + 63) >> 6;
+    for (int c = wid; c < nch; c += 4) {
+      const int jt = (c << 6) + lane;
+      const int j = j0 + jt;
+      const bool vj = jt < tc;
+      const St o = vj ? tile[jt] : St{0, 0, 0, 0};
+      uint64_t* arow = adj + (j0 >> 6) + c;
+      uint64_t* nrow = nearb + c;
+
+      for (int r = 0; r < nrows; ++r) {
+        const double dx = rows[r].px - o.px;
+        const double dy = rows[r].py - o.py;
+        const double r2 = dx * dx + dy * dy;
+        const bool ok = vj && (j != i0 + r);
+        const uint64_t am = __ballot(ok && r2 < a.cr2);
+        if (lane == 0) arow[(size_t)r * Wn] = am;
+        if constexpr (CTRL) {
+          const uint64_t nm = __ballot(ok && r2 <= a.cr);
+          if (lane == 0) nrow[(size_t)r * Wt] = nm;
+        }
+      }
+    }
+    __syncthreads();
+
+    // pass 2: features / gradients for set bits only, ascending j per slice
+    if (frow) {
+      const int wpt = (nch + S - 1) / S;
+      const int wb = fs * wpt, we = min(nch, wb + wpt);
+      for (int w = wb; w < we; ++w) {
+        const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
+        const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
+        uint64_t m = am | nm;
+        while (m) {
+          const int k = __builtin_ctzll(m);
+          m &= m - 1;
+          const St o = tile[(w << 6) + k];
+          const double dx = me.px - o.px, dy = me.py - o.py;
+          const double r2 = dx * dx + dy * dy;
+          const double rr = r2 * r2;
+          const double q1x = dx / rr, q2x = dx / r2;
+          const double q1y = dy / rr, q2y = dy / r2;
+          const bool isadj = (am >> k) & 1ull;
+          if (isadj) {
+            f0 += me.vx - o.vx;
+            f1 += q1x;
+            f2 += q2x;
+            f3 += me.vy - o.vy;
+            f4 += q1y;
+            f5 += q2y;
+          }
+          if constexpr (CTRL) {
+            const bool isnear = (nm >> k) & 1ull;
+            if (isnear && (a.centralized || isadj)) {
+              gx += (-2.0 * q1x) + (2.0 * q2x);
+              gy += (-2.0 * q1y) + (2.0 * q2y);
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // combine the S slices of each row (xor butterfly: identical bits in every lane)
+  for (int o = 1; o < S; o <<= 1) {
+    f0 += __shfl_xor(f0, o);
+    f1 += __shfl_xor(f1, o);
+    f2 += __shfl_xor(f2, o);
+    f3 += __shfl_xor(f3, o);
+    f4 += __shfl_xor(f4, o);
+    f5 += __shfl_xor(f5, o);
+    if constexpr (CTRL) {
+      gx += __shfl_xor(gx, o);
+      gy += __shfl_xor(gy, o);
+    }
+  }
+  int deg = 0;
+  if (frow) {
+    const int wpt = (Wn + S - 1) / S;
+    const int wb = fs * wpt, we = min(Wn, wb + wpt);
+    for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
+  }
+  for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
+
+  const double Svx = block_sum(svx, red);
+  const double Svy = block_sum(svy, red);
+
+  if (frow && fs == 0) {
+    const int i = i0 + fr;
+    const size_t g = env0 + i;
+    inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg))
+                             : 1.0f;
+    if (a.state_values) {
+      float* sv = a.state_values + g * 6;
+      sv[0] = static_cast<float>(f0);
+      sv[1] = static_cast<float>(f1);
+      sv[2] = static_cast<float>(f2);
+      sv[3] = static_cast<float>(f3);
+      sv[4] = static_cast<float>(f4);
+      sv[5] = static_cast<float>(f5);
+    }
+    if constexpr (DYN) {
+      double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
+      xo[0] = double2{me.px, me.py};
+      xo[1] = double2{me.vx, me.vy};
+    }
+    if constexpr (CTRL) {
+      // centralized: sum over ALL j of (v_i - v_j) = N*v_i - sum_j v_j (:200-208)
+      const double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
+      const double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
+      double2 u;
+      u.x = clip10(-gx - p2) / a.action_scalar;  // (-p4 - p2), :209-211
+      u.y = clip10(-p3 - gy) / a.action_scalar;  // (-p3 - p5)
+      reinterpret_cast<double2*>(a.ctrl_out)[g] = u;
+    }
+  }
+
+  // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the
+  // env's first row block only
+  if (a.reward && i0 == 0) {
+    const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
+    double qx = 0, qy = 0;
+    for (int j0 = 0; j0 < N; j0 += T) {
+      const int tc = min(T, N - j0);
+      for (int t = tid; t < tc; t += kThreads) {
+        const St s = load_state<DYN, UF64>(a, env0 + j0 + t);
+        const double ex = s.vx - mx, ey = s.vy - my;
+        qx += ex * ex;
+        qy += ey * ey;
+      }
+    }
+    const double Qx = block_sum(qx, red);
+    const double Qy = block_sum(qy, red);
+    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
+  }
+
+  // pass 3: dense network rows, adj/deg as 16-byte stores (1 KiB per wave instruction)
+  if (a.network) {
+    __syncthreads();
+    const bool vec4 = (N & 3) == 0;
+    for (int r = wid; r < nrows; r += 4) {
+      const float iv = inv[r];
+      const uint64_t* bits = adj + (size_t)r * Wn;
+      float* rowp = a.network + (env0 + i0 + r) * (size_t)N;
+      if (vec4) {
+        float4* r4 = reinterpret_cast<float4*>(rowp);
+        const int nq = N >> 2;
+        for (int q = lane; q < nq; q += 64) {
+          const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
+          float4 v;
+          v.x = (nib & 1u) ? iv : 0.0f;
+          v.y = (nib & 2u) ? iv : 0.0f;
+          v.z = (nib & 4u) ? iv : 0.0f;
+          v.w = (nib & 8u) ? iv : 0.0f;
+          r4[q] = v;
+        }
+      } else {
+        for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Flocking-v0 observation (flocking.py:20-25): the K smallest r2 per row, ties to the
+// lower index (the reference's argsort is unstable), self has r2=inf.
+// One thread per row keeps a sorted (r2, j) list in registers; the env's positions
+// stream through LDS and are read as wave-uniform broadcasts.
+template <int K>
+__global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
+  __shared__ double2 tile[kTileMax];
+  const int N = a.N;
+  const int bpe = (N + kThreads - 1) / kThreads;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = L / bpe;
+  const int i = (L - b * bpe) * kThreads + threadIdx.x;
+  const bool vi = i < N;
+  const double* xb = a.x + (size_t)b * N * 4;
+  double pxi = 0, pyi = 0;
+  if (vi) {
+    pxi = xb[4 * (size_t)i];
+    pyi = xb[4 * (size_t)i + 1];
+  }
+  double kr[K];
+  int kj[K];
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    kr[m] = __builtin_inf();
+    kj[m] = INT_MAX;
+  }
+  for (int j0 = 0; j0 < N; j0 += kTileMax) {
+    const int tc = min(kTileMax, N - j0);
+    __syncthreads();
+    for (int t = threadIdx.x; t < tc; t += kThreads)
+      tile[t] = reinterpret_cast<const double2*>(xb)[2 * (size_t)(j0 + t)];
+    __syncthreads();
+    if (vi) {
+      for (int t = 0; t < tc; ++t) {
+        const int j = j0 + t;
+        const double2 p = tile[t];
+        const double dx = pxi - p.x, dy = pyi - p.y;
+        const double r2 = (j == i) ? __builtin_inf() : dx * dx + dy * dy;
+        if (r2 < kr[K - 1] || (r2 == kr[K - 1] && j < kj[K - 1])) {
+          double cr = r2;
+          int cj = j;
+#pragma unroll
+          for (int m = 0; m < K; ++m) {
+            const bool sw = (cr < kr[m]) || (cr == kr[m] && cj < kj[m]);
+            const double tr = sw ? kr[m] : cr;
+            const int tj = sw ? kj[m] : cj;
+            kr[m] = sw ? cr : kr[m];
+            kj[m] = sw ? cj : kj[m];
+            cr = tr;
+            cj = tj;
+          }
+        }
+      }
+    }
+  }
+  if (!vi) return;
+  const size_t g = (size_t)b * N + i;
+  const double2* xi = reinterpret_cast<const double2*>(xb) + 2 * (size_t)i;
+  const double2 pi = xi[0], vv = xi[1];
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    const int j = kj[m];
+    a.idx[g * K + m] = j;
+    const double2* xj = reinterpret_cast<const double2*>(xb) + 2 * (size_t)j;
+    const double2 pj = xj[0], vj = xj[1];
+    float4 o;
+    o.x = static_cast<float>(pi.x - pj.x);
+    o.y = static_cast<float>(pi.y - pj.y);
+    o.z = static_cast<float>(vv.x - vj.x);
+    o.w = static_cast<float>(vv.y - vj.y);
+    reinterpret_cast<float4*>(a.obs + g * 4 * K)[m] = o;
+  }
+}
+
+// get_stats (:136-143): vel_diffs_i = |v_i - mean v|, min_dists_i = sqrt(min_j r2_ij)
+// (r2 is exactly symmetric, so the reference's column min equals this row min), plus
+// the degree used by reset()'s acceptance test (:177-184).
+__global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
+  __shared__ St tile[kTileMax];
+  __shared__ double red[8];
+  const int N = a.N;
+  const int bpe = (N + kThreads - 1) / kThreads;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = L / bpe;
+  const int i = (L - b * bpe) * kThreads + threadIdx.x;
+  const bool vi = i < N;
+  const St* xb = reinterpret_cast<const St*>(a.x + (size_t)b * N * 4);
+  St me{0, 0, 0, 0};
+  if (vi) me = xb[i];
+  double mn = __builtin_inf(), sx = 0, sy = 0;
+  int deg = 0;
+  for (int j0 = 0; j0 < N; j0 += kTileMax) {
+    const int tc = min(kTileMax, N - j0);
+    __syncthreads();
+    for (int t = threadIdx.x; t < tc; t += kThreads) {
+      const St s = xb[j0 + t];
+      tile[t] = s;
+      sx += s.vx;
+      sy += s.vy;
+    }
+    __syncthreads();
+    if (vi) {
+      for (int t = 0; t < tc; ++t) {
+        const double dx = me.px - tile[t].px, dy = me.py - tile[t].py;
+        const double r2 = dx * dx + dy * dy;
+        const bool other = j0 + t != i;
+        if (other && r2 < mn) mn = r2;
+        deg += (other && r2 < a.cr2) ? 1 : 0;
+      }
+    }
+  }
+  const double mx = block_sum(sx, red) / static_cast<double>(N);
+  const double my = block_sum(sy, red) / static_cast<double>(N);
+  if (!vi) return;
+  const size_t g = (size_t)b * N + i;
+  const double ex = me.vx - mx, ey = me.vy - my;
+  a.vel_diffs[g] = sqrt(ex * ex + ey * ey);
+  a.min_dists[g] = sqrt(mn);
+  a.degree[g] = deg;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------- host
+int step_rows_per_block(int N) {
+  const int words = (N + 63) / 64;
+  int R = 64;
+  while (R > 4 && (size_t)R * words * 8 > 16384) R >>= 1;  // adjacency bits <= 16 KiB
+  while (R > 4 && R / 2 >= N) R >>= 1;
+  return R;
+}
+
+int step_tile(int N) {
+  const int t = ((N + 63) / 64) * 64;
+  return t < kTileMax ? t : kTileMax;
+}
+
+size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
+  const size_t Wn = (N + 63) / 64, Wt = T / 64;
+  size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
+  s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0);
+  s += 8 * sizeof(double) + (((size_t)R * 4 + 15) / 16) * 16;
+  return s;
+}
+
+template <bool DYN, bool UF64, bool CTRL>
+static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
+  const size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int grid = a.B * a.bpe;
+  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL>), dim3(grid), dim3(kThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s) {
+  if (dyn) {
+    if (u_f64) return ctrl ? launch_step_t<true, true, true>(a, s) : launch_step_t<true, true, false>(a, s);
+    return ctrl ? launch_step_t<true, false, true>(a, s) : launch_step_t<true, false, false>(a, s);
+  }
+  return ctrl ? launch_step_t<false, false, true>(a, s) : launch_step_t<false, false, false>(a, s);
+}
+
+hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
+  const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
+  switch (a.K) {
+#define GF_KNN_CASE(k) \
+  case k: hipLaunchKernelGGL(flock_knn_kernel<k>, dim3(grid), dim3(kThreads), 0, s, a); break;
+    GF_KNN_CASE(1) GF_KNN_CASE(2) GF_KNN_CASE(3) GF_KNN_CASE(4) GF_KNN_CASE(5) GF_KNN_CASE(6)
+    GF_KNN_CASE(7) GF_KNN_CASE(8) GF_KNN_CASE(10) GF_KNN_CASE(12) GF_KNN_CASE(16)
+#undef GF_KNN_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
+  const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(flock_stats_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gf

@@ -1,0 +1,279 @@
+"""ctypes binding of libgymflock.so (include/gymflock.h).
+
+No PyTorch here: the env talks to the HIP kernels through this thin C-ABI only.
+The library is built in-tree (gym-flock_amd/lib/libgymflock.so, see
+__graft_entry__.build()); if it is missing or no GPU is present, every call that
+needs it raises — there is no CPU fallback in the product path.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "GYMFLOCK_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libgymflock.so"))
+
+GF_OK, GF_EINVAL, GF_EHIP, GF_ENOMEM, GF_ESTATE, GF_ECOMM = range(6)
+
+FE_WITH_CONTROLLER = 0x01
+FE_U_DEVICE = 0x02
+FE_U_F64 = 0x04
+FE_U_EXPERT = 0x08
+FE_WITH_KNN = 0x10
+FE_NO_NETWORK = 0x20
+FE_NO_STATE_VALUES = 0x40
+FE_U_RESIDENT = 0x80
+
+
+class FeConfig(ctypes.Structure):
+    _fields_ = [("n_agents", ctypes.c_int32), ("n_envs", ctypes.c_int32),
+                ("comm_radius", ctypes.c_double), ("dt", ctypes.c_double),
+                ("action_scalar", ctypes.c_double), ("mean_pooling", ctypes.c_int32),
+                ("centralized", ctypes.c_int32), ("n_neighbors", ctypes.c_int32),
+                ("device", ctypes.c_int32)]
+
+
+class FeBuffers(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("state_values", ctypes.c_void_p),
+                ("network", ctypes.c_void_p), ("controls", ctypes.c_void_p),
+                ("rewards", ctypes.c_void_p), ("knn_idx", ctypes.c_void_p),
+                ("knn_obs", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
+class GymFlockError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libgymflock error %d: %s" % (code, msg))
+        self.code = code
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+# name -> argtypes (every function returns int unless listed in _RESTYPE)
+SIGNATURES = {
+    "fe_create": [ctypes.POINTER(FeConfig), ctypes.POINTER(_P)],
+    "fe_destroy": [_P],
+    "fe_get_config": [_P, ctypes.POINTER(FeConfig)],
+    "fe_set_state": [_P, _P],
+    "fe_set_state_env": [_P, _I, _P],
+    "fe_get_state": [_P, _P],
+    "fe_get_state_env": [_P, _I, _P],
+    "fe_set_actions": [_P, _P, _I],
+    "fe_compute_helpers": [_P, _I],
+    "fe_step": [_P, _P, _I],
+    "fe_controller": [_P, _I, _P],
+    "fe_get_stats": [_P, _I, _P, _P],
+    "fe_get_stats_ex": [_P, _I, _P, _P, _P],
+    "fe_get_state_values": [_P, _I, _P],
+    "fe_get_network": [_P, _I, _P],
+    "fe_get_network_rows": [_P, _I, _I, _I, _P],
+    "fe_get_controls": [_P, _I, _P],
+    "fe_get_rewards": [_P, _P],
+    "fe_get_knn": [_P, _I, _P, _P],
+    "fe_device_buffers": [_P, ctypes.POINTER(FeBuffers)],
+    "fe_sync": [_P],
+    "fe_comm_unique_id": [_P],
+    "fe_comm_init": [_P, _I, _I, _P],
+    "fe_allgather_rewards": [_P],
+    "fe_get_gathered_rewards": [_P, _P],
+    "fe_comm_destroy": [_P],
+    "fe_last_error": [],
+    "fe_abi_version": [],
+    "fe_kernel_timing": [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
+}
+_RESTYPE = {"fe_last_error": ctypes.c_char_p}
+
+_lib = None
+
+
+def load(path=None):
+    """Load (once) and return the ctypes library; raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError("libgymflock.so not found at %s: build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(or make -C gym-flock_amd/csrc)" % p)
+    lib = ctypes.CDLL(p)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != GF_OK:
+        raise GymFlockError(rc, load().fe_last_error().decode(errors="replace"))
+
+
+def ptr(a):
+    """Pointer to a C-contiguous numpy array (None passes NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class FlockHandle:
+    """Owns one fe_handle: B envs x N agents of FlockingRelative on one GPU."""
+
+    def __init__(self, n_agents, n_envs=1, comm_radius=0.9, dt=0.01, action_scalar=10.0,
+                 mean_pooling=True, centralized=True, n_neighbors=0, device=0):
+        self.lib = load()
+        self.cfg = FeConfig(int(n_agents), int(n_envs), float(comm_radius), float(dt),
+                            float(action_scalar), int(bool(mean_pooling)), int(bool(centralized)),
+                            int(n_neighbors), int(device))
+        self.n_agents, self.n_envs, self.n_neighbors = int(n_agents), int(n_envs), int(n_neighbors)
+        h = ctypes.c_void_p()
+        check(self.lib.fe_create(ctypes.byref(self.cfg), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fe_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    # -- state
+    def set_state(self, x, env=None):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if env is None:
+            assert x.shape == (self.n_envs, self.n_agents, 4), x.shape
+            check(self.lib.fe_set_state(self.h, ptr(x)))
+        else:
+            assert x.shape == (self.n_agents, 4), x.shape
+            check(self.lib.fe_set_state_env(self.h, int(env), ptr(x)))
+
+    def get_state(self, env=None):
+        if env is None:
+            x = np.empty((self.n_envs, self.n_agents, 4))
+            check(self.lib.fe_get_state(self.h, ptr(x)))
+        else:
+            x = np.empty((self.n_agents, 4))
+            check(self.lib.fe_get_state_env(self.h, int(env), ptr(x)))
+        return x
+
+    # -- hot path
+    def compute_helpers(self, flags=0):
+        check(self.lib.fe_compute_helpers(self.h, int(flags)))
+
+    def set_actions(self, u):
+        """Upload (B,N,2) actions to the resident buffer used by FE_U_RESIDENT."""
+        u = np.asarray(u)
+        f64 = u.dtype == np.float64
+        u = np.ascontiguousarray(u, dtype=np.float64 if f64 else np.float32)
+        assert u.shape == (self.n_envs, self.n_agents, 2), u.shape
+        check(self.lib.fe_set_actions(self.h, ptr(u), int(f64)))
+
+    def step(self, u=None, flags=0):
+        """u: host ndarray (B,N,2) float32/float64, or a device pointer (int) with
+        FE_U_DEVICE, or None with FE_U_EXPERT / FE_U_RESIDENT."""
+        if flags & (FE_U_EXPERT | FE_U_RESIDENT):
+            check(self.lib.fe_step(self.h, None, int(flags)))
+        elif flags & FE_U_DEVICE:
+            check(self.lib.fe_step(self.h, ctypes.c_void_p(int(u)), int(flags)))
+        else:
+            u = np.asarray(u)
+            if u.dtype == np.float64:
+                flags |= FE_U_F64
+            else:
+                u = u.astype(np.float32, copy=False)
+                flags &= ~FE_U_F64
+            u = np.ascontiguousarray(u)
+            assert u.shape == (self.n_envs, self.n_agents, 2), u.shape
+            check(self.lib.fe_step(self.h, ptr(u), int(flags)))
+
+    def controller(self, centralized=None):
+        out = np.empty((self.n_envs, self.n_agents, 2))
+        c = -1 if centralized is None else int(bool(centralized))
+        check(self.lib.fe_controller(self.h, c, ptr(out)))
+        return out
+
+    def stats(self, env=0):
+        """(vel_diffs, min_dists, degree) of one env's current state."""
+        vd = np.empty(self.n_agents)
+        md = np.empty(self.n_agents)
+        deg = np.empty(self.n_agents, np.int32)
+        check(self.lib.fe_get_stats_ex(self.h, int(env), ptr(vd), ptr(md), ptr(deg)))
+        return vd, md, deg
+
+    # -- outputs
+    def state_values(self, env=None):
+        shape = (self.n_envs, self.n_agents, 6) if env is None else (self.n_agents, 6)
+        out = np.empty(shape, np.float32)
+        check(self.lib.fe_get_state_values(self.h, -1 if env is None else int(env), ptr(out)))
+        return out
+
+    def network(self, env=None):
+        n = self.n_agents
+        shape = (self.n_envs, n, n) if env is None else (n, n)
+        out = np.empty(shape, np.float32)
+        check(self.lib.fe_get_network(self.h, -1 if env is None else int(env), ptr(out)))
+        return out
+
+    def network_rows(self, env, row0, nrows):
+        out = np.empty((nrows, self.n_agents), np.float32)
+        check(self.lib.fe_get_network_rows(self.h, int(env), int(row0), int(nrows), ptr(out)))
+        return out
+
+    def controls(self, env=None):
+        shape = (self.n_envs, self.n_agents, 2) if env is None else (self.n_agents, 2)
+        out = np.empty(shape)
+        check(self.lib.fe_get_controls(self.h, -1 if env is None else int(env), ptr(out)))
+        return out
+
+    def rewards(self):
+        out = np.empty(self.n_envs)
+        check(self.lib.fe_get_rewards(self.h, ptr(out)))
+        return out
+
+    def knn(self, env=None):
+        k, n = self.n_neighbors, self.n_agents
+        lead = (self.n_envs, n) if env is None else (n,)
+        idx = np.empty(lead + (k,), np.int32)
+        obs = np.empty(lead + (4 * k,), np.float32)
+        check(self.lib.fe_get_knn(self.h, -1 if env is None else int(env), ptr(idx), ptr(obs)))
+        return idx, obs
+
+    def device_buffers(self):
+        b = FeBuffers()
+        check(self.lib.fe_device_buffers(self.h, ctypes.byref(b)))
+        return b
+
+    def sync(self):
+        check(self.lib.fe_sync(self.h))
+
+    # -- timing (bench)
+    def timing_start(self):
+        check(self.lib.fe_kernel_timing(self.h, 1, None, None))
+
+    def timing_stop(self):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        check(self.lib.fe_kernel_timing(self.h, 0, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    # -- RCCL metrics path
+    @staticmethod
+    def comm_unique_id():
+        buf = (ctypes.c_uint8 * 128)()
+        check(load().fe_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self.lib.fe_comm_init(self.h, int(nranks), int(rank), ctypes.cast(buf, ctypes.c_void_p)))
+        self.nranks = int(nranks)
+
+    def allgather_rewards(self):
+        check(self.lib.fe_allgather_rewards(self.h))
+
+    def gathered_rewards(self):
+        out = np.empty(self.nranks * self.n_envs)
+        check(self.lib.fe_get_gathered_rewards(self.h, ptr(out)))
+        return out

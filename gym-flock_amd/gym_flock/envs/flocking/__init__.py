@@ -1,0 +1,5 @@
+"""Flocking envs (reference: gym_flock/envs/flocking/__init__.py)."""
+from gym_flock.envs.flocking.flocking_relative import FlockingRelativeEnv
+from gym_flock.envs.flocking.flocking import FlockingEnv
+
+__all__ = ["FlockingRelativeEnv", "FlockingEnv"]

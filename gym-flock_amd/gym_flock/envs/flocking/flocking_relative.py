@@ -1,0 +1,209 @@
+"""FlockingRelative-v0 on the MI355X engine — drop-in for
+gym_flock/envs/flocking/flocking_relative.py of the reference.
+
+Same class name, attributes and method signatures as the reference
+(`__init__` :20-66, `params_from_cfg` :68-85, `seed` :87-89, `step` :91-109,
+`compute_helpers` :111-134, `get_stats` :136-143, `instant_cost` :145-147,
+`reset` :156-192, `controller` :194-212, `render` :234-257, `close` :303). Every
+per-step array computation runs in the HIP kernels of libgymflock.so through the
+C-ABI (gym_flock._native); nothing here computes pairwise quantities on the host.
+
+Differences a caller can observe:
+  - observations are float32 (the reference's observation_space dtype, :59-60); the
+    reference returns float64 arrays.
+  - `x` is a property backed by device memory: assigning `env.x = arr` uploads,
+    reading returns a float64 copy (in-place edits of that copy do not propagate).
+  - `diff` / `r2` (N,N,4)/(N,N) are not materialised; `adj_mat` is derived from
+    the network.
+  - reset() runs the reference's rejection sampler (same global-RNG call order, so
+    seeded runs reproduce the reference bit for bit) up to `reset_max_attempts`
+    draws, then falls back to a single draw (the reference would loop forever,
+    SURVEY.md finding 5); `reset_mode='synthetic'` skips the rejection.
+"""
+import numpy as np
+
+from ... import _native as nat
+from ..._spaces import Box, Env, np_random
+from ...init_states import draw_swarm
+
+
+class FlockingRelativeEnv(Env):
+
+    def __init__(self, device=0):
+        self.mean_pooling = True  # :27
+        self.centralized = True   # :28
+        self.nx_system = 4
+        self.n_features = 6
+        self.nu = 2
+
+        self.n_agents = 100       # :38
+        self.comm_radius = 0.9
+        self.dt = 0.01
+        self.v_max = 5.0
+        self.r_max = 1.0
+
+        self.comm_radius2 = self.comm_radius * self.comm_radius
+        self.vr = 1 / self.comm_radius2 + np.log(self.comm_radius2)
+        self.v_bias = self.v_max
+
+        self.u = None
+        self.mean_vel = None
+        self.init_vel = None
+        self.max_accel = 1
+        self.action_scalar = 10.0
+        self.device = device
+        self.n_neighbors = 0
+        self.reset_mode = "reference"
+        self.reset_max_attempts = 1000
+
+        self._make_spaces()
+        self.fig = None
+        self.line1 = None
+        self._h = None
+        self._hkey = None
+        self.state_values = None
+        self.state_network = None
+        self._reward = None
+        self.seed()
+
+    # ------------------------------------------------------------------ config
+    def _make_spaces(self):
+        self.action_space = Box(low=-self.max_accel, high=self.max_accel,
+                                shape=(2 * self.n_agents,), dtype=np.float32)
+        self.observation_space = Box(low=-np.inf, high=np.inf,
+                                     shape=(self.n_agents, self.n_features), dtype=np.float32)
+
+    def params_from_cfg(self, args):
+        """:68-85 (including the r_max *= sqrt(n_agents) compounding on repeat calls)."""
+        self.comm_radius = args.getfloat('comm_radius')
+        self.comm_radius2 = self.comm_radius * self.comm_radius
+        self.vr = 1 / self.comm_radius2 + np.log(self.comm_radius2)
+        self.n_agents = args.getint('n_agents')
+        self.r_max = self.r_max * np.sqrt(self.n_agents)
+        self._make_spaces()
+        self.v_max = args.getfloat('v_max')
+        self.v_bias = self.v_max
+        self.dt = args.getfloat('dt')
+
+    def seed(self, seed=None):
+        self.np_random, seed = np_random(seed)
+        return [seed]
+
+    def _key(self):
+        return (self.n_agents, self.comm_radius, self.dt, self.action_scalar,
+                bool(self.mean_pooling), bool(self.centralized), self.n_neighbors, self.device)
+
+    def _handle(self):
+        """The device handle for the current parameters (re-created if they changed)."""
+        key = self._key()
+        if self._h is None or key != self._hkey:
+            if self._h is not None:
+                self._h.close()
+            self._h = nat.FlockHandle(self.n_agents, 1, self.comm_radius, self.dt,
+                                      self.action_scalar, self.mean_pooling, self.centralized,
+                                      self.n_neighbors, self.device)
+            self._hkey = key
+        return self._h
+
+    # ------------------------------------------------------------------- state
+    @property
+    def x(self):
+        if self._h is None:
+            return None
+        return self._h.get_state(0)
+
+    @x.setter
+    def x(self, value):
+        value = np.asarray(value, dtype=np.float64)
+        assert value.shape == (self.n_agents, self.nx_system), value.shape
+        self._handle().set_state(value, env=0)
+
+    # ---------------------------------------------------------------- hot path
+    def _fetch_obs(self):
+        h = self._h
+        self.state_values = h.state_values(0)
+        self.state_network = h.network(0)
+        self._reward = float(h.rewards()[0])
+
+    def step(self, u):
+        """:91-109 — dynamics, compute_helpers and instant_cost in one device launch."""
+        u = np.asarray(u)
+        assert u.shape == (self.n_agents, self.nu)
+        self.u = u * self.action_scalar
+        self._handle().step(u[None])
+        self._fetch_obs()
+        return (self.state_values, self.state_network), self._reward, False, {}
+
+    def compute_helpers(self):
+        """:111-134 on the current state."""
+        self._handle().compute_helpers()
+        self._fetch_obs()
+
+    def instant_cost(self):
+        """:145-147 — reward of the current state (computed with the observations)."""
+        return self._reward
+
+    @property
+    def adj_mat(self):
+        return None if self.state_network is None else (self.state_network > 0).astype(float)
+
+    @property
+    def adj_mat_mean(self):
+        return self.state_network if self.mean_pooling else None
+
+    def get_stats(self):
+        """:136-143."""
+        vd, md, _ = self._handle().stats(0)
+        return {'vel_diffs': vd, 'min_dists': md}
+
+    def controller(self, centralized=None):
+        """:194-212 — Turner-2003 expert action (N,2) float64 for the current state."""
+        if centralized is None:
+            centralized = self.centralized
+        return self._handle().controller(centralized)[0]
+
+    # ------------------------------------------------------------------- reset
+    def _accept(self, x):
+        """:177-184 on the device: min degree >= 2 and min pairwise distance >= 0.1."""
+        h = self._handle()
+        h.set_state(x, env=0)
+        _, min_dists, deg = h.stats(0)
+        return deg.min() >= 2 and min_dists.min() >= 0.1
+
+    def reset(self):
+        """:156-192."""
+        x = None
+        for _ in range(self.reset_max_attempts if self.reset_mode == "reference" else 1):
+            x = draw_swarm(self.n_agents, self.r_max, self.v_max, self.v_bias)
+            if self.reset_mode != "reference" or self._accept(x):
+                break
+        self.mean_vel = np.mean(x[:, 2:4], axis=0)
+        self.init_vel = x[:, 2:4]
+        self.x = x
+        self.compute_helpers()
+        return (self.state_values, self.state_network)
+
+    # ------------------------------------------------------------------ render
+    def render(self, mode='human'):
+        """:234-257 (matplotlib, host side)."""
+        import matplotlib.pyplot as plt
+        x = self.x
+        if self.fig is None:
+            plt.ion()
+            fig = plt.figure()
+            self.ax = fig.add_subplot(111)
+            line1, = self.ax.plot(x[:, 0], x[:, 1], 'bo')
+            self.ax.plot([0], [0], 'kx')
+            plt.ylim(-1.0 * self.r_max, 1.0 * self.r_max)
+            plt.xlim(-1.0 * self.r_max, 1.0 * self.r_max)
+            plt.title('GNN Controller')
+            self.fig, self.line1 = fig, line1
+        self.line1.set_xdata(x[:, 0])
+        self.line1.set_ydata(x[:, 1])
+        self.fig.canvas.draw()
+        self.fig.canvas.flush_events()
+
+    def close(self):
+        if self._h is not None:
+            self._h.close()
+            self._h = None

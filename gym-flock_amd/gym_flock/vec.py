@@ -1,0 +1,102 @@
+"""Batched FlockingRelative / Flocking-v0: B independent envs stepped by one launch.
+
+This is the data-parallel form of the reference's per-env loop (one
+FlockingRelativeEnv.step per env per step, flocking_relative.py:91-109). Outputs
+stay in device memory; the getters copy to the host on demand, so a trainer that
+only needs rewards or a few envs' observations never pays for the (B,N,N) network
+transfer.
+"""
+import numpy as np
+
+from . import _native as nat
+from .init_states import synthetic_batch
+
+
+class VecFlockingRelative:
+    """B FlockingRelative-v0 envs of N agents on one GPU.
+
+    env_offset: global index of this shard's first env (seeds are env_offset + b),
+    so a batch sharded over ranks reproduces the single-device batch.
+    """
+
+    def __init__(self, n_envs, n_agents, comm_radius=0.9, dt=0.01, v_max=5.0,
+                 action_scalar=10.0, mean_pooling=True, centralized=True, n_neighbors=0,
+                 device=0, env_offset=0):
+        self.n_envs, self.n_agents = int(n_envs), int(n_agents)
+        self.v_max = v_max
+        self.env_offset = int(env_offset)
+        self.h = nat.FlockHandle(n_agents, n_envs, comm_radius, dt, action_scalar,
+                                 mean_pooling, centralized, n_neighbors, device)
+
+    # ------------------------------------------------------------------- state
+    def reset(self, seed=0, x=None):
+        """Synthetic init for envs seed+env_offset+b, or a given (B,N,4)."""
+        if x is None:
+            x = synthetic_batch(self.n_envs, self.n_agents, seed + self.env_offset, self.v_max)
+        self.h.set_state(x)
+        self.h.compute_helpers()
+        return x
+
+    def set_state(self, x):
+        self.h.set_state(x)
+
+    def get_state(self):
+        return self.h.get_state()
+
+    # ---------------------------------------------------------------- hot path
+    def step(self, u=None, controller=False, knn=False, network=True, expert=False,
+             resident=False, device_ptr=None):
+        """Advance every env one step.
+
+        u: (B,N,2) host actions (float32 or float64 arithmetic like the reference); or
+        expert=True to feed back the previous controller() output (closed loop); or
+        resident=True to reuse the actions last given to set_actions(); or
+        device_ptr=<int> for a device buffer of float32 actions.
+        Asynchronous: returns once the launch is queued (host actions are copied first).
+        """
+        flags = 0
+        if controller:
+            flags |= nat.FE_WITH_CONTROLLER
+        if knn:
+            flags |= nat.FE_WITH_KNN
+        if not network:
+            flags |= nat.FE_NO_NETWORK
+        if expert:
+            self.h.step(None, flags | nat.FE_U_EXPERT)
+        elif resident:
+            self.h.step(None, flags | nat.FE_U_RESIDENT)
+        elif device_ptr is not None:
+            self.h.step(device_ptr, flags | nat.FE_U_DEVICE)
+        else:
+            self.h.step(u, flags)
+
+    def set_actions(self, u):
+        self.h.set_actions(u)
+
+    def controller(self, centralized=None):
+        return self.h.controller(centralized)
+
+    # ----------------------------------------------------------------- outputs
+    def state_values(self, env=None):
+        return self.h.state_values(env)
+
+    def network(self, env=None):
+        return self.h.network(env)
+
+    def rewards(self):
+        return self.h.rewards()
+
+    def controls(self, env=None):
+        return self.h.controls(env)
+
+    def knn(self, env=None):
+        return self.h.knn(env)
+
+    def stats(self, env=0):
+        return self.h.stats(env)
+
+    def sync(self):
+        self.h.sync()
+
+    def close(self):
+        self.h.close()

@@ -1,0 +1,146 @@
+/*
+ * gymflock.h — C-ABI of libgymflock.so, the MI355X (gfx950) env-step engine for
+ * gym-flock's FlockingRelative-v0 / Flocking-v0 hot path.
+ *
+ * The reference (katetolstaya/gym-flock) has no FFI: its boundary is the Python
+ * gym.Env method surface. Each entry point below replaces one
+ * NumPy code region of that surface; the citation after each declaration names it
+ * (paths relative to the reference root). The Python binding that sits on top of
+ * this ABI (gym-flock_amd/gym_flock/_native.py, ctypes) mirrors the reference's
+ * reset()/step()/controller()/get_stats() methods; INTEGRATION.md shows it.
+ *
+ * Conventions
+ *  - Every function returns int: GF_OK (0) or a GF_E* code; the message of the
+ *    last failure on the calling thread is fe_last_error().
+ *  - Arrays are row-major, C-contiguous. Shapes use B = n_envs, N = n_agents.
+ *  - Host pointers are borrowed for the duration of the call. The library owns
+ *    all device memory; fe_device_buffers() exposes it for zero-copy consumers.
+ *  - One handle per host thread. All work of a handle is ordered on its own HIP
+ *    stream; getters synchronise that stream before copying out.
+ *  - Agent state is float64 (B,N,4) = [px, py, vx, vy] because the reference
+ *    integrates in float64 (flocking_relative.py:157); observations are float32.
+ */
+#ifndef GYMFLOCK_H
+#define GYMFLOCK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GF_ABI_VERSION 1
+
+enum gf_status {
+  GF_OK = 0,
+  GF_EINVAL = 1,   /* bad argument (shape, pointer, flag)                      */
+  GF_EHIP = 2,     /* HIP runtime error (no device, launch failure, ...)       */
+  GF_ENOMEM = 3,   /* device allocation failed                                  */
+  GF_ESTATE = 4,   /* call out of order (e.g. step before set_state)            */
+  GF_ECOMM = 5     /* RCCL error                                                */
+};
+
+/* fe_step / fe_compute_helpers flags */
+#define FE_WITH_CONTROLLER 0x01 /* also run controller() on the post-step state   */
+#define FE_U_DEVICE        0x02 /* u is a device pointer (else host)              */
+#define FE_U_F64           0x04 /* u is float64 (else float32); selects the NumPy
+                                   dtype-dependent arithmetic of :96-105          */
+#define FE_U_EXPERT        0x08 /* u := controller output of the previous call
+                                   (closed loop, float64; u argument ignored)     */
+#define FE_WITH_KNN        0x10 /* Flocking-v0 k-nearest observation              */
+#define FE_NO_NETWORK      0x20 /* skip the dense (N,N) state_network write       */
+#define FE_NO_STATE_VALUES 0x40 /* skip the (N,6) state_values write              */
+#define FE_U_RESIDENT      0x80 /* u := the handle's action buffer as last set by
+                                   fe_set_actions (already in HBM; u ignored)     */
+
+typedef struct fe_config {
+  int32_t n_agents;      /* N  (flocking_relative.py:38; params_from_cfg :74)      */
+  int32_t n_envs;        /* B  independent envs batched on this device            */
+  double comm_radius;    /* 0.9  (:39)                                            */
+  double dt;             /* 0.01 (:40)                                            */
+  double action_scalar;  /* 10.0 (:64)                                            */
+  int32_t mean_pooling;  /* 1 (:27): network = adj / deg, else adj                */
+  int32_t centralized;   /* 1 (:28): controller sums over all agents              */
+  int32_t n_neighbors;   /* k of Flocking-v0 (flocking.py:9, 7); 0 = no kNN buffers */
+  int32_t device;        /* HIP device ordinal                                    */
+} fe_config;
+
+typedef struct fe_handle fe_handle;
+
+/* Device pointers owned by the handle (valid until fe_destroy). Ping-pong
+ * buffers are reported as their CURRENT slot (the one the next getter reads). */
+typedef struct fe_buffers {
+  double* x;             /* (B,N,4) float64 current state                        */
+  float* state_values;   /* (B,N,6) float32                                      */
+  float* network;        /* (B,N,N) float32                                      */
+  double* controls;      /* (B,N,2) float64 last controller() output             */
+  double* rewards;       /* (B)     float64                                      */
+  int32_t* knn_idx;      /* (B,N,k) int32 or NULL                                */
+  float* knn_obs;        /* (B,N,4k) float32 or NULL                             */
+  void* stream;          /* hipStream_t of the handle                            */
+} fe_buffers;
+
+/* Lifecycle ---------------------------------------------------------------- */
+int fe_create(const fe_config* cfg, fe_handle** out);      /* FlockingRelativeEnv.__init__ :20-66 */
+int fe_destroy(fe_handle* h);                               /* close() :303 */
+int fe_get_config(const fe_handle* h, fe_config* out);
+
+/* State ---------------------------------------------------------------------- */
+int fe_set_state(fe_handle* h, const double* x);            /* env.x = ... (:189) */
+int fe_set_state_env(fe_handle* h, int env, const double* x);  /* one env's (N,4) */
+int fe_get_state(fe_handle* h, double* x);                  /* env.x (B,N,4) */
+int fe_get_state_env(fe_handle* h, int env, double* x);     /* one env's (N,4) */
+
+/* Hot path ------------------------------------------------------------------- */
+/* Upload (B,N,2) actions (float32, or float64 if f64) into the handle's resident
+ * action buffer, used by fe_step(..., FE_U_RESIDENT). */
+int fe_set_actions(fe_handle* h, const void* u, int f64);
+/* compute_helpers() on the current state (:111-134); used by reset() (:191). */
+int fe_compute_helpers(fe_handle* h, int flags);
+/* step(u) (:91-109): dynamics (:96-105) + compute_helpers + instant_cost (:145-147),
+ * optionally fused controller() (:194-226) and Flocking-v0 kNN (flocking.py:20-25).
+ * u: (B,N,2) float32 or float64 (FE_U_F64), host or device (FE_U_DEVICE). Async. */
+int fe_step(fe_handle* h, const void* u, int flags);
+/* controller(centralized) (:194-212) on the current state; centralized < 0 means the
+ * config default. Writes (B,N,2) float64 to u_out (host) if non-NULL. */
+int fe_controller(fe_handle* h, int centralized, double* u_out);
+/* get_stats() (:136-143) on the current state: vel_diffs (N) and min_dists (N). */
+int fe_get_stats(fe_handle* h, int env, double* vel_diffs, double* min_dists);
+/* get_stats plus each agent's degree (r2 < comm_radius^2): reset()'s acceptance test
+ * (:177-184) on the device. Any output pointer may be NULL. */
+int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists, int32_t* degree);
+
+/* Outputs (host copies; env < 0 copies all B envs) ---------------------------- */
+int fe_get_state_values(fe_handle* h, int env, float* dst);  /* (N,6) :128-129 */
+int fe_get_network(fe_handle* h, int env, float* dst);       /* (N,N) :131-134 */
+int fe_get_network_rows(fe_handle* h, int env, int row0, int nrows, float* dst);
+int fe_get_controls(fe_handle* h, int env, double* dst);     /* (N,2) :210-211 */
+int fe_get_rewards(fe_handle* h, double* dst);               /* (B)   :145-147 */
+int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs); /* (N,k), (N,4k) */
+int fe_device_buffers(fe_handle* h, fe_buffers* out);
+int fe_sync(fe_handle* h);
+
+/* Multi-GPU metrics path (RCCL over xGMI) ---------------------- */
+/* The env batch is sharded contiguously over ranks (one process per GPU); the
+ * step path has no exchange. Only per-env rewards are all-gathered, on a side
+ * stream, so the collective never sits on the step critical path. */
+int fe_comm_unique_id(uint8_t id[128]);
+int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]);
+/* Enqueue an all-gather of the current per-env rewards into slot (call k % 8). */
+int fe_allgather_rewards(fe_handle* h);
+/* Wait for the latest all-gather and copy its (nranks*B) rewards to dst. */
+int fe_get_gathered_rewards(fe_handle* h, double* dst);
+int fe_comm_destroy(fe_handle* h);
+
+/* Diagnostics ---------------------------------------------------------------- */
+const char* fe_last_error(void);
+int fe_abi_version(void);
+/* Average device time (ms) of the dominant step kernel over the launches since the
+ * last reset, measured with HIP events on the handle's stream (bench roofline). */
+int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GYMFLOCK_H */

@@ -1,0 +1,269 @@
+"""Parity of the HIP FlockingRelative / Flocking-v0 path against the reference's golden
+vectors and the CPU oracle, through the C-ABI (ctypes). Needs an MI355X.
+
+Tolerances (north star: 1e-5 rtol in float32, integer indices bit-exact):
+  state x (float64)          bit-exact (same op order, no FMA contraction)
+  adjacency / network        bit-exact (network = float32(1/deg) on set bits)
+  state_values (float32)     |d| <= 1e-5*|ref| + 1e-9 (float64 sums, order differs)
+  controller (float64)       |d| <= 1e-9*|ref| + 1e-12
+  reward (float64)           rtol 1e-12
+  kNN indices                bit-exact; kNN obs float32 of float64 differences
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import flocking as orc
+
+pytestmark = pytest.mark.gpu
+
+nat = pytest.importorskip("gym_flock._native")
+from gym_flock.init_states import synthetic_batch  # noqa: E402
+from gym_flock.vec import VecFlockingRelative  # noqa: E402
+
+STEP_FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "flock_n*_s*_step.npz")))
+
+
+def adj_from_bits(bits, n):
+    return np.unpackbits(bits, axis=1, count=n).astype(bool)
+
+
+def close_sv(ours, ref):
+    np.testing.assert_allclose(ours, ref, rtol=1e-5, atol=1e-9)
+
+
+def check_against_oracle(h, x0, u, b=None, ctrl=True):
+    """Compare env b of handle h (after one step from x0 with u) to the oracle."""
+    ref = orc.step(x0, u, with_controller=ctrl)
+    env = 0 if b is None else b
+    np.testing.assert_array_equal(h.get_state(env), ref["x"])
+    net = h.network(env)
+    np.testing.assert_array_equal(net > 0, ref["adj"])
+    np.testing.assert_array_equal(net, ref["network"].astype(np.float32))
+    close_sv(h.state_values(env), ref["state_values"])
+    np.testing.assert_allclose(h.rewards()[env], ref["reward"], rtol=1e-12)
+    if ctrl:
+        np.testing.assert_allclose(h.controls(env), ref["ctrl"], rtol=1e-9, atol=1e-12)
+    return ref
+
+
+@pytest.mark.parametrize("path", STEP_FIXTURES, ids=os.path.basename)
+def test_step_matches_reference_golden(path):
+    f = np.load(path)
+    n = f["x0"].shape[0]
+    h = nat.FlockHandle(n, 1, n_neighbors=7)
+    h.set_state(f["x0"][None])
+    h.step(f["u"][None], nat.FE_WITH_CONTROLLER | nat.FE_WITH_KNN)
+    np.testing.assert_array_equal(h.get_state(0), f["x1"])
+    net = h.network(0)
+    adj = adj_from_bits(f["adj_bits"], n)
+    np.testing.assert_array_equal(net > 0, adj)
+    deg = np.maximum(f["deg"], 1).astype(np.float64)
+    np.testing.assert_array_equal(net, (adj / deg[:, None]).astype(np.float32))
+    close_sv(h.state_values(0), f["state_values"])
+    np.testing.assert_allclose(h.rewards()[0], f["reward"], rtol=1e-12)
+    np.testing.assert_allclose(h.controls(0), f["ctrl"], rtol=1e-9, atol=1e-12)
+    idx, obs = h.knn(0)
+    np.testing.assert_array_equal(idx, f["knn_idx"])
+    x1 = f["x1"]
+    want_obs = np.concatenate([x1 - x1[f["knn_idx"][:, m]] for m in range(7)], axis=1)
+    if "knn_obs" in f:
+        np.testing.assert_array_equal(want_obs, f["knn_obs"])
+    np.testing.assert_array_equal(obs, want_obs.astype(np.float32))
+    vd, md, _ = h.stats(0)
+    np.testing.assert_allclose(vd, f["vel_diffs"], rtol=1e-12)
+    np.testing.assert_array_equal(md, f["min_dists"])
+    dec = h.controller(centralized=False)[0]
+    np.testing.assert_allclose(dec, f["ctrl_decentralized"], rtol=1e-9, atol=1e-12)
+    # float64 actions take the float64 arithmetic path of the reference
+    h.set_state(f["x0"][None])
+    h.step(f["u64"][None])
+    np.testing.assert_array_equal(h.get_state(0), f["x1_u64"])
+    np.testing.assert_array_equal((h.network(0) > 0).sum(axis=1), f["deg_u64"])
+    close_sv(h.state_values(0), f["sv_u64"])
+    np.testing.assert_allclose(h.rewards()[0], f["reward_u64"], rtol=1e-12)
+    h.close()
+
+
+def test_n10_episode_trajectory_bit_exact():
+    """Config 1: the reference's 40-step N=10 episode (20 expert, 20 float32 random
+    actions) replayed through the engine: state bit-exact at every step."""
+    f = np.load(os.path.join(GOLDEN, "flock_n10_episode.npz"))
+    h = nat.FlockHandle(10, 1)
+    h.set_state(f["x0"][None])
+    h.compute_helpers()
+    close_sv(h.state_values(0), f["sv0"])
+    np.testing.assert_array_equal(h.network(0), f["net0"].astype(np.float32))
+    for t in range(40):
+        u = f["u"][t].astype(np.float32) if f["u_is_f32"][t] else f["u"][t]
+        if not f["u_is_f32"][t]:
+            np.testing.assert_allclose(h.controller()[0], u, rtol=1e-9, atol=1e-12)
+        h.step(u[None], nat.FE_WITH_CONTROLLER)
+        np.testing.assert_array_equal(h.get_state(0), f["x"][t])
+        close_sv(h.state_values(0), f["sv"][t])
+        np.testing.assert_array_equal(h.network(0), f["net"][t].astype(np.float32))
+        np.testing.assert_allclose(h.rewards()[0], f["reward"][t], rtol=1e-12)
+        np.testing.assert_allclose(h.controls(0), f["ctrl"][t], rtol=1e-9, atol=1e-12)
+    h.close()
+
+
+@pytest.mark.parametrize("n", [7, 10, 63, 100, 130, 1000, 1030, 2049])
+def test_sizes_vs_oracle(n):
+    """Ragged N (scalar network path when N % 4 != 0, partial ballot words, several LDS
+    tiles above 1024) on a batch of 3 envs."""
+    B = 3
+    x0 = synthetic_batch(B, n, seed0=100 + n)
+    u = np.random.RandomState(n).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7 if n >= 7 else 0)
+    h.set_state(x0)
+    h.step(u, nat.FE_WITH_CONTROLLER | (nat.FE_WITH_KNN if n >= 7 else 0))
+    for b in range(B):
+        ref = check_against_oracle(h, x0[b], u[b], b)
+        if n >= 7:
+            idx, obs = h.knn(b)
+            ridx, robs = orc.knn_observation(ref["x"])
+            np.testing.assert_array_equal(idx, ridx)
+            np.testing.assert_array_equal(obs, robs.astype(np.float32))
+    h.close()
+
+
+def test_n1_and_isolated_agents():
+    """Edge cases: one agent (no pairs), and a sparse swarm with isolated agents
+    (deg 0 -> network row of zeros, state_values 0)."""
+    h = nat.FlockHandle(1, 2)
+    x0 = np.array([[[0.1, 0.2, 1.0, -1.0]], [[0.0, 0.0, 0.0, 0.0]]])
+    u = np.zeros((2, 1, 2), np.float32)
+    h.set_state(x0)
+    h.step(u, nat.FE_WITH_CONTROLLER)
+    for b in range(2):
+        check_against_oracle(h, x0[b], u[b], b)
+    h.close()
+    rs = np.random.RandomState(5)
+    x = np.zeros((1, 50, 4))
+    x[0, :, :2] = rs.uniform(-20, 20, size=(50, 2))
+    x[0, :, 2:] = rs.uniform(-1, 1, size=(50, 2))
+    h = nat.FlockHandle(50, 1)
+    h.set_state(x)
+    u = rs.uniform(-1, 1, size=(1, 50, 2)).astype(np.float32)
+    h.step(u, nat.FE_WITH_CONTROLLER)
+    ref = check_against_oracle(h, x[0], u[0])
+    assert (ref["deg"] == 0).any()
+    h.close()
+
+
+def test_noncentralized_and_sum_pooling():
+    n, B = 200, 2
+    x0 = synthetic_batch(B, n, seed0=42)
+    u = np.random.RandomState(1).uniform(-1, 1, size=(B, n, 2))  # float64 actions
+    h = nat.FlockHandle(n, B, mean_pooling=False, centralized=False)
+    h.set_state(x0)
+    h.step(u, nat.FE_WITH_CONTROLLER)
+    for b in range(B):
+        ref = orc.step(x0[b], u[b], mean_pooling=False, with_controller=True, centralized=False)
+        np.testing.assert_array_equal(h.get_state(b), ref["x"])
+        np.testing.assert_array_equal(h.network(b), ref["network"].astype(np.float32))
+        close_sv(h.state_values(b), ref["state_values"])
+        np.testing.assert_allclose(h.controls(b), ref["ctrl"], rtol=1e-9, atol=1e-12)
+    h.close()
+
+
+def test_closed_loop_expert_matches_oracle_rollout():
+    """FE_U_EXPERT feeds the fused controller output back as the next action (the
+    reference's env.step(env.controller()) loop): 30 steps against the oracle, the
+    oracle consuming the engine's own actions so both follow one trajectory."""
+    n, B = 64, 2
+    x = synthetic_batch(B, n, seed0=9)
+    h = nat.FlockHandle(n, B)
+    h.set_state(x)
+    h.compute_helpers(nat.FE_WITH_CONTROLLER)
+    for t in range(30):
+        u = h.controls()
+        for b in range(B):
+            np.testing.assert_allclose(u[b], orc.controller(x[b]), rtol=1e-9, atol=1e-12)
+        h.step(None, nat.FE_U_EXPERT | nat.FE_WITH_CONTROLLER)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        np.testing.assert_array_equal(h.get_state(), x)
+    h.close()
+
+
+def test_full_config2_properties_and_sampled_parity():
+    """Config 2 (N=1024 x 256 envs): size-independent properties on the whole batch
+    (row sums of the mean-pooled network, symmetric adjacency, determinism) and
+    oracle parity on sampled envs."""
+    B, N = 256, 1024
+    x0 = synthetic_batch(B, N, seed0=0)
+    u = np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    v = VecFlockingRelative(B, N)
+    v.set_state(x0)
+    v.step(u, controller=True)
+    net = v.network()
+    sv = v.state_values()
+    rew = v.rewards()
+    adj = net > 0
+    deg = adj.sum(axis=2)
+    rows = net.sum(axis=2, dtype=np.float64)
+    np.testing.assert_allclose(rows[deg > 0], 1.0, rtol=1e-5)
+    assert np.all(rows[deg == 0] == 0)
+    assert np.array_equal(adj, adj.transpose(0, 2, 1))
+    assert not adj[:, np.arange(N), np.arange(N)].any()
+    v.set_state(x0)
+    v.step(u, controller=True)
+    assert np.array_equal(v.network(), net) and np.array_equal(v.state_values(), sv)
+    assert np.array_equal(v.rewards(), rew)
+    for b in (0, 97, 255):
+        check_against_oracle(v.h, x0[b], u[b], b)
+    v.close()
+
+
+def test_env_api_reset_matches_reference_fixture():
+    """FlockingRelativeEnv.reset() reproduces the reference's rejection-sampled state
+    from the same global seed, with the acceptance test run on the device."""
+    import gym_flock
+
+    f = np.load(os.path.join(GOLDEN, "flock_n64_reset.npz"))
+
+    class Cfg:
+        def getfloat(self, k):
+            return {"comm_radius": 0.9, "v_max": 5.0, "dt": 0.01}[k]
+
+        def getint(self, k):
+            return 64
+
+    env = gym_flock.make("FlockingRelative-v0")
+    env.params_from_cfg(Cfg())
+    np.random.seed(int(f["seed"]))
+    sv, net = env.reset()
+    np.testing.assert_array_equal(env.x, f["x0"])
+    close_sv(sv, f["state_values"])
+    np.testing.assert_array_equal(net > 0, adj_from_bits(f["adj_bits"], 64))
+    (sv1, net1), r, done, info = env.step(np.zeros((64, 2), np.float32))
+    assert done is False and info == {} and isinstance(r, float)
+    with pytest.raises(AssertionError):
+        env.step(np.zeros((63, 2)))
+    u = env.controller()
+    assert u.shape == (64, 2) and u.dtype == np.float64
+    st = env.get_stats()
+    assert set(st) == {"vel_diffs", "min_dists"}
+    env.close()
+
+
+def test_flocking_v0_env_api():
+    import gym_flock
+
+    env = gym_flock.make("Flocking-v0")
+    env.n_agents = 100
+    env._make_spaces()
+    np.random.seed(3)
+    obs, net = env.reset()
+    assert obs.shape == (100, 28) and net.shape == (100, 100)
+    x = env.x
+    u = np.random.RandomState(2).uniform(-1, 1, size=(100, 2)).astype(np.float32)
+    (obs, net), r, done, _ = env.step(u)
+    ref = orc.step(x, u)
+    ridx, robs = orc.knn_observation(ref["x"])
+    np.testing.assert_array_equal(env.nearest, ridx)
+    np.testing.assert_array_equal(obs, robs.astype(np.float32))
+    env.close()
