@@ -3,6 +3,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,6 +57,8 @@ struct fe_handle {
   int R = 0, T = 0, bpe = 0;
   size_t BN = 0;
   // kernel timing (bench roofline)
+  int diag = 0;                         // ablation switches for every step launch
+  int lds_pad = 0;                      // occupancy tuning (GYMFLOCK_LDS_PAD)
   bool timing = false;
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
@@ -141,6 +144,8 @@ gf::StepArgs base_args(fe_handle* h) {
   a.bpe = h->bpe;
   a.mean_pooling = h->cfg.mean_pooling;
   a.centralized = h->cfg.centralized;
+  a.diag = h->diag;
+  a.lds_pad = h->lds_pad;
   return a;
 }
 
@@ -215,6 +220,16 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   h->BN = B * N;
   h->R = gf::step_rows_per_block(cfg->n_agents);
   h->T = gf::step_tile(cfg->n_agents);
+  // tuning overrides (power-of-two rows 4..64; tile a multiple of 64, <= 1024)
+  if (const char* e = getenv("GYMFLOCK_ROWS")) {
+    const int r = atoi(e);
+    if (r >= 4 && r <= 64 && (r & (r - 1)) == 0) h->R = r;
+  }
+  if (const char* e = getenv("GYMFLOCK_LDS_PAD")) h->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
+  if (const char* e = getenv("GYMFLOCK_TILE")) {
+    const int t = atoi(e);
+    if (t >= 64 && t <= gf::kTileMax && t % 64 == 0) h->T = t < h->T ? t : h->T;
+  }
   h->bpe = (cfg->n_agents + h->R - 1) / h->R;
   if ((size_t)h->bpe * B > 0x7fffffff) {
     delete h;
@@ -522,6 +537,32 @@ int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches
   if (avg_ms) *avg_ms = n ? tot / n : 0.0;
   if (launches) *launches = n;
   if (enable == 0) h->timing = false;
+  return GF_OK;
+}
+
+int fe_diag(fe_handle* h, int what, int reps, double* avg_ms) {
+  if (!h || reps < 1) return fail(GF_EINVAL, "bad argument");
+  if (int rc = use_dev(h)) return rc;
+  if (what >= 0x100) {  // set ablation switches for subsequent step launches
+    h->diag = what & 0xff;
+    return GF_OK;
+  }
+  hipEvent_t e0, e1;
+  GF_HIP(hipEventCreate(&e0));
+  GF_HIP(hipEventCreate(&e1));
+  const size_t bytes = h->BN * (size_t)h->cfg.n_agents * 4;
+  GF_HIP(hipEventRecord(e0, h->stream));
+  for (int r = 0; r < reps; ++r) {
+    hipError_t e = gf::launch_fill(h->net, bytes, what == 1, h->stream);
+    if (e != hipSuccess) return fail_hip("fill launch", e);
+  }
+  GF_HIP(hipEventRecord(e1, h->stream));
+  GF_HIP(hipEventSynchronize(e1));
+  float ms = 0;
+  GF_HIP(hipEventElapsedTime(&ms, e0, e1));
+  if (avg_ms) *avg_ms = ms / reps;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
   return GF_OK;
 }
 

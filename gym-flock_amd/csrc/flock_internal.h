@@ -6,7 +6,8 @@
 namespace gf {
 
 constexpr int kThreads = 256;   // 4 wave64s per workgroup
-constexpr int kTileMax = 1024;  // agents staged per LDS tile (32 KiB of float64 state)
+constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float64 state)
+constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
 
 // One batched hot-path launch. Pointers are device pointers; all per-env arrays
 // are [B][N][...] contiguous.
@@ -25,6 +26,10 @@ struct StepArgs {
   int T;                  // agents per LDS tile (multiple of 64)
   int bpe;                // workgroups per env = ceil(N / R)
   int mean_pooling, centralized;
+  int lds_pad;            // extra dynamic LDS bytes (occupancy control; tuning knob)
+  int diag;               // ablation switches (0 in production): 2 skip feature pass,
+                          // 4 non-temporal network stores, 8 skip pass 1 (bits are left
+                          // unwritten: timing only), 16 skip tile loads (timing only)
 };
 
 struct KnnArgs {
@@ -51,5 +56,8 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl);
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
+// Diagnostic: stream `bytes` of float4 stores into p (nt = non-temporal), the
+// write-bandwidth ceiling of the network buffer on this device.
+hipError_t launch_fill(void* p, size_t bytes, bool nt, hipStream_t s);
 
 }  // namespace gf

@@ -28,6 +28,9 @@ namespace gf {
 
 namespace {
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 struct __attribute__((aligned(16))) St {
   double px, py, vx, vy;
 };
@@ -92,27 +95,83 @@ __device__ __forceinline__ double clip10(double v) {  // np.clip(v, -10, 10); Na
   return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v);
 }
 
+// float32 prefilter band for one threshold: a pair whose float32 r2 (from float32-
+// rounded positions) is < lo is below the threshold in float64 too, one >= hi is not;
+// pairs in [lo, hi) are decided exactly in float64. For coordinates bounded by Pi, Pj
+// the float32 r2 is within 2^-20 (Pi + Pj + 4) of the float64 one.
+struct Band {
+  float lo, hi;
+};
+
+__device__ __forceinline__ Band make_band(double thr, double delta) {
+  const double lo = thr - delta, hi = thr + delta;
+  float l = static_cast<float>(lo), h = static_cast<float>(hi);
+  if (static_cast<double>(l) > lo) l = nextafterf(l, -__builtin_inff());
+  if (static_cast<double>(h) < hi) h = nextafterf(h, __builtin_inff());
+  return {l, h};
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// A value the whole wave holds (compiler-visible as scalar).
+__device__ __forceinline__ float uniform_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// v_writelane_b32 through the LLVM intrinsic (this clang has no __builtin for it), so
+// the compiler applies the constant-bus and lane-select hazard rules itself.
+extern "C" __device__ int gf_writelane_i32(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// Lane l of (w0, w1) takes the wave-uniform 64-bit mask m.
+__device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m, int l) {
+  w0 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m), l, static_cast<int>(w0)));
+  w1 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m >> 32), l, static_cast<int>(w1)));
+}
+
 // ---------------------------------------------------------------------------------
 // The fused step: DYN = apply dynamics (step) or not (compute_helpers on the current
 // state: reset / standalone controller), UF64 = action dtype, CTRL = also controller().
+#ifndef GF_STEP_MIN_WAVES
+#define GF_STEP_MIN_WAVES 1
+#endif
 template <bool DYN, bool UF64, bool CTRL>
-__global__ __launch_bounds__(kThreads) void flock_step_kernel(StepArgs a) {
+__global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
   const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
   const int Wt = T >> 6;         // words per row of one tile
-  St* tile = reinterpret_cast<St*>(smem);
-  St* rows = tile + T;
-  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);
-  uint64_t* nearb = adj + (size_t)R * Wn;
+  St* tile = reinterpret_cast<St*>(smem);                      // float64 state, T
+  float2* tile32 = reinterpret_cast<float2*>(tile + T);        // float32 positions, T
+  St* rows = reinterpret_cast<St*>(tile32 + T);                // this block's rows, R
+  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
+  uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
   double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)R * Wt : 0));
+  float* redf = reinterpret_cast<float*>(red + 4);
   float* inv = reinterpret_cast<float*>(red + 8);
 
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / a.bpe;
   const int i0 = (L - b * a.bpe) * R;
   const int nrows = min(R, N - i0);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const size_t env0 = (size_t)b * N;
 
   // rows owned by this workgroup (post-update state)
@@ -125,81 +184,209 @@ __global__ __launch_bounds__(kThreads) void flock_step_kernel(StepArgs a) {
   double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
   double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
   St me{0, 0, 0, 0};
+  float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
+
+  // pass 2: features / gradients for the set bits of one tile, ascending j per slice
+  auto feature_pass = [&](int j0, int nch) {
+    if (!frow || (a.diag & 2)) return;
+    const int wpt = (nch + S - 1) / S;
+    const int wb = fs * wpt, we = min(nch, wb + wpt);
+    for (int w = wb; w < we; ++w) {
+      const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
+      const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
+      uint64_t m = am | nm;
+      while (m) {
+        const int k = __builtin_ctzll(m);
+        m &= m - 1;
+        const St o = tile[(w << 6) + k];
+        const double dx = me.px - o.px, dy = me.py - o.py;
+        const double r2 = dx * dx + dy * dy;
+        const double rr = r2 * r2;
+        const double q1x = dx / rr, q2x = dx / r2;
+        const double q1y = dy / rr, q2y = dy / r2;
+        const bool isadj = (am >> k) & 1ull;
+        if (isadj) {
+          f0 += me.vx - o.vx;
+          f1 += q1x;
+          f2 += q2x;
+          f3 += me.vy - o.vy;
+          f4 += q1y;
+          f5 += q2y;
+        }
+        if constexpr (CTRL) {
+          const bool isnear = (nm >> k) & 1ull;
+          if (isnear && (a.centralized || isadj)) {
+            gx += (-2.0 * q1x) + (2.0 * q2x);
+            gy += (-2.0 * q1y) + (2.0 * q2y);
+          }
+        }
+      }
+    }
+  };
 
   for (int j0 = 0; j0 < N; j0 += T) {
     const int tc = min(T, N - j0);
     __syncthreads();  // previous tile fully consumed; rows[] visible on first pass
-    for (int t = tid; t < tc; t += kThreads) {
+    float pt = 0.f;
+    for (int t = (a.diag & 16) ? tc : tid; t < tc; t += kThreads) {
       const St s = load_state<DYN, UF64>(a, env0 + j0 + t);
       tile[t] = s;
+      const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
+      tile32[t] = make_float2(fx, fy);
+      pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
       svx += s.vx;
       svy += s.vy;
     }
-    if (j0 == 0 && frow) me = rows[fr];
-    __syncthreads();
+    if (j0 == 0) {
+      if (frow) me = rows[fr];
+      if (lane < nrows) {
+        const St ri = rows[lane];
+        rx32 = static_cast<float>(ri.px);
+        ry32 = static_cast<float>(ri.py);
+      }
+      Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
+    }
+    const float Pt = block_max(pt, redf);  // also the barrier that publishes the tile
 
-    // pass 1: adjacency (and controller "near") bits, lane = column j, loop over rows
+    // pass 1: adjacency (and controller "near") bits. A wave takes 128 columns (lane
+    // j and j+64, packed float32 math) and loops over the block's rows; the compare
+    // masks are the bit words, collected so that lane r ends up holding row r's words.
+    // float32 decides every pair outside the error band (make_band); if any pair of
+    // the chunk falls inside it, the rows are swept again deciding those in float64.
     const int nch = (tc + 63) >> 6;
-    for (int c = wid; c < nch; c += 4) {
-      const int jt = (c << 6) + lane;
-      const int j = j0 + jt;
-      const bool vj = jt < tc;
-      const St o = vj ? tile[jt] : St{0, 0, 0, 0};
-      uint64_t* arow = adj + (j0 >> 6) + c;
-      uint64_t* nrow = nearb + c;
-
+    const int npair = (nch + 1) >> 1;
+    const float pu = uniform_f(Pr) + uniform_f(Pt);
+    Band ba{-__builtin_inff(), __builtin_inff()}, bn = ba;  // huge/non-finite: all exact
+    if (pu < 1.0e5f) {
+      const double delta = ldexp(static_cast<double>(pu) * (1.0 + 1e-6) + 4.0, -20);
+      ba = make_band(a.cr2, delta);
+      bn = make_band(a.cr, delta);
+    }
+    ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
+    bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
+    for (int cp = (a.diag & 8) ? npair : wid; cp < npair; cp += 4) {
+      const int ca = cp << 1;
+      const bool has_b = ca + 1 < nch;
+      const int jta = (ca << 6) + lane, jtb = jta + 64;
+      const bool va = jta < tc, vb = jtb < tc;
+      // columns past the tile sit far away: never adjacent, never in the band
+      const float2 qa = va ? tile32[jta] : make_float2(1.0e18f, 1.0e18f);
+      const float2 qb = vb ? tile32[jtb] : make_float2(1.0e18f, 1.0e18f);
+      const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
+      unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
+      uint64_t band = 0;
       for (int r = 0; r < nrows; ++r) {
-        const double dx = rows[r].px - o.px;
-        const double dy = rows[r].py - o.py;
-        const double r2 = dx * dx + dy * dy;
-        const bool ok = vj && (j != i0 + r);
-        const uint64_t am = __ballot(ok && r2 < a.cr2);
-        if (lane == 0) arow[(size_t)r * Wn] = am;
+        const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+        const f2v dx = xi - qx, dy = yi - qy;
+        const f2v d2 = dx * dx + dy * dy;
+        const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+        const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+        band |= (Aa ^ Ma) | (Ab ^ Mb);
+        put_lane(wa0, wa1, Aa, r);
+        put_lane(wb0, wb1, Ab, r);
         if constexpr (CTRL) {
-          const uint64_t nm = __ballot(ok && r2 <= a.cr);
-          if (lane == 0) nrow[(size_t)r * Wt] = nm;
+          const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+          const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+          band |= (Na ^ NMa) | (Nb ^ NMb);
+          put_lane(na0, na1, Na, r);
+          put_lane(nb0, nb1, Nb, r);
         }
       }
-    }
-    __syncthreads();
-
-    // pass 2: features / gradients for set bits only, ascending j per slice
-    if (frow) {
-      const int wpt = (nch + S - 1) / S;
-      const int wb = fs * wpt, we = min(nch, wb + wpt);
-      for (int w = wb; w < we; ++w) {
-        const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
-        const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
-        uint64_t m = am | nm;
-        while (m) {
-          const int k = __builtin_ctzll(m);
-          m &= m - 1;
-          const St o = tile[(w << 6) + k];
-          const double dx = me.px - o.px, dy = me.py - o.py;
-          const double r2 = dx * dx + dy * dy;
-          const double rr = r2 * r2;
-          const double q1x = dx / rr, q2x = dx / r2;
-          const double q1y = dy / rr, q2y = dy / r2;
-          const bool isadj = (am >> k) & 1ull;
-          if (isadj) {
-            f0 += me.vx - o.vx;
-            f1 += q1x;
-            f2 += q2x;
-            f3 += me.vy - o.vy;
-            f4 += q1y;
-            f5 += q2y;
-          }
+      if (band) {  // rare: some pair is within the float32 error band of a threshold
+        const St oa = va ? tile[jta] : St{1.0e300, 1.0e300, 0, 0};
+        const St ob = vb ? tile[jtb] : St{1.0e300, 1.0e300, 0, 0};
+        for (int r = 0; r < nrows; ++r) {
+          const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+          const f2v dx = xi - qx, dy = yi - qy;
+          const f2v d2 = dx * dx + dy * dy;
+          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+          uint64_t Na = 0, Nb = 0, NMa = 0, NMb = 0;
           if constexpr (CTRL) {
-            const bool isnear = (nm >> k) & 1ull;
-            if (isnear && (a.centralized || isadj)) {
-              gx += (-2.0 * q1x) + (2.0 * q2x);
-              gy += (-2.0 * q1y) + (2.0 * q2y);
+            Na = __ballot(d2.x <= bn.lo);
+            Nb = __ballot(d2.y <= bn.lo);
+            NMa = __ballot(!(d2.x > bn.hi));
+            NMb = __ballot(!(d2.y > bn.hi));
+          }
+          if ((Aa ^ Ma) | (Ab ^ Mb) | (Na ^ NMa) | (Nb ^ NMb)) {
+            const St ri = rows[r];
+            const double dxa = ri.px - oa.px, dya = ri.py - oa.py;
+            const double dxb = ri.px - ob.px, dyb = ri.py - ob.py;
+            const double r2a = dxa * dxa + dya * dya, r2b = dxb * dxb + dyb * dyb;
+            put_lane(wa0, wa1, Aa | (__ballot(r2a < a.cr2) & (Aa ^ Ma)), r);
+            put_lane(wb0, wb1, Ab | (__ballot(r2b < a.cr2) & (Ab ^ Mb)), r);
+            if constexpr (CTRL) {
+              put_lane(na0, na1, Na | (__ballot(r2a <= a.cr) & (Na ^ NMa)), r);
+              put_lane(nb0, nb1, Nb | (__ballot(r2b <= a.cr) & (Nb ^ NMb)), r);
             }
           }
         }
       }
+      if (lane < nrows) {
+        // the diagonal (self, r2 = 0 here; inf in the reference) is never a neighbour
+        const int dl = i0 + lane - (j0 + (ca << 6));
+        const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
+        const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
+        uint64_t* arow = adj + (size_t)lane * Wn + (j0 >> 6) + ca;
+        arow[0] = ((static_cast<uint64_t>(wa1) << 32) | wa0) & ka;
+        if (has_b) arow[1] = ((static_cast<uint64_t>(wb1) << 32) | wb0) & kb;
+        if constexpr (CTRL) {
+          uint64_t* nrow = nearb + (size_t)lane * Wt + ca;
+          nrow[0] = ((static_cast<uint64_t>(na1) << 32) | na0) & ka;
+          if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
+        }
+      }
+    }
+    __syncthreads();
+
+    // pass 2 (features) of every tile but the last runs here; the last tile's runs
+    // after the network stores are issued, so the stores drain under it.
+    if (j0 + T < N) feature_pass(j0, nch);
+  }
+  const int jl = ((N - 1) / T) * T;  // first column of the last tile (still in LDS)
+  const int nchl = (N - jl + 63) >> 6;
+
+  // degree of each row -> 1/deg for the mean-pooled network (:120-122)
+  {
+    int deg = 0;
+    if (frow) {
+      const int wpt = (Wn + S - 1) / S;
+      const int wb = fs * wpt, we = min(Wn, wb + wpt);
+      for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
+    }
+    for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
+    if (frow && fs == 0)
+      inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
+  }
+  __syncthreads();
+
+  // pass 3: dense network rows adj/deg, 16-byte stores (1 KiB per wave instruction);
+  // the block's R rows are one contiguous R*N*4-byte range
+  if (a.network) {
+    const bool vec4 = (N & 3) == 0;
+    for (int r = wid; r < nrows; r += 4) {
+      const float iv = inv[r];
+      const uint64_t* bits = adj + (size_t)r * Wn;
+      float* rowp = a.network + (env0 + i0 + r) * (size_t)N;
+      if (vec4) {
+        f4v* r4 = reinterpret_cast<f4v*>(rowp);
+        const int nq = N >> 2;
+        for (int q = lane; q < nq; q += 64) {
+          const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
+          const f4v v = {(nib & 1u) ? iv : 0.0f, (nib & 2u) ? iv : 0.0f, (nib & 4u) ? iv : 0.0f,
+                         (nib & 8u) ? iv : 0.0f};
+          if (a.diag & 4)
+            __builtin_nontemporal_store(v, &r4[q]);
+          else
+            r4[q] = v;
+        }
+      } else {
+        for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
+      }
     }
   }
+
+  feature_pass(jl, nchl);
 
   // combine the S slices of each row (xor butterfly: identical bits in every lane)
   for (int o = 1; o < S; o <<= 1) {
@@ -214,22 +401,12 @@ __global__ __launch_bounds__(kThreads) void flock_step_kernel(StepArgs a) {
       gy += __shfl_xor(gy, o);
     }
   }
-  int deg = 0;
-  if (frow) {
-    const int wpt = (Wn + S - 1) / S;
-    const int wb = fs * wpt, we = min(Wn, wb + wpt);
-    for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
-  }
-  for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
 
   const double Svx = block_sum(svx, red);
   const double Svy = block_sum(svy, red);
 
   if (frow && fs == 0) {
-    const int i = i0 + fr;
-    const size_t g = env0 + i;
-    inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg))
-                             : 1.0f;
+    const size_t g = env0 + i0 + fr;
     if (a.state_values) {
       float* sv = a.state_values + g * 6;
       sv[0] = static_cast<float>(f0);
@@ -255,15 +432,20 @@ __global__ __launch_bounds__(kThreads) void flock_step_kernel(StepArgs a) {
     }
   }
 
-  // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the
-  // env's first row block only
+  // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
+  // first row block; single-tile envs read the velocities from the LDS tile
   if (a.reward && i0 == 0) {
     const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
     double qx = 0, qy = 0;
-    for (int j0 = 0; j0 < N; j0 += T) {
-      const int tc = min(T, N - j0);
-      for (int t = tid; t < tc; t += kThreads) {
-        const St s = load_state<DYN, UF64>(a, env0 + j0 + t);
+    if (N <= T) {
+      for (int t = tid; t < N; t += kThreads) {
+        const double ex = tile[t].vx - mx, ey = tile[t].vy - my;
+        qx += ex * ex;
+        qy += ey * ey;
+      }
+    } else {
+      for (int j = tid; j < N; j += kThreads) {
+        const St s = load_state<DYN, UF64>(a, env0 + j);
         const double ex = s.vx - mx, ey = s.vy - my;
         qx += ex * ex;
         qy += ey * ey;
@@ -272,32 +454,6 @@ __global__ __launch_bounds__(kThreads) void flock_step_kernel(StepArgs a) {
     const double Qx = block_sum(qx, red);
     const double Qy = block_sum(qy, red);
     if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
-  }
-
-  // pass 3: dense network rows, adj/deg as 16-byte stores (1 KiB per wave instruction)
-  if (a.network) {
-    __syncthreads();
-    const bool vec4 = (N & 3) == 0;
-    for (int r = wid; r < nrows; r += 4) {
-      const float iv = inv[r];
-      const uint64_t* bits = adj + (size_t)r * Wn;
-      float* rowp = a.network + (env0 + i0 + r) * (size_t)N;
-      if (vec4) {
-        float4* r4 = reinterpret_cast<float4*>(rowp);
-        const int nq = N >> 2;
-        for (int q = lane; q < nq; q += 64) {
-          const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
-          float4 v;
-          v.x = (nib & 1u) ? iv : 0.0f;
-          v.y = (nib & 2u) ? iv : 0.0f;
-          v.z = (nib & 4u) ? iv : 0.0f;
-          v.w = (nib & 8u) ? iv : 0.0f;
-          r4[q] = v;
-        }
-      } else {
-        for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
-      }
-    }
   }
 }
 
@@ -426,9 +582,13 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
 }  // namespace
 
 // ----------------------------------------------------------------------------- host
+// Geometry measured on MI355X (scripts/ablate.py, N=1024 x 256 envs): 32-row blocks
+// with 512-agent LDS tiles keep ~5 workgroups per CU resident, which is what hides the
+// per-block load/compute latency under the network stores (fewer resident workgroups
+// were markedly slower).
 int step_rows_per_block(int N) {
   const int words = (N + 63) / 64;
-  int R = 64;
+  int R = 32;
   while (R > 4 && (size_t)R * words * 8 > 16384) R >>= 1;  // adjacency bits <= 16 KiB
   while (R > 4 && R / 2 >= N) R >>= 1;
   return R;
@@ -436,12 +596,12 @@ int step_rows_per_block(int N) {
 
 int step_tile(int N) {
   const int t = ((N + 63) / 64) * 64;
-  return t < kTileMax ? t : kTileMax;
+  return t < kTileDefault ? t : kTileDefault;
 }
 
 size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
-  size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
+  size_t s = (size_t)T * (sizeof(St) + 8) + (size_t)R * sizeof(St);
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 + 15) / 16) * 16;
   return s;
@@ -449,7 +609,7 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
 
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
-  const size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL);
+  const size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL>),
@@ -480,6 +640,27 @@ hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
 #undef GF_KNN_CASE
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void diag_fill_kernel(f4v* p, size_t n4) {
+  const f4v v{1.0f, 0.0f, 0.5f, 0.0f};
+  for (size_t k = blockIdx.x * (size_t)kThreads + threadIdx.x; k < n4; k += (size_t)gridDim.x * kThreads) {
+    if (NT)
+      __builtin_nontemporal_store(v, &p[k]);
+    else
+      p[k] = v;
+  }
+}
+
+hipError_t launch_fill(void* p, size_t bytes, bool nt, hipStream_t s) {
+  const size_t n4 = bytes / 16;
+  const int grid = 256 * 16;
+  if (nt)
+    hipLaunchKernelGGL(diag_fill_kernel<true>, dim3(grid), dim3(kThreads), 0, s, (f4v*)p, n4);
+  else
+    hipLaunchKernelGGL(diag_fill_kernel<false>, dim3(grid), dim3(kThreads), 0, s, (f4v*)p, n4);
   return hipGetLastError();
 }
 

@@ -79,6 +79,7 @@ SIGNATURES = {
     "fe_comm_destroy": [_P],
     "fe_last_error": [],
     "fe_abi_version": [],
+    "fe_diag": [_P, _I, _I, ctypes.POINTER(ctypes.c_double)],
     "fe_kernel_timing": [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
 }
 _RESTYPE = {"fe_last_error": ctypes.c_char_p}
@@ -257,6 +258,14 @@ class FlockHandle:
         ms, n = ctypes.c_double(), ctypes.c_int64()
         check(self.lib.fe_kernel_timing(self.h, 0, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    def diag_fill(self, nontemporal=False, reps=10):
+        ms = ctypes.c_double()
+        check(self.lib.fe_diag(self.h, 1 if nontemporal else 0, int(reps), ctypes.byref(ms)))
+        return ms.value
+
+    def diag_switches(self, bits):
+        check(self.lib.fe_diag(self.h, 0x100 | int(bits), 1, None))
 
     # -- RCCL metrics path
     @staticmethod

@@ -1,0 +1,24 @@
+"""A few steps of the bench workload, for rocprofv3 --pmc passes (no timing)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-flock_amd")]
+from gym_flock import _native as nat  # noqa: E402
+from gym_flock.init_states import synthetic_batch  # noqa: E402
+
+N = int(os.environ.get("N", 1024))
+B = int(os.environ.get("B", 256))
+STEPS = int(os.environ.get("STEPS", 5))
+h = nat.FlockHandle(N, B)
+h.set_state(synthetic_batch(B, N))
+h.set_actions(np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
+h.diag_switches(int(os.environ.get("DIAG", 0)))
+for _ in range(STEPS):
+    h.step(None, nat.FE_U_RESIDENT)
+if os.environ.get("FILL"):
+    h.diag_fill(os.environ["FILL"] == "nt", STEPS)
+h.sync()
+print("done")
