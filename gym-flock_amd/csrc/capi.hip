@@ -228,7 +228,10 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   if (const char* e = getenv("GYMFLOCK_LDS_PAD")) h->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
   if (const char* e = getenv("GYMFLOCK_TILE")) {
     const int t = atoi(e);
-    if (t >= 64 && t <= gf::kTileMax && t % 64 == 0) h->T = t < h->T ? t : h->T;
+    if (t >= 64 && t <= gf::kTileMax && t % 64 == 0) {
+      const int full = ((cfg->n_agents + 63) / 64) * 64;
+      h->T = t < full ? t : full;
+    }
   }
   h->bpe = (cfg->n_agents + h->R - 1) / h->R;
   if ((size_t)h->bpe * B > 0x7fffffff) {
