@@ -34,6 +34,11 @@ constexpr int kRewardSlots = 8;  // reward ring: step t writes slot t % 8
 
 }  // namespace
 
+namespace gf {
+// Shared with the Coverage C-ABI (cov_capi.hip): one thread-local error message.
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace gf
+
 struct fe_handle {
   fe_config cfg{};
   hipStream_t stream = nullptr;

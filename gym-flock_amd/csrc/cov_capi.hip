@@ -1,0 +1,299 @@
+// C-ABI of the Coverage-v0 engine (include/gymflock.h, cov_* functions).
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "coverage_internal.h"
+#include "gymflock.h"
+
+namespace gf {
+int set_error(int code, const std::string& msg);
+}
+
+namespace {
+
+int cfail(int code, const std::string& m) { return gf::set_error(code, m); }
+
+#define CV_HIP(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) return cfail(GF_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int calloc_dev(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) return GF_OK;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+  if (e != hipSuccess) return cfail(GF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  e = hipMemset(*p, 0, n * sizeof(T));
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  return GF_OK;
+}
+
+}  // namespace
+
+struct cov_handle {
+  cov_config cfg{};
+  hipStream_t stream = nullptr;
+  gf::CovArgs a{};
+  int32_t* ntg = nullptr;
+  double* tgt = nullptr;
+  int32_t* actions = nullptr;
+  int32_t* start = nullptr;
+  uint8_t* visited0 = nullptr;
+  int32_t* envsel = nullptr;
+  int* err = nullptr;
+  std::vector<int> ntg_host;
+  bool has_graph = false, has_state = false;
+};
+
+namespace {
+
+int use(const cov_handle* h) {
+  CV_HIP(hipSetDevice(h->cfg.device));
+  return GF_OK;
+}
+
+void cov_release(cov_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->cfg.device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  gf::CovArgs& a = h->a;
+  void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
+                  a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
+                  a.receivers, a.obs_step, h->err, h->start, h->visited0, h->envsel};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+// Read and clear the device error bits; translate to a status.
+int check_err(cov_handle* h) {
+  int err = 0;
+  CV_HIP(hipMemcpyAsync(&err, h->err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  if (!err) return GF_OK;
+  CV_HIP(hipMemset(h->err, 0, sizeof(int)));
+  std::string m;
+  if (err & 1) m += "a target has more than 4 motion-graph neighbours (coverage.py:257 assert); ";
+  if (err & 2) m += "motion edges + 8*n_robots exceed 4*max_nodes (\"Increase MAX_EDGES\", coverage.py:288); ";
+  if (err & 4) m += "action outside [0, 4) (coverage.py:189 index); ";
+  return cfail(GF_EINVAL, m);
+}
+
+int copy_out(cov_handle* h, void* dst, const void* src, size_t bytes) {
+  if (!dst) return GF_OK;
+  CV_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  return GF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cov_create(const cov_config* cfg, cov_handle** out) {
+  if (!cfg || !out) return cfail(GF_EINVAL, "null argument");
+  *out = nullptr;
+  if (cfg->n_robots < 1 || cfg->n_envs < 1 || cfg->max_nodes <= cfg->n_robots)
+    return cfail(GF_EINVAL, "need n_robots >= 1, n_envs >= 1, max_nodes > n_robots");
+  if (cfg->n_robots > 4096) return cfail(GF_EINVAL, "n_robots > 4096 not supported");
+  if (!(cfg->res > 0) || !(cfg->motion_radius > 0)) return cfail(GF_EINVAL, "bad res/motion_radius");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return cfail(GF_EHIP, "no HIP device available (libgymflock needs an MI355X)");
+  if (cfg->device < 0 || cfg->device >= ndev) return cfail(GF_EINVAL, "device ordinal out of range");
+  cov_handle* h = new cov_handle();
+  h->cfg = *cfg;
+  const size_t B = cfg->n_envs, R = cfg->n_robots, M = cfg->max_nodes, Tm = M - R, E = 4 * M;
+  gf::CovArgs& a = h->a;
+  a.B = (int)B;
+  a.R = (int)R;
+  a.M = (int)M;
+  a.Tmax = (int)Tm;
+  a.episode_length = cfg->episode_length;
+  a.res = cfg->res;
+  a.motion_radius = cfg->motion_radius;
+  int rc = GF_OK;
+  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    cov_release(h);
+    return cfail(GF_EHIP, "stream create failed");
+  }
+  if ((rc = calloc_dev(&h->ntg, B)) || (rc = calloc_dev(&h->tgt, B * Tm * 2)) || (rc = calloc_dev(&a.nbr, B * Tm * 4)) ||
+      (rc = calloc_dev(&a.cnt, B * Tm)) || (rc = calloc_dev(&a.n_motion, B)) || (rc = calloc_dev(&a.xr, B * R * 2)) ||
+      (rc = calloc_dev(&a.cur, B * R)) || (rc = calloc_dev(&a.visited, B * Tm)) || (rc = calloc_dev(&a.nvisited, B)) ||
+      (rc = calloc_dev(&a.step_counter, B)) || (rc = calloc_dev(&a.dirty, B)) || (rc = calloc_dev(&h->actions, B * R)) ||
+      (rc = calloc_dev(&a.reward, B)) || (rc = calloc_dev(&a.done, B)) || (rc = calloc_dev(&a.nodes, B * M * 3)) ||
+      (rc = calloc_dev(&a.edges, B * E)) || (rc = calloc_dev(&a.senders, B * E)) || (rc = calloc_dev(&a.receivers, B * E)) ||
+      (rc = calloc_dev(&a.obs_step, B)) || (rc = calloc_dev(&h->err, 1)) || (rc = calloc_dev(&h->start, B * R)) ||
+      (rc = calloc_dev(&h->visited0, B * Tm)) || (rc = calloc_dev(&h->envsel, B))) {
+    cov_release(h);
+    return rc;
+  }
+  a.tgt = h->tgt;
+  a.ntg = h->ntg;
+  a.err = h->err;
+  h->ntg_host.assign(B, 0);
+  *out = h;
+  return GF_OK;
+}
+
+int cov_destroy(cov_handle* h) {
+  cov_release(h);
+  return GF_OK;
+}
+
+int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets) {
+  if (!h || !targets) return cfail(GF_EINVAL, "null argument");
+  const int B = h->cfg.n_envs, Tm = h->a.Tmax;
+  if (env >= B) return cfail(GF_EINVAL, "env index out of range");
+  if (n_targets < 1 || n_targets > Tm)
+    return cfail(GF_EINVAL, "n_targets must be in [1, max_nodes - n_robots] (PAD_NODES, coverage.py:540-543)");
+  if (n_targets < h->cfg.n_robots) return cfail(GF_EINVAL, "fewer targets than robots (reset draws distinct starts)");
+  if (int rc = use(h)) return rc;
+  const int b0 = env < 0 ? 0 : env, b1 = env < 0 ? B : env + 1;
+  std::vector<int32_t> sel;
+  for (int b = b0; b < b1; ++b) {
+    CV_HIP(hipMemcpyAsync(h->tgt + (size_t)b * Tm * 2, targets, (size_t)n_targets * 2 * sizeof(double),
+                          hipMemcpyHostToDevice, h->stream));
+    h->ntg_host[b] = n_targets;
+    sel.push_back(b);
+  }
+  CV_HIP(hipMemcpyAsync(h->ntg, h->ntg_host.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipMemcpyAsync(h->envsel, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  hipError_t e = gf::launch_cov_graph(h->a, h->envsel, (int)sel.size(), h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_graph_kernel: ") + hipGetErrorString(e));
+  if (int rc = check_err(h)) return rc;
+  h->has_graph = true;
+  for (int b = 0; b < B; ++b) h->has_graph = h->has_graph && h->ntg_host[b] > 0;
+  return GF_OK;
+}
+
+int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited) {
+  if (!h || !start || !visited) return cfail(GF_EINVAL, "null argument");
+  if (!h->has_graph) return cfail(GF_ESTATE, "set the target graph of every env first (cov_set_targets)");
+  const size_t B = h->cfg.n_envs, R = h->cfg.n_robots, Tm = h->a.Tmax;
+  for (size_t b = 0; b < B; ++b)
+    for (size_t i = 0; i < R; ++i)
+      if (start[b * R + i] < 0 || start[b * R + i] >= h->ntg_host[b]) return cfail(GF_EINVAL, "start target out of range");
+  if (int rc = use(h)) return rc;
+  CV_HIP(hipMemcpyAsync(h->start, start, B * R * 4, hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipMemcpyAsync(h->visited0, visited, B * Tm, hipMemcpyHostToDevice, h->stream));
+  hipError_t e = gf::launch_cov_reset(h->a, h->start, h->visited0, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_reset_kernel: ") + hipGetErrorString(e));
+  gf::CovArgs a = h->a;
+  a.actions = nullptr;
+  e = gf::launch_cov_step(a, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  h->has_state = true;
+  return GF_OK;
+}
+
+int cov_set_actions(cov_handle* h, const int32_t* actions) {
+  if (!h || !actions) return cfail(GF_EINVAL, "null argument");
+  if (int rc = use(h)) return rc;
+  CV_HIP(hipMemcpyAsync(h->actions, actions, (size_t)h->cfg.n_envs * h->cfg.n_robots * 4, hipMemcpyHostToDevice,
+                        h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_step(cov_handle* h, const int32_t* actions, int flags) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (int rc = use(h)) return rc;
+  gf::CovArgs a = h->a;
+  if (flags & COV_ACTIONS_DEVICE) {
+    if (!actions) return cfail(GF_EINVAL, "null action pointer");
+    a.actions = actions;
+  } else if (flags & COV_ACTIONS_RESIDENT) {
+    a.actions = h->actions;
+  } else {
+    if (!actions) return cfail(GF_EINVAL, "null action pointer");
+    const size_t n = (size_t)h->cfg.n_envs * h->cfg.n_robots;
+    for (size_t k = 0; k < n; ++k)
+      if (actions[k] < 0 || actions[k] >= 4) return cfail(GF_EINVAL, "action outside [0, 4) (coverage.py:189 index)");
+    CV_HIP(hipMemcpyAsync(h->actions, actions, n * 4, hipMemcpyHostToDevice, h->stream));
+    a.actions = h->actions;
+  }
+  hipError_t e = gf::launch_cov_step(a, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
+  if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT))) CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_set_robot_positions(cov_handle* h, int env, const double* xr) {
+  if (!h || !xr || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (int rc = use(h)) return rc;
+  const size_t R = h->cfg.n_robots;
+  const uint8_t one = 1;
+  CV_HIP(hipMemcpyAsync(h->a.xr + env * R * 2, xr, R * 2 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipMemcpyAsync(h->a.dirty + env, &one, 1, hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_get_obs(cov_handle* h, int env, float* nodes, float* edges, int32_t* senders, int32_t* receivers,
+                int64_t* step) {
+  if (!h || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (int rc = use(h)) return rc;
+  const size_t M = h->cfg.max_nodes, E = 4 * M;
+  const gf::CovArgs& a = h->a;
+  if (int rc = copy_out(h, nodes, a.nodes + env * M * 3, M * 3 * 4)) return rc;
+  if (int rc = copy_out(h, edges, a.edges + env * E, E * 4)) return rc;
+  if (int rc = copy_out(h, senders, a.senders + env * E, E * 4)) return rc;
+  if (int rc = copy_out(h, receivers, a.receivers + env * E, E * 4)) return rc;
+  if (int rc = copy_out(h, step, a.obs_step + env, 8)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return check_err(h);
+}
+
+int cov_get_rewards(cov_handle* h, double* reward, uint8_t* done) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (int rc = use(h)) return rc;
+  const size_t B = h->cfg.n_envs;
+  if (int rc = copy_out(h, reward, h->a.reward, B * 8)) return rc;
+  if (int rc = copy_out(h, done, h->a.done, B)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return check_err(h);
+}
+
+int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes) {
+  if (!h || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
+  if (int rc = use(h)) return rc;
+  const size_t R = h->cfg.n_robots;
+  if (int rc = copy_out(h, xr, h->a.xr + env * R * 2, R * 16)) return rc;
+  if (int rc = copy_out(h, nodes, h->a.cur + env * R, R * 4)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_get_visited(cov_handle* h, int env, uint8_t* visited) {
+  if (!h || !visited || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
+  if (int rc = use(h)) return rc;
+  const size_t Tm = h->a.Tmax;
+  if (int rc = copy_out(h, visited, h->a.visited + env * Tm, Tm)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_get_n_motion(cov_handle* h, int32_t* n_motion) {
+  if (!h || !n_motion) return cfail(GF_EINVAL, "null argument");
+  if (int rc = use(h)) return rc;
+  if (int rc = copy_out(h, n_motion, h->a.n_motion, (size_t)h->cfg.n_envs * 4)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_sync(cov_handle* h) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (int rc = use(h)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return check_err(h);
+}
+
+}  // extern "C"

@@ -1,0 +1,305 @@
+// HIP kernels (gfx950) for gym-flock's Coverage-v0 step, batched over B envs.
+//
+// Reference (gym_flock/envs/spatial/): coverage.py step :174-204, get_action_edges
+// :206-232, _get_obs_reward :234-364, closest_targets :427-432, _initialize_graph
+// :529-594; utils.py _get_graph_edges :8-24.
+//
+// One workgroup per env. Node indices are global as in the reference: robots
+// 0..R-1, targets R..R+T-1. The padded graph observation (nodes (M,3), edges (4M,1),
+// senders/receivers (4M)) lives in HBM and is updated in place: the motion-graph part
+// is written once per graph (cov_graph_kernel), each step rewrites the 8R action
+// edges at the tail and flips the "unvisited" feature of newly visited nodes, which
+// leaves the arrays equal to what the reference rebuilds every step.
+#include <limits.h>
+
+#include "coverage_internal.h"
+
+namespace gf {
+
+namespace {
+
+constexpr int kCovThreads = 256;
+
+__device__ __forceinline__ double dist2d(double ax, double ay, double bx, double by) {
+  const double dx = ax - bx, dy = ay - by;
+  return sqrt(dx * dx + dy * dy);  // np.linalg.norm of a 2-vector: sqrt(dx*dx + dy*dy)
+}
+
+// Motion graph of one env (utils.py:8-24 with self_loops=True, coverage.py:572-594):
+// every ordered target pair with 0 < |p_i - p_j| <= radius, in row-major order, which
+// per sender is ascending receiver order (what np.where returns in get_action_edges).
+__global__ __launch_bounds__(kCovThreads) void cov_graph_kernel(CovArgs a, const int32_t* envs, int n_envs_sel) {
+  __shared__ int scan[kCovThreads];
+  __shared__ int total_s;
+  const int e = blockIdx.x;
+  if (e >= n_envs_sel) return;
+  const int b = envs ? envs[e] : e;
+  const int R = a.R, M = a.M, Tm = a.Tmax, E = 4 * M;
+  const int T = a.ntg[b];
+  const double* tg = a.tgt + (size_t)b * Tm * 2;
+  int32_t* nbr = a.nbr + (size_t)b * Tm * 4;
+  int32_t* cnt = a.cnt + (size_t)b * Tm;
+  const int tid = threadIdx.x;
+  // 1. neighbour lists (<= 4 per node; more is the reference's "Increase MAX_EDGES")
+  for (int i = tid; i < T; i += kCovThreads) {
+    const double px = tg[2 * i], py = tg[2 * i + 1];
+    int c = 0;
+    for (int j = 0; j < T; ++j) {
+      const double d = dist2d(px, py, tg[2 * j], tg[2 * j + 1]);
+      if (d > 0.0 && d <= a.motion_radius) {
+        if (c < 4) nbr[4 * i + c] = j;
+        ++c;
+      }
+    }
+    if (c > 4) atomicOr(a.err, 1);
+    for (int k = c; k < 4; ++k) nbr[4 * i + k] = -1;
+    cnt[i] = c > 4 ? 4 : c;
+  }
+  __syncthreads();
+  // 2. exclusive scan of the degrees -> position of each node's edges in the list
+  const int per = (T + kCovThreads - 1) / kCovThreads;
+  const int i0 = tid * per, i1 = min(T, i0 + per);
+  int local = 0;
+  for (int i = i0; i < i1; ++i) local += cnt[i];
+  scan[tid] = local;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int k = 0; k < kCovThreads; ++k) {
+      const int v = scan[k];
+      scan[k] = run;
+      run += v;
+    }
+    total_s = run;
+  }
+  __syncthreads();
+  const int n_motion = total_s;
+  if (n_motion + 8 * R > E) atomicOr(a.err, 2);
+  int32_t* snd = a.senders + (size_t)b * E;
+  int32_t* rcv = a.receivers + (size_t)b * E;
+  float* edg = a.edges + (size_t)b * E;
+  // 3. static observation: motion edges, then -1 / 0 padding
+  int off = scan[tid];
+  for (int i = i0; i < i1; ++i) {
+    for (int k = 0; k < cnt[i]; ++k) {
+      const int j = nbr[4 * i + k];
+      snd[off] = i + R;
+      rcv[off] = j + R;
+      edg[off] = static_cast<float>(dist2d(tg[2 * i], tg[2 * i + 1], tg[2 * j], tg[2 * j + 1]));
+      ++off;
+    }
+  }
+  for (int k = n_motion + tid; k < E; k += kCovThreads) {
+    snd[k] = -1;
+    rcv[k] = -1;
+    edg[k] = 0.0f;
+  }
+  float* nodes = a.nodes + (size_t)b * M * 3;
+  for (int k = tid; k < M; k += kCovThreads) {
+    nodes[3 * k] = k < R ? 1.0f : 0.0f;
+    nodes[3 * k + 1] = (k >= R && k < R + T) ? 1.0f : 0.0f;
+    nodes[3 * k + 2] = 0.0f;
+  }
+  if (tid == 0) a.n_motion[b] = n_motion;
+}
+
+// Action targets of a robot on node c (global): its out-neighbours, padded with c.
+__device__ __forceinline__ int action_node(const int32_t* nbr, const int32_t* cnt, int c, int act, int R) {
+  const int t = c - R;
+  return act < cnt[t] ? nbr[4 * t + act] + R : c;
+}
+
+// One step (or, with a.actions == nullptr, the observation that reset() returns).
+__global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int R = a.R, M = a.M, Tm = a.Tmax, E = 4 * M;
+  const int T = a.ntg[b];
+  int* cur_s = reinterpret_cast<int*>(smem);          // R: node before the move
+  int* new_s = cur_s + R;                             // R: node after the move
+  int* chosen = new_s + R;                            // R: node the action points at
+  unsigned* claim = reinterpret_cast<unsigned*>(chosen + R);  // (M+31)/32 claim bits
+  unsigned* seen = claim + (M + 31) / 32;                      // visited-this-step bits
+  int* counter = reinterpret_cast<int*>(seen + (M + 31) / 32);
+  const int W = (M + 31) / 32;
+  const int tid = threadIdx.x;
+  const double* tg = a.tgt + (size_t)b * Tm * 2;
+  const int32_t* nbr = a.nbr + (size_t)b * Tm * 4;
+  const int32_t* cnt = a.cnt + (size_t)b * Tm;
+  double* xr = a.xr + (size_t)b * R * 2;
+  int32_t* cur = a.cur + (size_t)b * R;
+  uint8_t* vis = a.visited + (size_t)b * Tm;
+
+  for (int k = tid; k < W; k += kCovThreads) {
+    claim[k] = 0u;
+    seen[k] = 0u;
+  }
+  if (tid == 0) *counter = 0;
+  // closest_targets (:427-432): cached node unless the robots were placed externally
+  const bool dirty = a.dirty[b] != 0;
+  for (int i = tid; i < R; i += kCovThreads) {
+    int c = cur[i];
+    if (dirty) {
+      const double px = xr[2 * i], py = xr[2 * i + 1];
+      double best = __builtin_inf();
+      c = 0;
+      for (int j = 0; j < T; ++j) {
+        const double d = dist2d(px, py, tg[2 * j], tg[2 * j + 1]);
+        if (d < best) {  // strict: first index on ties, like np.argmin
+          best = d;
+          c = j;
+        }
+      }
+      c += R;
+    }
+    cur_s[i] = c;
+  }
+  __syncthreads();
+
+  if (a.actions) {
+    // step (:184-200): chosen node per robot; robots that stay claim first
+    const int32_t* act = a.actions + (size_t)b * R;
+    for (int i = tid; i < R; i += kCovThreads) {
+      int ai = act[i];
+      if (ai < 0 || ai >= 4) {
+        atomicOr(a.err, 4);
+        ai = 0;
+      }
+      const int c = cur_s[i];
+      const int n = action_node(nbr, cnt, c, ai, R);
+      chosen[i] = n;
+      if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
+    }
+    __syncthreads();
+    // then, in robot order, a move succeeds unless its node is already claimed; a
+    // blocked robot stays and its node joins the claims (serial in the reference too)
+    if (tid == 0) {
+      for (int i = 0; i < R; ++i) {
+        const int c = cur_s[i], n = chosen[i];
+        if (n == c) {
+          new_s[i] = c;
+          continue;
+        }
+        const unsigned bit = 1u << (n & 31);
+        if (!(claim[n >> 5] & bit)) {
+          claim[n >> 5] |= bit;
+          new_s[i] = n;
+        } else {
+          claim[c >> 5] |= 1u << (c & 31);
+          new_s[i] = c;
+        }
+      }
+    }
+    __syncthreads();
+  } else {
+    for (int i = tid; i < R; i += kCovThreads) new_s[i] = cur_s[i];
+    __syncthreads();
+  }
+
+  // move (:198) and visit (:265-266, :359): count nodes that flip to visited
+  float* nodes = a.nodes + (size_t)b * M * 3;
+  for (int i = tid; i < R; i += kCovThreads) {
+    const int n = new_s[i];
+    if (n != cur_s[i]) {  // a robot that does not move keeps its position (:198)
+      xr[2 * i] = tg[2 * (n - R)];
+      xr[2 * i + 1] = tg[2 * (n - R) + 1];
+    }
+    cur[i] = n;
+    const int t = n - R;
+    if (!vis[t]) {
+      const unsigned old = atomicOr(&seen[n >> 5], 1u << (n & 31));
+      if (!(old & (1u << (n & 31)))) {
+        vis[t] = 1;
+        nodes[3 * n + 2] = 0.0f;
+        atomicAdd(counter, 1);
+      }
+    }
+  }
+  __syncthreads();
+
+  // observation tail (:259-323): 4 action edges per robot, both directions
+  int32_t* snd = a.senders + (size_t)b * E;
+  int32_t* rcv = a.receivers + (size_t)b * E;
+  float* edg = a.edges + (size_t)b * E;
+  const int base = E - 8 * R;
+  for (int k = tid; k < 4 * R; k += kCovThreads) {
+    const int i = k >> 2, ac = k & 3;
+    const int c = new_s[i];
+    const int q = action_node(nbr, cnt, c, ac, R);
+    const float d = static_cast<float>(dist2d(xr[2 * i], xr[2 * i + 1], tg[2 * (q - R)], tg[2 * (q - R) + 1]) / a.res);
+    snd[base + k] = q;
+    snd[base + 4 * R + k] = i;
+    rcv[base + k] = i;
+    rcv[base + 4 * R + k] = q;
+    edg[base + k] = d;
+    edg[base + 4 * R + k] = d;
+  }
+  if (tid == 0) {
+    const int newly = *counter;
+    const int nv = a.nvisited[b] + newly;
+    a.nvisited[b] = nv;
+    const int sc = a.step_counter[b];
+    a.obs_step[b] = sc;
+    a.step_counter[b] = sc + 1;
+    a.reward[b] = static_cast<double>(newly);
+    a.done[b] = (sc + 1 == a.episode_length || nv == T) ? 1 : 0;
+    a.dirty[b] = 0;
+  }
+}
+
+// reset (:405-424 after the random draws): robots onto their start targets, the
+// unvisited flags, then the same observation pass as a step without actions.
+__global__ __launch_bounds__(kCovThreads) void cov_reset_kernel(CovArgs a, const int32_t* start,
+                                                                 const uint8_t* visited0) {
+  const int b = blockIdx.x;
+  const int R = a.R, M = a.M, Tm = a.Tmax;
+  const int T = a.ntg[b];
+  const double* tg = a.tgt + (size_t)b * Tm * 2;
+  __shared__ int count;
+  if (threadIdx.x == 0) count = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < R; i += kCovThreads) {
+    const int t = start[(size_t)b * R + i];
+    a.cur[(size_t)b * R + i] = t + R;
+    a.xr[((size_t)b * R + i) * 2] = tg[2 * t];
+    a.xr[((size_t)b * R + i) * 2 + 1] = tg[2 * t + 1];
+  }
+  float* nodes = a.nodes + (size_t)b * M * 3;
+  int local = 0;
+  for (int t = threadIdx.x; t < Tm; t += kCovThreads) {
+    const uint8_t v = t < T ? visited0[(size_t)b * Tm + t] : 1;
+    a.visited[(size_t)b * Tm + t] = v;
+    if (t < T) {
+      nodes[3 * (t + R) + 2] = v ? 0.0f : 1.0f;
+      local += v ? 1 : 0;
+    }
+  }
+  atomicAdd(&count, local);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.nvisited[b] = count;
+    a.step_counter[b] = 0;
+    a.dirty[b] = 0;
+  }
+}
+
+}  // namespace
+
+size_t cov_step_lds_bytes(int R, int M) { return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16; }
+
+hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {
+  hipLaunchKernelGGL(cov_graph_kernel, dim3(n), dim3(kCovThreads), 0, s, a, envs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_t* visited0, hipStream_t s) {
+  hipLaunchKernelGGL(cov_reset_kernel, dim3(a.B), dim3(kCovThreads), 0, s, a, start, visited0);
+  return hipGetLastError();
+}
+
+hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(cov_step_kernel, dim3(a.B), dim3(kCovThreads), cov_step_lds_bytes(a.R, a.M), s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gf

@@ -13,6 +13,7 @@ __version__ = "0.1.0"
 ENV_IDS = {
     "FlockingRelative-v0": ("gym_flock.envs.flocking:FlockingRelativeEnv", 1000),  # :95-99
     "Flocking-v0": ("gym_flock.envs.flocking:FlockingEnv", 1000),                  # :89-93
+    "Coverage-v0": ("gym_flock.envs.spatial:CoverageEnv", 75),                     # :76-80
 }
 
 if HAVE_GYM:  # pragma: no cover - gym is not installed in the build image

@@ -41,6 +41,17 @@ class FeBuffers(ctypes.Structure):
                 ("knn_obs", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
 
 
+class CovConfig(ctypes.Structure):
+    _fields_ = [("n_robots", ctypes.c_int32), ("n_envs", ctypes.c_int32),
+                ("max_nodes", ctypes.c_int32), ("episode_length", ctypes.c_int32),
+                ("res", ctypes.c_double), ("motion_radius", ctypes.c_double),
+                ("device", ctypes.c_int32)]
+
+
+COV_ACTIONS_DEVICE = 0x1
+COV_ACTIONS_RESIDENT = 0x2
+
+
 class GymFlockError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("libgymflock error %d: %s" % (code, msg))
@@ -77,6 +88,19 @@ SIGNATURES = {
     "fe_allgather_rewards": [_P],
     "fe_get_gathered_rewards": [_P, _P],
     "fe_comm_destroy": [_P],
+    "cov_create": [ctypes.POINTER(CovConfig), ctypes.POINTER(_P)],
+    "cov_destroy": [_P],
+    "cov_set_targets": [_P, _I, _I, _P],
+    "cov_reset": [_P, _P, _P],
+    "cov_step": [_P, _P, _I],
+    "cov_set_actions": [_P, _P],
+    "cov_set_robot_positions": [_P, _I, _P],
+    "cov_get_obs": [_P, _I, _P, _P, _P, _P, _P],
+    "cov_get_rewards": [_P, _P, _P],
+    "cov_get_robots": [_P, _I, _P, _P],
+    "cov_get_visited": [_P, _I, _P],
+    "cov_get_n_motion": [_P, _P],
+    "cov_sync": [_P],
     "fe_last_error": [],
     "fe_abi_version": [],
     "fe_diag": [_P, _I, _I, ctypes.POINTER(ctypes.c_double)],
@@ -286,3 +310,91 @@ class FlockHandle:
         out = np.empty(self.nranks * self.n_envs)
         check(self.lib.fe_get_gathered_rewards(self.h, ptr(out)))
         return out
+
+
+class CoverageHandle:
+    """Owns one cov_handle: B Coverage-v0 envs with R robots, max_nodes padded nodes."""
+
+    def __init__(self, n_robots, n_envs=1, max_nodes=500, episode_length=75, res=5.5,
+                 motion_radius=None, device=0):
+        self.lib = load()
+        if motion_radius is None:
+            motion_radius = res * 1.2
+        self.cfg = CovConfig(int(n_robots), int(n_envs), int(max_nodes), int(episode_length),
+                             float(res), float(motion_radius), int(device))
+        self.n_robots, self.n_envs, self.max_nodes = int(n_robots), int(n_envs), int(max_nodes)
+        self.t_max = self.max_nodes - self.n_robots
+        h = ctypes.c_void_p()
+        check(self.lib.cov_create(ctypes.byref(self.cfg), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cov_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def set_targets(self, targets, env=-1):
+        t = np.ascontiguousarray(targets, dtype=np.float64)
+        assert t.ndim == 2 and t.shape[1] == 2, t.shape
+        check(self.lib.cov_set_targets(self.h, int(env), int(t.shape[0]), ptr(t)))
+
+    def reset(self, start, visited):
+        """start: (B,R) target-local start nodes; visited: (B, max_nodes-R) 0/1."""
+        st = np.ascontiguousarray(start, dtype=np.int32)
+        vi = np.ascontiguousarray(visited, dtype=np.uint8)
+        assert st.shape == (self.n_envs, self.n_robots), st.shape
+        assert vi.shape == (self.n_envs, self.t_max), vi.shape
+        check(self.lib.cov_reset(self.h, ptr(st), ptr(vi)))
+
+    def step(self, actions=None, resident=False):
+        if resident:
+            check(self.lib.cov_step(self.h, None, COV_ACTIONS_RESIDENT))
+            return
+        a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
+        check(self.lib.cov_step(self.h, ptr(a), 0))
+
+    def set_actions(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
+        check(self.lib.cov_set_actions(self.h, ptr(a)))
+
+    def set_robot_positions(self, env, xr):
+        x = np.ascontiguousarray(xr, dtype=np.float64)
+        assert x.shape == (self.n_robots, 2)
+        check(self.lib.cov_set_robot_positions(self.h, int(env), ptr(x)))
+
+    def obs(self, env=0):
+        m = self.max_nodes
+        nodes = np.empty((m, 3), np.float32)
+        edges = np.empty((4 * m, 1), np.float32)
+        snd = np.empty(4 * m, np.int32)
+        rcv = np.empty(4 * m, np.int32)
+        step = np.empty((1, 1), np.int64)
+        check(self.lib.cov_get_obs(self.h, int(env), ptr(nodes), ptr(edges), ptr(snd), ptr(rcv), ptr(step)))
+        return {"nodes": nodes, "edges": edges, "senders": snd, "receivers": rcv, "step": step}
+
+    def rewards(self):
+        r = np.empty(self.n_envs)
+        d = np.empty(self.n_envs, np.uint8)
+        check(self.lib.cov_get_rewards(self.h, ptr(r), ptr(d)))
+        return r, d.astype(bool)
+
+    def robots(self, env=0):
+        x = np.empty((self.n_robots, 2))
+        n = np.empty(self.n_robots, np.int32)
+        check(self.lib.cov_get_robots(self.h, int(env), ptr(x), ptr(n)))
+        return x, n
+
+    def visited(self, env=0):
+        v = np.empty(self.t_max, np.uint8)
+        check(self.lib.cov_get_visited(self.h, int(env), ptr(v)))
+        return v
+
+    def n_motion(self):
+        n = np.empty(self.n_envs, np.int32)
+        check(self.lib.cov_get_n_motion(self.h, ptr(n)))
+        return n
+
+    def sync(self):
+        check(self.lib.cov_sync(self.h))

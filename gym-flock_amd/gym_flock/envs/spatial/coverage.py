@@ -1,0 +1,195 @@
+"""Coverage-v0 on the MI355X engine — drop-in for gym_flock/envs/spatial/coverage.py.
+
+Same constructor arguments, `keys`, spaces and methods as the reference
+(`__init__` :83-164, `seed` :166-172, `step` :174-204, `reset` :366-425,
+`closest_targets` :427-432, `controller(random=True)` :805-806). The step — action
+targets, collision-resolved moves, visited/reward and the padded graph observation —
+and the per-graph setup (motion radius graph, static observation) run in
+libgymflock.so (cov_* C-ABI). Host code keeps what the reference draws from its RNGs:
+the target map (global np.random, maps.generate_targets) and reset()'s start and
+unvisited draws (self.np_random), in the reference's call order.
+
+Supported configuration: the module constants the reference ships with (PAD_ACTIONS,
+COLLISION_CHECKS, PAD_NODES, distance edge features, HIDE_NODES False). Like the
+reference, observations alias buffers that the next step overwrites only in the sense
+that each call returns fresh host copies of the device arrays.
+"""
+import numpy as np
+
+from ... import _native as nat
+from ..._spaces import Box, Dict, Env, MultiDiscrete, np_random
+from .maps import generate_targets
+
+N_NODE_FEAT = 3
+N_EDGE_FEAT = 1
+N_GLOB_FEAT = 1
+MAX_NODES = 500
+MAX_EDGES = 4
+N_ACTIONS = 4
+EPISODE_LENGTH = 75
+HORIZON = 10
+N_ROBOTS = 6
+XMAX = 120
+YMAX = 120
+FRAC_ACTIVE = 0.5
+NEARBY_STARTS = True
+NEARBY_DENSITY = 5
+DELTA = 5.5
+unvisited_regions = [(-100, 100, -100, 100)]
+start_regions = [(-100, 100, -100, 100)]
+
+
+class CoverageEnv(Env):
+    def __init__(self, n_robots=N_ROBOTS, frac_active_targets=FRAC_ACTIVE, xmax=XMAX, ymax=YMAX,
+                 starts=start_regions, unvisiteds=unvisited_regions, init_graph=True,
+                 episode_length=EPISODE_LENGTH, res=DELTA, pad_nodes=True, max_nodes=MAX_NODES,
+                 nearby_starts=NEARBY_STARTS, horizon=HORIZON, hide_nodes=False,
+                 n_node_feat=N_NODE_FEAT, device=0):
+        super(CoverageEnv, self).__init__()
+        if hide_nodes or not pad_nodes or n_node_feat != N_NODE_FEAT:
+            raise NotImplementedError("only the reference's shipped configuration (PAD_NODES, no hidden nodes, "
+                                      "3 node features) is implemented")
+        self.keys = ['nodes', 'edges', 'senders', 'receivers', 'step']
+        self.n_node_feat = n_node_feat
+        self.hide_nodes = hide_nodes
+        self.horizon = horizon
+        self.episode_length = episode_length
+        self.nearby_starts = nearby_starts
+        self.pad_nodes = pad_nodes
+        self.max_nodes = max_nodes
+        self.x_min, self.x_max, self.y_min, self.y_max = -xmax, xmax, -ymax, ymax
+        self.res = res
+        self.start_ranges = starts
+        self.unvisited_ranges = unvisiteds
+        self.np_random = None
+        self.seed()
+        self.nx = 2
+        self.nu = 2
+        self.n_robots = n_robots
+        self.frac_active_targets = frac_active_targets
+        self.comm_radius = 100.0
+        self.motion_radius = self.res * 1.2
+        self.obs_radius = self.res * 1.2
+        self.n_actions = N_ACTIONS
+        self.device = device
+        self._h = nat.CoverageHandle(n_robots, 1, max_nodes, episode_length, res, self.motion_radius, device)
+        if init_graph:
+            targets, _ = self._generate_targets()
+            self._initialize_graph(targets)
+        self.episode_reward = 0
+        self.step_counter = 0
+        self.last_loc = None
+        self.fig = None
+
+    def seed(self, seed=None):
+        self.np_random, seed = np_random(seed)
+        return [seed]
+
+    # --------------------------------------------------------------- graph setup
+    def _generate_targets(self):
+        """coverage.py:516-527 (host, global np.random)."""
+        return generate_targets(self.x_max, self.y_max, self.res, self.motion_radius), True
+
+    def _initialize_graph(self, targets):
+        """coverage.py:529-619; the motion graph itself is built on the device."""
+        self.targets = np.asarray(targets, dtype=np.float64)
+        self.n_targets = self.targets.shape[0]
+        self.n_agents = self.n_targets + self.n_robots
+        self.max_edges = self.max_nodes * MAX_EDGES
+        self._h.set_targets(self.targets, env=0)
+        self.n_motion_edges = int(self._h.n_motion()[0])
+        if self.nearby_starts:
+            n_nearest = self.get_n_nearest(self.np_random.choice(self.n_targets), self.n_robots * NEARBY_DENSITY)
+            self.start_region = [i in n_nearest for i in range(self.n_targets)]
+        else:
+            self.start_region = [True] * self.n_targets
+        self.unvisited_region = [True] * self.n_targets
+        self.action_space = MultiDiscrete([self.n_actions] * self.n_robots)
+        self.observation_space = Dict([
+            ("nodes", Box(shape=(self.max_nodes, self.n_node_feat), low=-np.inf, high=np.inf, dtype=np.float32)),
+            ("edges", Box(shape=(self.max_edges, N_EDGE_FEAT), low=-np.inf, high=np.inf, dtype=np.float32)),
+            ("senders", Box(shape=(self.max_edges, 1), low=0, high=self.n_agents, dtype=np.float32)),
+            ("receivers", Box(shape=(self.max_edges, 1), low=0, high=self.n_agents, dtype=np.float32)),
+            ("step", Box(shape=(1, 1), low=0, high=EPISODE_LENGTH, dtype=np.float32)),
+        ])
+
+    @property
+    def motion_edges(self):
+        o = self._h.obs(0)
+        n = self.n_motion_edges
+        return o["senders"][:n].astype(np.int64), o["receivers"][:n].astype(np.int64)
+
+    def get_n_nearest(self, i, n):
+        """coverage.py:655-673: grow a node set through the motion graph until it holds n."""
+        s, q = self.motion_edges
+        s, q = s - self.n_robots, q - self.n_robots
+        n_nearest = {i}
+        while len(n_nearest) < n:
+            n_nearest = n_nearest.union(set(q[np.isin(s, list(n_nearest))].tolist()))
+        return n_nearest
+
+    # --------------------------------------------------------------------- API
+    def reset(self):
+        """coverage.py:366-425."""
+        self.episode_reward = 0
+        self.step_counter = 0
+        self.last_loc = None
+        targets, graph_changed = self._generate_targets()
+        if graph_changed:
+            self._initialize_graph(targets)
+        starts = self.np_random.choice(np.arange(self.n_targets)[self.start_region], size=(self.n_robots,),
+                                       replace=False)
+        unvisited = np.arange(self.n_targets)[self.unvisited_region] + self.n_robots
+        drop = self.np_random.choice(unvisited, size=(int(len(unvisited) * self.frac_active_targets),),
+                                     replace=False)
+        visited = np.ones((1, self._h.t_max), np.uint8)
+        visited[0, drop - self.n_robots] = 0
+        self._h.reset(starts[None], visited)
+        self.step_counter = 1
+        return self._h.obs(0)
+
+    def step(self, action):
+        """coverage.py:174-204."""
+        if action is not None:
+            a = np.asarray(action).reshape(-1)
+            if a.shape[0] != self.n_robots or np.any((a < 0) | (a >= self.n_actions)):
+                raise IndexError("each robot's action must be in [0, %d)" % self.n_actions)
+            self.last_loc = self.closest_targets
+            self._h.step(a[None])
+        else:
+            self._h.step(np.zeros((1, self.n_robots)))  # pragma: no cover
+        obs = self._h.obs(0)
+        r, d = self._h.rewards()
+        reward, done = float(r[0]), bool(d[0])
+        self.step_counter += 1
+        self.episode_reward += reward
+        return obs, reward, done, {}
+
+    @property
+    def closest_targets(self):
+        """coverage.py:427-432 (global node indices)."""
+        return self._h.robots(0)[1].astype(np.int64)
+
+    @property
+    def x(self):
+        xr, _ = self._h.robots(0)
+        return np.vstack([xr, self.targets])
+
+    @property
+    def visited(self):
+        return np.r_[np.ones(self.n_robots), self._h.visited(0)[:self.n_targets]].reshape(-1, 1)
+
+    def controller(self, random=False, greedy=False, reset_solution=False):
+        """coverage.py:800-806 (random branch). The greedy/VRP experts are not on the
+        step hot path."""
+        if random:
+            return self.np_random.choice(self.n_actions, size=(self.n_robots, 1))
+        raise NotImplementedError("greedy / VRP expert controllers are not implemented yet")
+
+    def render(self, mode='human'):
+        pass
+
+    def close(self):
+        if self._h is not None:
+            self._h.close()
+            self._h = None

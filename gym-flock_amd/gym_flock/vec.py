@@ -100,3 +100,58 @@ class VecFlockingRelative:
 
     def close(self):
         self.h.close()
+
+
+class VecCoverage:
+    """B Coverage-v0 envs (R robots each) on one GPU, one workgroup per env.
+
+    Each env gets its own target graph (set_targets(env=b)) or all share one
+    (env=-1); reset() draws starts and the unvisited set per env from
+    np.random.RandomState(seed + env_offset + b) in the reference's order.
+    """
+
+    def __init__(self, n_envs, n_robots, max_nodes=1000, episode_length=75, res=5.5,
+                 frac_active_targets=0.5, device=0, env_offset=0):
+        self.n_envs, self.n_robots = int(n_envs), int(n_robots)
+        self.frac = frac_active_targets
+        self.env_offset = int(env_offset)
+        self.h = nat.CoverageHandle(n_robots, n_envs, max_nodes, episode_length, res, None, device)
+        self.n_targets = np.zeros(self.n_envs, np.int64)
+
+    def set_targets(self, targets, env=-1):
+        self.h.set_targets(targets, env)
+        if env < 0:
+            self.n_targets[:] = len(targets)
+        else:
+            self.n_targets[env] = len(targets)
+
+    def reset(self, seed=0):
+        R, tmax = self.n_robots, self.h.t_max
+        start = np.empty((self.n_envs, R), np.int32)
+        visited = np.ones((self.n_envs, tmax), np.uint8)
+        for b in range(self.n_envs):
+            rs = np.random.RandomState(seed + self.env_offset + b)
+            T = int(self.n_targets[b])
+            start[b] = rs.choice(np.arange(T), size=(R,), replace=False)
+            drop = rs.choice(np.arange(T) + R, size=(int(T * self.frac),), replace=False)
+            visited[b, drop - R] = 0
+        self.h.reset(start, visited)
+        return start, visited
+
+    def step(self, actions=None, resident=False):
+        self.h.step(actions, resident)
+
+    def set_actions(self, actions):
+        self.h.set_actions(actions)
+
+    def rewards(self):
+        return self.h.rewards()
+
+    def obs(self, env=0):
+        return self.h.obs(env)
+
+    def sync(self):
+        self.h.sync()
+
+    def close(self):
+        self.h.close()

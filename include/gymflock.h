@@ -133,6 +133,48 @@ int fe_allgather_rewards(fe_handle* h);
 int fe_get_gathered_rewards(fe_handle* h, double* dst);
 int fe_comm_destroy(fe_handle* h);
 
+/* ============================ Coverage-v0 ==================================== */
+/* gym_flock/envs/spatial/coverage.py. B envs of n_robots robots moving on a per-env
+ * target graph (at most max_nodes - n_robots targets). Node indices are global as in
+ * the reference: robots 0..R-1, targets R..R+T-1. */
+typedef struct cov_config {
+  int32_t n_robots;        /* R (coverage.py:83, N_ROBOTS=6; config 4 uses 200)        */
+  int32_t n_envs;          /* B                                                         */
+  int32_t max_nodes;       /* padded node count (MAX_NODES :55; config 4 uses 1000)     */
+  int32_t episode_length;  /* 75 (EPISODE_LENGTH :64)                                   */
+  double res;              /* lattice spacing, edge-feature scale (DELTA 5.5, :80)       */
+  double motion_radius;    /* res * 1.2 (:136)                                          */
+  int32_t device;
+} cov_config;
+
+typedef struct cov_handle cov_handle;
+
+#define COV_ACTIONS_DEVICE   0x1 /* actions is a device pointer                          */
+#define COV_ACTIONS_RESIDENT 0x2 /* use the actions last given to cov_set_actions        */
+
+int cov_create(const cov_config* cfg, cov_handle** out);        /* CoverageEnv.__init__ :83 */
+int cov_destroy(cov_handle* h);
+/* Targets of one env (env < 0: every env) and its motion graph + static observation
+ * (_initialize_graph :529-594, utils._get_graph_edges :8-24), built on the device. */
+int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets);
+/* reset() after its random draws (:405-424): start[B][R] target-local start nodes,
+ * visited[B][max_nodes-R] (1 = visited); computes reset's observation (:424). */
+int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited);
+/* step(action) (:174-204, :234-364): actions[B][R] in [0,4). */
+int cov_step(cov_handle* h, const int32_t* actions, int flags);
+int cov_set_actions(cov_handle* h, const int32_t* actions);
+/* Place one env's robots anywhere (x[:R] = ...); closest targets are recomputed. */
+int cov_set_robot_positions(cov_handle* h, int env, const double* xr);
+/* Observation of one env (:353): nodes (M,3) f32, edges (4M) f32, senders/receivers
+ * (4M) i32, step; any pointer may be NULL. */
+int cov_get_obs(cov_handle* h, int env, float* nodes, float* edges, int32_t* senders, int32_t* receivers,
+                int64_t* step);
+int cov_get_rewards(cov_handle* h, double* reward, uint8_t* done);   /* (B), (B) */
+int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes); /* closest_targets :427 */
+int cov_get_visited(cov_handle* h, int env, uint8_t* visited);
+int cov_get_n_motion(cov_handle* h, int32_t* n_motion);
+int cov_sync(cov_handle* h);
+
 /* Diagnostics ---------------------------------------------------------------- */
 const char* fe_last_error(void);
 int fe_abi_version(void);

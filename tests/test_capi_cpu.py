@@ -16,12 +16,13 @@ HEADER = os.path.join(ROOT, "include", "gymflock.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(fe_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+((?:fe|cov)_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_declares_the_abi():
     syms = declared_symbols()
-    for s in ("fe_create", "fe_step", "fe_controller", "fe_get_network", "fe_allgather_rewards"):
+    for s in ("fe_create", "fe_step", "fe_controller", "fe_get_network", "fe_allgather_rewards",
+              "cov_create", "cov_step", "cov_reset", "cov_get_obs"):
         assert s in syms
 
 
@@ -138,3 +139,29 @@ def test_shard_range_partitions_the_batch():
         assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_range(10, 2, 2)
+
+
+def test_coverage_map_generation_matches_reference():
+    """Host map generation (maps.py) reproduces the reference's target sets from the same
+    global seeds (coverage.py:516-527, make_map.py:30-67, :207-231)."""
+    from conftest import GOLDEN
+    from gym_flock.envs.spatial.maps import generate_targets, square_lattice
+    f = np.load(os.path.join(GOLDEN, "coverage_maps.npz"))
+    np.testing.assert_array_equal(square_lattice(-120, 120, -120, 120, 5.5), f["lattice"])
+    for s in (0, 1, 2):
+        np.random.seed(s)
+        np.testing.assert_array_equal(generate_targets(), f["targets_seed%d" % s])
+    for path in ("coverage_r6_random.npz", "coverage_r6_greedy.npz", "coverage_r200_random.npz"):
+        g = np.load(os.path.join(GOLDEN, path))
+        np.random.seed({"coverage_r6_random.npz": 3, "coverage_r6_greedy.npz": 5,
+                        "coverage_r200_random.npz": 8}[path])
+        np.testing.assert_array_equal(generate_targets(), g["targets"])
+
+
+def test_coverage_create_validates_arguments():
+    from gym_flock import _native as nat
+    lib = nat.load()
+    h = ctypes.c_void_p()
+    for cfg in (nat.CovConfig(0, 1, 500, 75, 5.5, 6.6, 0), nat.CovConfig(6, 1, 6, 75, 5.5, 6.6, 0),
+                nat.CovConfig(6, 0, 500, 75, 5.5, 6.6, 0), nat.CovConfig(6, 1, 500, 75, -1.0, 6.6, 0)):
+        assert lib.cov_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.GF_EINVAL

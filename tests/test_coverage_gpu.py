@@ -1,0 +1,147 @@
+"""Parity of the HIP Coverage-v0 path with the reference's recorded episodes and the
+CPU oracle, through the C-ABI. Integer outputs (nodes, senders/receivers, step,
+rewards, done, robot nodes, visited) and the float32 edge features are compared
+bit-exactly. Needs an MI355X."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import coverage as oc
+
+pytestmark = pytest.mark.gpu
+
+nat = pytest.importorskip("gym_flock._native")
+from gym_flock.vec import VecCoverage  # noqa: E402
+
+EPISODES = sorted(glob.glob(os.path.join(GOLDEN, "coverage_r*.npz")))
+
+
+def assert_obs(o, f, t=None):
+    get = (lambda k: f[k + "0"]) if t is None else (lambda k: f[k][t])
+    np.testing.assert_array_equal(o["nodes"], get("nodes"))
+    np.testing.assert_array_equal(o["edges"], get("edges"))
+    np.testing.assert_array_equal(o["senders"], get("senders"))
+    np.testing.assert_array_equal(o["receivers"], get("receivers"))
+    np.testing.assert_array_equal(o["step"], get("step"))
+
+
+@pytest.mark.parametrize("path", EPISODES, ids=os.path.basename)
+def test_episode_matches_reference_golden(path):
+    f = np.load(path)
+    R, T, M = int(f["n_robots"]), int(f["n_targets"]), int(f["max_nodes"])
+    h = nat.CoverageHandle(R, 1, M)
+    h.set_targets(f["targets"], env=0)
+    assert h.n_motion()[0] == len(f["motion_senders"])
+    start = oc.closest_targets(f["x0"][:R], f["targets"], R) - R
+    visited = np.ones((1, M - R), np.uint8)
+    visited[0, :T] = f["visited0"][R:].astype(np.uint8)
+    h.reset(start[None], visited)
+    assert_obs(h.obs(0), f)
+    for t in range(len(f["actions"])):
+        h.step(f["actions"][t][None])
+        assert_obs(h.obs(0), f, t)
+        r, d = h.rewards()
+        assert r[0] == f["reward"][t] and d[0] == f["done"][t]
+        xr, nodes = h.robots(0)
+        np.testing.assert_array_equal(xr, f["xr"][t])
+        np.testing.assert_array_equal(nodes, f["closest"][t])
+        np.testing.assert_array_equal(h.visited(0)[:T], f["visited"][t][R:])
+    h.close()
+
+
+def test_batched_envs_with_distinct_graphs_vs_oracle():
+    """4 envs, each its own map and random actions, 20 steps against the oracle."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, R, M = 4, 12, 600
+    maps = []
+    for b in range(B):
+        np.random.seed(100 + b)
+        maps.append(generate_targets())
+    v = VecCoverage(B, R, max_nodes=M)
+    for b in range(B):
+        v.set_targets(maps[b], env=b)
+    start, visited = v.reset(seed=5)
+    orcs = []
+    for b in range(B):
+        o = oc.CoverageOracle(maps[b], R, M)
+        T = len(maps[b])
+        obs0 = o.reset(start[b], np.nonzero(visited[b, :T] == 0)[0] + R)
+        assert_obs(v.obs(b), {k + "0": val for k, val in obs0.items()})
+        orcs.append(o)
+    rs = np.random.RandomState(0)
+    for t in range(20):
+        acts = rs.randint(0, 4, size=(B, R))
+        v.step(acts)
+        r, d = v.rewards()
+        for b in range(B):
+            obs, rr, dd = orcs[b].step(acts[b])
+            assert_obs(v.obs(b), {k + "0": val for k, val in obs.items()})
+            assert r[b] == rr and d[b] == dd
+    v.close()
+
+
+def test_collisions_and_blocking_order():
+    """Crowded start (robots on adjacent nodes of a small grid) so that moves collide:
+    stays claim first, then index order decides, blocked robots stay (:187-200)."""
+    xs, ys = np.meshgrid(np.arange(6) * 5.5, np.arange(6) * 5.5)
+    targets = np.stack([ys.ravel(), xs.ravel()], axis=1)
+    R, M = 10, 200
+    h = nat.CoverageHandle(R, 1, M)
+    h.set_targets(targets, env=0)
+    o = oc.CoverageOracle(targets, R, M)
+    start = np.arange(R)
+    visited = np.zeros((1, M - R), np.uint8)
+    h.reset(start[None], visited)
+    o.reset(start, np.arange(len(targets)) + R)
+    rs = np.random.RandomState(3)
+    for t in range(40):
+        a = rs.randint(0, 4, size=R)
+        h.step(a[None])
+        obs, rr, dd = o.step(a)
+        assert_obs(h.obs(0), {k + "0": val for k, val in obs.items()})
+        np.testing.assert_array_equal(h.robots(0)[1], o.closest())
+        assert h.rewards()[0][0] == rr
+    h.close()
+
+
+def test_external_robot_positions_recompute_closest():
+    f = np.load(EPISODES[0])
+    R, M = int(f["n_robots"]), int(f["max_nodes"])
+    h = nat.CoverageHandle(R, 1, M)
+    h.set_targets(f["targets"], env=0)
+    o = oc.CoverageOracle(f["targets"], R, M)
+    start = np.arange(R) * 7
+    h.reset(start[None], np.ones((1, M - R), np.uint8))
+    o.reset(start, [])
+    xr = f["targets"][start] + np.random.RandomState(1).uniform(-2.0, 2.0, size=(R, 2))
+    h.set_robot_positions(0, xr)
+    o.xr = xr.copy()
+    a = np.random.RandomState(2).randint(0, 4, size=R)
+    h.step(a[None])
+    obs, rr, dd = o.step(a)
+    assert_obs(h.obs(0), {k + "0": val for k, val in obs.items()})
+    np.testing.assert_array_equal(h.robots(0)[0], o.xr)
+    h.close()
+
+
+def test_env_api_reproduces_reference_reset_and_episode():
+    """CoverageEnv with the fixture's seeds regenerates the reference's map, starts and
+    unvisited set (global and env RNGs in the reference's call order)."""
+    from gym_flock.envs.spatial import CoverageEnv
+    f = np.load(os.path.join(GOLDEN, "coverage_r6_random.npz"))
+    np.random.seed(3)
+    env = CoverageEnv(n_robots=6, nearby_starts=False, max_nodes=500)
+    env.seed(4)
+    np.random.seed(3)
+    obs = env.reset()
+    assert_obs(obs, f)
+    for t in range(len(f["actions"])):
+        obs, r, d, _ = env.step(f["actions"][t].reshape(-1, 1))
+        assert_obs(obs, f, t)
+        assert r == f["reward"][t] and d == f["done"][t]
+    with pytest.raises(IndexError):
+        env.step(np.full((6, 1), 4))
+    env.close()
