@@ -108,7 +108,7 @@ class CoverageOracle:
         start_targets (target-local), unvisited_targets (global) are unvisited."""
         self.xr = self.targets[np.asarray(start_targets)].copy()
         self.visited = np.ones(self.n_agents)
-        self.visited[np.asarray(unvisited_targets)] = 0
+        self.visited[np.asarray(unvisited_targets, dtype=np.int64)] = 0
         self.step_counter = 0
         return self._obs_reward()[0]
 

@@ -109,11 +109,11 @@ def test_collisions_and_blocking_order():
 
 def test_external_robot_positions_recompute_closest():
     f = np.load(EPISODES[0])
-    R, M = int(f["n_robots"]), int(f["max_nodes"])
+    R, T, M = int(f["n_robots"]), int(f["n_targets"]), int(f["max_nodes"])
     h = nat.CoverageHandle(R, 1, M)
     h.set_targets(f["targets"], env=0)
     o = oc.CoverageOracle(f["targets"], R, M)
-    start = np.arange(R) * 7
+    start = np.arange(R) * (T // R)
     h.reset(start[None], np.ones((1, M - R), np.uint8))
     o.reset(start, [])
     xr = f["targets"][start] + np.random.RandomState(1).uniform(-2.0, 2.0, size=(R, 2))
