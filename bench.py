@@ -76,8 +76,68 @@ def load_traffic(n_agents, n_envs):
         return None
 
 
+def coverage_cpu_baseline(targets, n_robots, max_nodes, seconds):
+    """The oracle's NumPy Coverage step (one core) on one env of the same workload."""
+    from oracle import coverage as oc
+    rs = np.random.RandomState(0)
+    o = oc.CoverageOracle(targets, n_robots, max_nodes)
+    T = len(targets)
+    o.reset(rs.choice(T, n_robots, replace=False), rs.choice(T, T // 2, replace=False) + n_robots)
+    acts = rs.randint(0, 4, size=(n_robots,))
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        o.step(acts)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and steps >= 3:
+            break
+    return {"value": n_robots * steps / el, "unit": "robot-steps/s", "cores": 1, "kind": "port",
+            "sample": "oracle/coverage.py step() (NumPy, 1 thread) on 1 env, R=%d, T=%d, %d steps (%.1f s)"
+                      % (n_robots, T, steps, el)}
+
+
+def bench_coverage(args):
+    """BASELINE.json configs[3]: Coverage-v0, 200 robots on a ~550-target map, 512 envs,
+    max_nodes 1000 (the reference needs nearby_starts=False and max_nodes=1000 at this
+    size, SURVEY.md finding 7). All envs share one generated map (global seed 8);
+    starts, unvisited sets and actions differ per env; actions stay resident in HBM."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    from gym_flock.vec import VecCoverage
+    R, B, M, K, W = 200, args.n_envs if args.n_envs != 256 else 512, 1000, args.steps, args.warmup
+    np.random.seed(8)
+    targets = generate_targets()
+    v = VecCoverage(B, R, max_nodes=M, episode_length=10 ** 9)
+    v.set_targets(targets)
+    v.reset(seed=0)
+    v.set_actions(np.random.RandomState(7).randint(0, 4, size=(B, R)))
+    for _ in range(W):
+        v.step(resident=True)
+    v.sync()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        v.step(resident=True)
+    v.sync()
+    el = time.perf_counter() - t0
+    per_env = 8 * R * 12 + R * (16 + 4 + 4 + 4 + 16) + 16
+    line = {"metric": "robot-steps/sec (N_robots x N_envs x steps/s), Coverage-v0 R=200",
+            "value": R * B * K / el, "unit": "robot-steps/s", "n_gpus": 1, "steps": K, "warmup": W,
+            "ms_per_step": 1e3 * el / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic (generated map, random starts/unvisited/actions)",
+            "config": {"workload": "Coverage-v0 step(), R=200 robots, T=%d targets, max_nodes %d, %d envs "
+                                   "(BASELINE.json configs[3])" % (len(targets), M, B)},
+            "roofline": {"bound": "latency", "note": "one workgroup per env; the collision pass is serial "
+                         "in robot order like the reference", "achieved": B * per_env / (el / K) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B * per_env / (el / K) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": None}}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = coverage_cpu_baseline(targets, R, M, min(args.cpu_seconds, 8.0))
+    print(json.dumps(line), flush=True)
+    v.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["flocking", "coverage"], default="flocking")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -87,13 +147,18 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-controller-line", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the multi-rank path (gloo rendezvous + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
+    if args.workload == "coverage":
+        return bench_coverage(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    multi = world > 1 or args.force_dist
+    if multi:
         import torch.distributed as dist  # CPU (gloo) only: rendezvous, barrier, max
         dist.init_process_group("gloo")
 
@@ -107,7 +172,7 @@ def main():
     u = np.random.RandomState(1234 + rank).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
     env.set_actions(u)
     gather = None
-    if world > 1:
+    if multi:
         uid = [env.h.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         gather = RcclRewardGather(env.h, world, rank, uid[0])
