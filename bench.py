@@ -143,7 +143,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n-agents", type=int, default=1024)
     ap.add_argument("--n-envs", type=int, default=256, help="envs per GPU")
-    ap.add_argument("--metrics-every", type=int, default=1, help="reward all-gather period (N>1)")
+    ap.add_argument("--metrics-every", type=int, default=8,
+                    help="steps per reward all-gather (N>1); each collective carries all those steps")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-controller-line", action="store_true")
@@ -210,9 +211,10 @@ def main():
 
     extra = {}
     if gather is not None:
-        allr = gather.result()
+        gather.issue()  # one all-gather after the timed region, checked against the local rewards
+        allr = gather.result()  # (steps, world*B), the last row is the latest step
         mine = env.rewards()
-        extra["gathered_rewards_ok"] = bool(np.array_equal(allr[rank * B:(rank + 1) * B], mine))
+        extra["gathered_rewards_ok"] = bool(np.array_equal(allr[-1, rank * B:(rank + 1) * B], mine))
 
     # closed-loop step + fused controller (u = previous controller output), same workload
     if not args.no_controller_line:

@@ -30,7 +30,11 @@ int fail_hip(const char* what, hipError_t e) {
     if (e_ != hipSuccess) return fail_hip(#expr, e_);       \
   } while (0)
 
-constexpr int kRewardSlots = 8;  // reward ring: step t writes slot t % 8
+// Reward ring: step t writes slot t % 16. The metrics all-gather ships one block of
+// up to 8 consecutive steps at a time while the steps fill the other block.
+constexpr int kRewardSlots = 16;
+constexpr int kGatherBlock = 8;
+constexpr int kBlocks = kRewardSlots / kGatherBlock;
 
 }  // namespace
 
@@ -70,12 +74,12 @@ struct fe_handle {
   // RCCL metrics path
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  double* gather = nullptr;             // kRewardSlots x nranks x B
+  double* gather = nullptr;             // kBlocks x nranks x kGatherBlock x B
   hipEvent_t step_ev = nullptr;
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
-  hipEvent_t ag_ev[kRewardSlots] = {};
-  bool ag_pending[kRewardSlots] = {};
-  int last_gather = -1;
+  hipEvent_t ag_ev[kBlocks] = {};
+  bool ag_pending[kBlocks] = {};
+  int last_gather = -1, last_count = 0;
 };
 
 namespace {
@@ -127,9 +131,10 @@ double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h-
 // still be reading that slot, order the stream behind it (a device-side wait).
 int next_reward_slot(fe_handle* h) {
   h->rslot = (h->rslot + 1) % kRewardSlots;
-  if (h->ag_pending[h->rslot]) {
-    GF_HIP(hipStreamWaitEvent(h->stream, h->ag_ev[h->rslot], 0));
-    h->ag_pending[h->rslot] = false;
+  const int blk = h->rslot / kGatherBlock;
+  if (h->rslot % kGatherBlock == 0 && h->ag_pending[blk]) {  // re-entering a gathered block
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ag_ev[blk], 0));
+    h->ag_pending[blk] = false;
   }
   return GF_OK;
 }
@@ -601,7 +606,7 @@ int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
   GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
   GF_HIP(hipEventCreateWithFlags(&h->step_ev, hipEventDisableTiming));
   for (auto& e : h->ag_ev) GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (int rc = dalloc(&h->gather, (size_t)kRewardSlots * nranks * h->cfg.n_envs)) return rc;
+  if (int rc = dalloc(&h->gather, (size_t)kBlocks * nranks * kGatherBlock * h->cfg.n_envs)) return rc;
   return GF_OK;
 }
 
@@ -609,16 +614,19 @@ int fe_allgather_rewards(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->comm) return fail(GF_ESTATE, "fe_comm_init not called");
   if (int rc = use_dev(h)) return rc;
-  const int s = h->rslot;
   const size_t B = h->cfg.n_envs;
+  const int blk = h->rslot / kGatherBlock;
+  const int count = h->rslot % kGatherBlock + 1;  // steps of this block written so far
+  const double* src = h->reward_ring + (size_t)blk * kGatherBlock * B;
+  double* dst = h->gather + (size_t)blk * h->nranks * kGatherBlock * B;
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
   GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
-  ncclResult_t r = ncclAllGather(cur_reward(h), h->gather + (size_t)s * h->nranks * B, B, ncclFloat64, h->comm,
-                                 h->comm_stream);
+  ncclResult_t r = ncclAllGather(src, dst, (size_t)count * B, ncclFloat64, h->comm, h->comm_stream);
   if (r != ncclSuccess) return fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-  GF_HIP(hipEventRecord(h->ag_ev[s], h->comm_stream));
-  h->ag_pending[s] = true;
-  h->last_gather = s;
+  GF_HIP(hipEventRecord(h->ag_ev[blk], h->comm_stream));
+  h->ag_pending[blk] = true;
+  h->last_gather = blk;
+  h->last_count = count;
   return GF_OK;
 }
 
@@ -626,11 +634,14 @@ int fe_get_gathered_rewards(fe_handle* h, double* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
   if (h->last_gather < 0) return fail(GF_ESTATE, "no all-gather issued");
   if (int rc = use_dev(h)) return rc;
-  const size_t n = (size_t)h->nranks * h->cfg.n_envs;
+  const size_t n = (size_t)h->nranks * h->last_count * h->cfg.n_envs;
   GF_HIP(hipEventSynchronize(h->ag_ev[h->last_gather]));
-  GF_HIP(hipMemcpy(dst, h->gather + (size_t)h->last_gather * n, n * 8, hipMemcpyDeviceToHost));
+  GF_HIP(hipMemcpy(dst, h->gather + (size_t)h->last_gather * h->nranks * kGatherBlock * h->cfg.n_envs, n * 8,
+                   hipMemcpyDeviceToHost));
   return GF_OK;
 }
+
+int fe_gathered_steps(fe_handle* h) { return h ? h->last_count : 0; }
 
 int fe_comm_destroy(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");

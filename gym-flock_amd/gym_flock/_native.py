@@ -87,6 +87,7 @@ SIGNATURES = {
     "fe_comm_init": [_P, _I, _I, _P],
     "fe_allgather_rewards": [_P],
     "fe_get_gathered_rewards": [_P, _P],
+    "fe_gathered_steps": [_P],
     "fe_comm_destroy": [_P],
     "cov_create": [ctypes.POINTER(CovConfig), ctypes.POINTER(_P)],
     "cov_destroy": [_P],
@@ -121,7 +122,13 @@ def load(path=None):
         raise ImportError("libgymflock.so not found at %s: build it with "
                           "`python -c 'import __graft_entry__ as g; g.build()'` "
                           "(or make -C gym-flock_amd/csrc)" % p)
-    lib = ctypes.CDLL(p)
+    # RTLD_DEEPBIND: resolve the library's HIP/RCCL symbols against its own ROCm
+    # dependencies even when another copy of the HIP runtime (e.g. PyTorch's bundled
+    # one) is already in the process' global scope. GYMFLOCK_DEEPBIND=0 disables it.
+    mode = ctypes.DEFAULT_MODE
+    if os.environ.get("GYMFLOCK_DEEPBIND", "1") != "0":
+        mode |= os.RTLD_DEEPBIND
+    lib = ctypes.CDLL(p, mode=mode)
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -307,9 +314,11 @@ class FlockHandle:
         check(self.lib.fe_allgather_rewards(self.h))
 
     def gathered_rewards(self):
-        out = np.empty(self.nranks * self.n_envs)
+        """(nranks, steps, B) rewards of the steps covered by the latest all-gather."""
+        steps = self.lib.fe_gathered_steps(self.h)
+        out = np.empty((self.nranks, max(steps, 1), self.n_envs))
         check(self.lib.fe_get_gathered_rewards(self.h, ptr(out)))
-        return out
+        return out[:, :steps]
 
 
 class CoverageHandle:

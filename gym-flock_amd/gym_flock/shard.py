@@ -27,7 +27,11 @@ def shard_range(total_envs, world_size, rank):
 
 
 class RcclRewardGather:
-    """All-gather of per-env rewards with RCCL (equal shard sizes on every rank)."""
+    """All-gather of per-env rewards with RCCL (equal shard sizes on every rank).
+
+    issue() after a step enqueues one collective for the steps since the start of the
+    current 8-step block (call it every 8 steps to ship each step's rewards once);
+    result() returns them as (steps, world * B) in global env order."""
 
     def __init__(self, handle, world_size, rank, unique_id):
         self.handle = handle
@@ -37,7 +41,8 @@ class RcclRewardGather:
         self.handle.allgather_rewards()
 
     def result(self):
-        return self.handle.gathered_rewards()
+        g = self.handle.gathered_rewards()  # (world, steps, B)
+        return np.concatenate(list(g), axis=1)
 
 
 class GlooRewardGather:

@@ -127,10 +127,14 @@ int fe_sync(fe_handle* h);
  * stream, so the collective never sits on the step critical path. */
 int fe_comm_unique_id(uint8_t id[128]);
 int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]);
-/* Enqueue an all-gather of the current per-env rewards into slot (call k % 8). */
+/* Enqueue (side stream, after the latest step) an all-gather of the per-env rewards of
+ * the steps since the start of the current 8-step block: one collective per 8 steps
+ * carries every step's rewards. */
 int fe_allgather_rewards(fe_handle* h);
-/* Wait for the latest all-gather and copy its (nranks*B) rewards to dst. */
+/* Wait for the latest all-gather; dst gets (nranks, steps, B) rewards, rank-major,
+ * steps = fe_gathered_steps(h) (oldest first). */
 int fe_get_gathered_rewards(fe_handle* h, double* dst);
+int fe_gathered_steps(fe_handle* h);
 int fe_comm_destroy(fe_handle* h);
 
 /* ============================ Coverage-v0 ==================================== */
