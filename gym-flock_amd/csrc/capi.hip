@@ -64,6 +64,7 @@ struct fe_handle {
   int u_resident_f64 = -1;              // dtype of the resident actions (-1: none)
   bool has_state = false, has_ctrl = false, has_obs = false, has_knn = false;
   int R = 0, T = 0, bpe = 0;
+  int resident = 0, spe = 1, rps = 0;  // env-resident kernel geometry
   size_t BN = 0;
   // kernel timing (bench roofline)
   int diag = 0;                         // ablation switches for every step launch
@@ -152,6 +153,9 @@ gf::StepArgs base_args(fe_handle* h) {
   a.R = h->R;
   a.T = h->T;
   a.bpe = h->bpe;
+  a.resident = h->resident;
+  a.spe = h->spe;
+  a.rps = h->rps;
   a.mean_pooling = h->cfg.mean_pooling;
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
@@ -234,6 +238,20 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   if (const char* e = getenv("GYMFLOCK_ROWS")) {
     const int r = atoi(e);
     if (r >= 4 && r <= 64 && (r & (r - 1)) == 0) h->R = r;
+  }
+  // env-resident kernel (opt-in, GYMFLOCK_RESIDENT=1, N <= 1024): measured 226-234 us vs
+  // 213-217 us for the tiled kernel at 256 x 1024, so off by default.
+  // GYMFLOCK_RESIDENT_WGS sets its target workgroup count (default 3 per CU).
+  h->resident = 0;
+  if (const char* e = getenv("GYMFLOCK_RESIDENT")) h->resident = atoi(e) != 0 && cfg->n_agents <= gf::kResidentMax;
+  {
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
+      cus = prop.multiProcessorCount;
+    int target = 3 * cus;
+    if (const char* e = getenv("GYMFLOCK_RESIDENT_WGS")) target = atoi(e) > 0 ? atoi(e) : target;
+    gf::step_resident_geometry(cfg->n_agents, cfg->n_envs, target, &h->spe, &h->rps);
   }
   if (const char* e = getenv("GYMFLOCK_LDS_PAD")) h->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
   if (const char* e = getenv("GYMFLOCK_TILE")) {

@@ -8,6 +8,8 @@ namespace gf {
 constexpr int kThreads = 256;   // 4 wave64s per workgroup
 constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float64 state)
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
+constexpr int kResidentRows = 32;   // rows per block of the env-resident kernel
+constexpr int kResidentMax = 1024;  // largest N whose env fits the resident kernel's LDS
 
 // One batched hot-path launch. Pointers are device pointers; all per-env arrays
 // are [B][N][...] contiguous.
@@ -26,6 +28,8 @@ struct StepArgs {
   int T;                  // agents per LDS tile (multiple of 64)
   int bpe;                // workgroups per env = ceil(N / R)
   int mean_pooling, centralized;
+  int resident;           // 1: env-resident kernel (N <= kResidentMax)
+  int spe, rps;           // resident kernel: slices per env, rows per slice
   int lds_pad;            // extra dynamic LDS bytes (occupancy control; tuning knob)
   int diag;               // ablation switches (0 in production): 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
@@ -52,6 +56,8 @@ struct StatsArgs {
 int step_rows_per_block(int N);
 int step_tile(int N);
 size_t step_lds_bytes(int N, int R, int T, bool ctrl);
+size_t step_resident_lds_bytes(int N, bool ctrl);
+void step_resident_geometry(int N, int B, int target_wgs, int* spe, int* rps);
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);

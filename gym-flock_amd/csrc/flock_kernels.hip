@@ -458,6 +458,273 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
 }
 
 // ---------------------------------------------------------------------------------
+// Env-resident form of the same step (N <= kResidentMax): a workgroup loads its env's
+// agents into LDS once, then walks a slice of 32-row blocks. Nothing inside the block
+// loop reads global memory, so the network stores of block k drain while block k+1
+// computes (no vmcnt wait ever sits behind them), and the env's state is read and
+// integrated once per slice instead of once per 32 rows. Same numerics and outputs as
+// flock_step_kernel (pass 1 float32 prefilter + float64 band, float64 features).
+template <bool DYN, bool UF64, bool CTRL>
+__global__ __launch_bounds__(kThreads) void flock_step_resident_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int RB = kResidentRows;
+  constexpr int S = kThreads / RB;  // word-slices per row in the feature pass
+  const int N = a.N;
+  const int Np = (N + 63) & ~63;
+  const int Wn = Np >> 6;
+  St* tile = reinterpret_cast<St*>(smem);                    // Np float64 states
+  float2* tile32 = reinterpret_cast<float2*>(tile + Np);     // Np float32 positions
+  uint64_t* adj = reinterpret_cast<uint64_t*>(tile32 + Np);  // RB x Wn
+  uint64_t* nearb = adj + (size_t)RB * Wn;                   // RB x Wn (CTRL)
+  double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)RB * Wn : 0));
+  float* redf = reinterpret_cast<float*>(red + 4);
+  float* inv = reinterpret_cast<float*>(red + 8);  // RB
+
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = L / a.spe, sl = L - b * a.spe;
+  const int r0 = sl * a.rps, r1 = min(N, r0 + a.rps);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const size_t env0 = (size_t)b * N;
+
+  // prologue: the env's post-update state, once per workgroup
+  double svx = 0, svy = 0;
+  float pt = 0.f;
+  for (int t = tid; t < N; t += kThreads) {
+    const St s = load_state<DYN, UF64>(a, env0 + t);
+    tile[t] = s;
+    const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
+    tile32[t] = make_float2(fx, fy);
+    pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
+    svx += s.vx;
+    svy += s.vy;
+  }
+  const float Pt = uniform_f(block_max(pt, redf));
+  const double Svx = block_sum(svx, red);
+  const double Svy = block_sum(svy, red);
+  if (a.reward && sl == 0) {  // instant_cost (:145-147), two-pass like np.var
+    const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
+    double qx = 0, qy = 0;
+    for (int t = tid; t < N; t += kThreads) {
+      const double ex = tile[t].vx - mx, ey = tile[t].vy - my;
+      qx += ex * ex;
+      qy += ey * ey;
+    }
+    const double Qx = block_sum(qx, red);
+    const double Qy = block_sum(qy, red);
+    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
+  }
+  const float pu = Pt + Pt;  // rows are agents of the same env
+  Band ba{-__builtin_inff(), __builtin_inff()}, bn = ba;
+  if (pu < 1.0e5f) {
+    const double delta = ldexp(static_cast<double>(pu) * (1.0 + 1e-6) + 4.0, -20);
+    ba = make_band(a.cr2, delta);
+    bn = make_band(a.cr, delta);
+  }
+  ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
+  bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
+  const int npair = (Wn + 1) >> 1;
+  const int fr = tid / S, fs = tid - fr * S;
+  const bool vec4 = (N & 3) == 0;
+
+  for (int i0 = r0; i0 < r1; i0 += RB) {
+    const int nrows = min(RB, r1 - i0);
+    float rx32 = 0.f, ry32 = 0.f;
+    if (lane < nrows) {
+      const float2 p = tile32[i0 + lane];
+      rx32 = p.x;
+      ry32 = p.y;
+    }
+    // pass 1 over every column of the env (see flock_step_kernel)
+    for (int cp = (a.diag & 8) ? npair : wid; cp < npair; cp += 4) {
+      const int ca = cp << 1;
+      const bool has_b = ca + 1 < Wn;
+      const int jta = (ca << 6) + lane, jtb = jta + 64;
+      const bool va = jta < N, vb = jtb < N;
+      const float2 qa = va ? tile32[jta] : make_float2(1.0e18f, 1.0e18f);
+      const float2 qb = vb ? tile32[jtb] : make_float2(1.0e18f, 1.0e18f);
+      const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
+      unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
+      uint64_t band = 0;
+      for (int r = 0; r < nrows; ++r) {
+        const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+        const f2v dx = xi - qx, dy = yi - qy;
+        const f2v d2 = dx * dx + dy * dy;
+        const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+        const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+        band |= (Aa ^ Ma) | (Ab ^ Mb);
+        put_lane(wa0, wa1, Aa, r);
+        put_lane(wb0, wb1, Ab, r);
+        if constexpr (CTRL) {
+          const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+          const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+          band |= (Na ^ NMa) | (Nb ^ NMb);
+          put_lane(na0, na1, Na, r);
+          put_lane(nb0, nb1, Nb, r);
+        }
+      }
+      if (band) {  // rare: decide the band pairs exactly in float64
+        const St oa = va ? tile[jta] : St{1.0e300, 1.0e300, 0, 0};
+        const St ob = vb ? tile[jtb] : St{1.0e300, 1.0e300, 0, 0};
+        for (int r = 0; r < nrows; ++r) {
+          const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+          const f2v dx = xi - qx, dy = yi - qy;
+          const f2v d2 = dx * dx + dy * dy;
+          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+          uint64_t Na = 0, Nb = 0, NMa = 0, NMb = 0;
+          if constexpr (CTRL) {
+            Na = __ballot(d2.x <= bn.lo);
+            Nb = __ballot(d2.y <= bn.lo);
+            NMa = __ballot(!(d2.x > bn.hi));
+            NMb = __ballot(!(d2.y > bn.hi));
+          }
+          if ((Aa ^ Ma) | (Ab ^ Mb) | (Na ^ NMa) | (Nb ^ NMb)) {
+            const St ri = tile[i0 + r];
+            const double dxa = ri.px - oa.px, dya = ri.py - oa.py;
+            const double dxb = ri.px - ob.px, dyb = ri.py - ob.py;
+            const double r2a = dxa * dxa + dya * dya, r2b = dxb * dxb + dyb * dyb;
+            put_lane(wa0, wa1, Aa | (__ballot(r2a < a.cr2) & (Aa ^ Ma)), r);
+            put_lane(wb0, wb1, Ab | (__ballot(r2b < a.cr2) & (Ab ^ Mb)), r);
+            if constexpr (CTRL) {
+              put_lane(na0, na1, Na | (__ballot(r2a <= a.cr) & (Na ^ NMa)), r);
+              put_lane(nb0, nb1, Nb | (__ballot(r2b <= a.cr) & (Nb ^ NMb)), r);
+            }
+          }
+        }
+      }
+      if (lane < nrows) {
+        const int dl = i0 + lane - (ca << 6);  // the diagonal is never a neighbour
+        const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
+        const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
+        uint64_t* arow = adj + (size_t)lane * Wn + ca;
+        arow[0] = ((static_cast<uint64_t>(wa1) << 32) | wa0) & ka;
+        if (has_b) arow[1] = ((static_cast<uint64_t>(wb1) << 32) | wb0) & kb;
+        if constexpr (CTRL) {
+          uint64_t* nrow = nearb + (size_t)lane * Wn + ca;
+          nrow[0] = ((static_cast<uint64_t>(na1) << 32) | na0) & ka;
+          if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
+        }
+      }
+    }
+    __syncthreads();
+
+    // degrees -> 1/deg
+    const bool frow = fr < nrows;
+    const int wpt = (Wn + S - 1) / S;
+    const int wb = fs * wpt, we = min(Wn, wb + wpt);
+    {
+      int deg = 0;
+      if (frow)
+        for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
+      for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
+      if (frow && fs == 0)
+        inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
+    }
+    __syncthreads();
+
+    // network rows of this block (one contiguous nrows*N*4-byte range)
+    if (a.network) {
+      for (int r = wid; r < nrows; r += 4) {
+        const float iv = inv[r];
+        const uint64_t* bits = adj + (size_t)r * Wn;
+        float* rowp = a.network + (env0 + i0 + r) * (size_t)N;
+        if (vec4) {
+          f4v* r4 = reinterpret_cast<f4v*>(rowp);
+          const int nq = N >> 2;
+          for (int q = lane; q < nq; q += 64) {
+            const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
+            const f4v v = {(nib & 1u) ? iv : 0.0f, (nib & 2u) ? iv : 0.0f, (nib & 4u) ? iv : 0.0f,
+                           (nib & 8u) ? iv : 0.0f};
+            if (a.diag & 4)
+              __builtin_nontemporal_store(v, &r4[q]);
+            else
+              r4[q] = v;
+          }
+        } else {
+          for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
+        }
+      }
+    }
+
+    // features / gradients of this block's rows (set bits only), then per-row outputs
+    double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
+    const St me = frow ? tile[i0 + fr] : St{0, 0, 0, 0};
+    if (frow && !(a.diag & 2)) {
+      for (int w = wb; w < we; ++w) {
+        const uint64_t am = adj[(size_t)fr * Wn + w];
+        const uint64_t nm = CTRL ? nearb[(size_t)fr * Wn + w] : 0ull;
+        uint64_t m = am | nm;
+        while (m) {
+          const int k = __builtin_ctzll(m);
+          m &= m - 1;
+          const St o = tile[(w << 6) + k];
+          const double dx = me.px - o.px, dy = me.py - o.py;
+          const double r2 = dx * dx + dy * dy;
+          const double rr = r2 * r2;
+          const double q1x = dx / rr, q2x = dx / r2;
+          const double q1y = dy / rr, q2y = dy / r2;
+          const bool isadj = (am >> k) & 1ull;
+          if (isadj) {
+            f0 += me.vx - o.vx;
+            f1 += q1x;
+            f2 += q2x;
+            f3 += me.vy - o.vy;
+            f4 += q1y;
+            f5 += q2y;
+          }
+          if constexpr (CTRL) {
+            const bool isnear = (nm >> k) & 1ull;
+            if (isnear && (a.centralized || isadj)) {
+              gx += (-2.0 * q1x) + (2.0 * q2x);
+              gy += (-2.0 * q1y) + (2.0 * q2y);
+            }
+          }
+        }
+      }
+    }
+    for (int o = 1; o < S; o <<= 1) {
+      f0 += __shfl_xor(f0, o);
+      f1 += __shfl_xor(f1, o);
+      f2 += __shfl_xor(f2, o);
+      f3 += __shfl_xor(f3, o);
+      f4 += __shfl_xor(f4, o);
+      f5 += __shfl_xor(f5, o);
+      if constexpr (CTRL) {
+        gx += __shfl_xor(gx, o);
+        gy += __shfl_xor(gy, o);
+      }
+    }
+    if (frow && fs == 0) {
+      const size_t g = env0 + i0 + fr;
+      if (a.state_values) {
+        float* sv = a.state_values + g * 6;
+        sv[0] = static_cast<float>(f0);
+        sv[1] = static_cast<float>(f1);
+        sv[2] = static_cast<float>(f2);
+        sv[3] = static_cast<float>(f3);
+        sv[4] = static_cast<float>(f4);
+        sv[5] = static_cast<float>(f5);
+      }
+      if constexpr (DYN) {
+        double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
+        xo[0] = double2{me.px, me.py};
+        xo[1] = double2{me.vx, me.vy};
+      }
+      if constexpr (CTRL) {
+        const double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
+        const double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
+        double2 u;
+        u.x = clip10(-gx - p2) / a.action_scalar;
+        u.y = clip10(-p3 - gy) / a.action_scalar;
+        reinterpret_cast<double2*>(a.ctrl_out)[g] = u;
+      }
+    }
+    __syncthreads();  // bits and 1/deg are rewritten by the next block
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Flocking-v0 observation (flocking.py:20-25): the K smallest r2 per row, ties to the
 // lower index (the reference's argsort is unstable), self has r2=inf.
 // One thread per row keeps a sorted (r2, j) list in registers; the env's positions
@@ -607,8 +874,38 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
   return s;
 }
 
+size_t step_resident_lds_bytes(int N, bool ctrl) {
+  const size_t Np = (N + 63) / 64 * 64, Wn = Np / 64;
+  return Np * (sizeof(St) + 8) + (size_t)kResidentRows * Wn * 8 * (ctrl ? 2 : 1) + 8 * sizeof(double) +
+         kResidentRows * 4;
+}
+
+void step_resident_geometry(int N, int B, int target_wgs, int* spe, int* rps) {
+  const int blocks = (N + kResidentRows - 1) / kResidentRows;
+  int s = (target_wgs + B - 1) / B;
+  s = s < 1 ? 1 : (s > blocks ? blocks : s);
+  const int per = ((N + s - 1) / s + kResidentRows - 1) / kResidentRows * kResidentRows;
+  *rps = per;
+  *spe = (N + per - 1) / per;
+}
+
+template <bool DYN, bool UF64, bool CTRL>
+static hipError_t launch_step_resident_t(const StepArgs& a, hipStream_t s) {
+  const size_t lds = step_resident_lds_bytes(a.N, CTRL) + (size_t)a.lds_pad;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_resident_kernel<DYN, UF64, CTRL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((flock_step_resident_kernel<DYN, UF64, CTRL>), dim3(a.B * a.spe), dim3(kThreads), lds, s, a);
+  return hipGetLastError();
+}
+
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
+  if (a.resident) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
   const size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
   static bool attr_set = false;
   if (!attr_set) {

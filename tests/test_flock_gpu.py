@@ -288,3 +288,18 @@ def test_rccl_reward_gather_single_rank():
         k = min(got.shape[0], len(hist))
         np.testing.assert_array_equal(got[-k:], np.array(hist[-k:]))
     v.close()
+
+
+def test_env_resident_kernel_parity(monkeypatch):
+    """The opt-in env-resident step kernel (GYMFLOCK_RESIDENT=1) gives the same bits as
+    the tiled kernel and the oracle."""
+    monkeypatch.setenv("GYMFLOCK_RESIDENT", "1")
+    for n, B in ((100, 3), (1024, 2)):
+        x0 = synthetic_batch(B, n, seed0=7 * n)
+        u = np.random.RandomState(n).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+        h = nat.FlockHandle(n, B)
+        h.set_state(x0)
+        h.step(u, nat.FE_WITH_CONTROLLER)
+        for b in range(B):
+            check_against_oracle(h, x0[b], u[b], b)
+        h.close()
