@@ -62,6 +62,51 @@ __global__ __launch_bounds__(256) void fill_rows(f4v* p, size_t n4) {
     }
 }
 
+// The tiled step kernel's shape (32 rows x N=1024 per block, 8192 blocks per GiB) with
+// one of its side costs added, to find what slows its store stream:
+// V=0 plain, 1 +26 KB LDS (occupancy), 2 +40 KB L2-resident reads per block (the env
+// tile), 3 +scattered per-row small writes (state_values / x), 4 values built from LDS
+// bits, 5 = 2+3+4.
+template <int V>
+__global__ __launch_bounds__(256) void rows32(f4v* p, const f4v* src, float* small, size_t n4) {
+  extern __shared__ unsigned char lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  f4v acc{0, 0, 0, 0};
+  if (V == 2 || V == 5) {  // 40 KB per block, the same 40 KB for each group of 32 blocks
+    const f4v* s = src + (size_t)(blockIdx.x / 32) * 2560;
+    for (int k = threadIdx.x; k < 2560; k += 256) acc += s[k];
+  }
+  unsigned long long* bits = reinterpret_cast<unsigned long long*>(lds);
+  if (V == 4 || V == 5) {
+    for (int k = threadIdx.x; k < 32 * 16; k += 256) bits[k] = 0x9249249249249249ull * (k + 1);
+    __syncthreads();
+  }
+  if (V == 1) {
+    lds[threadIdx.x] = 1;
+    __syncthreads();
+  }
+  f4v* base = p + (size_t)blockIdx.x * 32 * 256;
+  const float iv = 0.25f + acc.x;
+  for (int r = wid; r < 32; r += 4)
+    for (int q = lane; q < 256; q += 64) {
+      f4v v{iv, 0.0f, iv, 0.0f};
+      if (V == 4 || V == 5) {
+        const unsigned nib = (unsigned)(bits[r * 16 + (q >> 4)] >> ((q & 15) << 2)) & 0xFu;
+        v = f4v{(nib & 1u) ? iv : 0.f, (nib & 2u) ? iv : 0.f, (nib & 4u) ? iv : 0.f, (nib & 8u) ? iv : 0.f};
+      }
+      base[r * 256 + q] = v;
+    }
+  if (V == 3 || V == 5) {  // 6 floats + 4 doubles per row, one lane per row
+    const int S = 8, fr = threadIdx.x / S, fs = threadIdx.x % S;
+    if (fs == 0) {
+      const size_t g = (size_t)blockIdx.x * 32 + fr;
+      for (int k = 0; k < 6; ++k) small[g * 6 + k] = iv;
+      double* x = reinterpret_cast<double*>(small + (size_t)gridDim.x * 32 * 6);
+      for (int k = 0; k < 4; ++k) x[g * 4 + k] = iv;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void readk(const f4v* p, size_t n4, float* out) {
   f4v acc{0, 0, 0, 0};
   for (size_t k = blockIdx.x * 256ull + threadIdx.x; k < n4; k += (size_t)gridDim.x * 256) acc += p[k];
@@ -78,6 +123,44 @@ int main(int argc, char** argv) {
   const int grids[] = {1024, 4096, 16384};
   f4v *a = nullptr, *b = nullptr;
   float* o = nullptr;
+  if (argc > 1 && argv[1][0] == 'v') {  // side-cost variants of the 32-row store shape
+    const size_t bytes = 1024 * MB, n4 = bytes / 16;
+    const int g = (int)(bytes / (32 * 1024 * 4));
+    f4v* src;
+    float* small;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&src, (size_t)(g / 32 + 1) * 2560 * 16));
+    CK(hipMemset(src, 0, (size_t)(g / 32 + 1) * 2560 * 16));
+    CK(hipMalloc(&small, (size_t)g * 32 * (24 + 32)));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int rep = 0; rep < 2; ++rep)
+      for (int v = 0; v < 6; ++v) {
+        auto launch = [&]() {
+          switch (v) {
+            case 0: rows32<0><<<g, 256, 0>>>(a, src, small, n4); break;
+            case 1: rows32<1><<<g, 256, 26 * 1024>>>(a, src, small, n4); break;
+            case 2: rows32<2><<<g, 256, 0>>>(a, src, small, n4); break;
+            case 3: rows32<3><<<g, 256, 0>>>(a, src, small, n4); break;
+            case 4: rows32<4><<<g, 256, 4096>>>(a, src, small, n4); break;
+            case 5: rows32<5><<<g, 256, 4096>>>(a, src, small, n4); break;
+          }
+        };
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < 10; ++r) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        static const char* names[] = {"plain", "+26KB LDS", "+40KB L2 reads", "+small writes", "+LDS bits",
+                                      "+reads+small+bits"};
+        printf("rows32 %-18s %8.1f us %7.0f GB/s\n", names[v], ms / 10 * 1e3, bytes / (ms / 10 * 1e-3) / 1e9);
+      }
+    return 0;
+  }
   if (argc > 1) {  // rows mode: the step kernel's store shape at 1 GiB, 16384 blocks
     const size_t bytes = 1024 * MB, n4 = bytes / 16;
     const int g = (int)(bytes / (64 * 1024 * 4));
