@@ -167,3 +167,58 @@ def generate_lattice(xmin, xmax, ymin, ymax, spacing=RES):
     mask = (xl < w / 2.0) & (xl > -w / 2.0) & (yl < h / 2.0) & (yl > -h / 2.0)
     xl, yl = xl[mask] + (w // 2 + xmin), yl[mask] + (h // 2 + ymin)
     return np.stack([yl, xl], axis=1)
+
+
+MAX_COST = 1000  # coverage.py:68
+HORIZON = 10     # coverage.py:66
+
+
+def time_matrix(n_targets, senders, receivers, horizon=HORIZON, edge_time=1.0):
+    """construct_time_matrix(), coverage.py:621-653: per-source hop counts relaxed
+    column-wise over the motion edges in list order (in place, Gauss-Seidel), sweeping
+    while some entry changed and some entry is still infinite, at most horizon+1 sweeps.
+    senders/receivers are target-local. Returns (cost with inf -> MAX_COST, prev)."""
+    tm = np.full((n_targets, n_targets), np.inf)
+    prev = -np.ones((n_targets, n_targets), dtype=int)
+    np.fill_diagonal(tm, 0.0)
+    changed, steps = True, 0
+    while changed and np.sum(tm) == np.inf:
+        changed = False
+        for s, q in zip(senders, receivers):
+            via = tm[:, s] + edge_time
+            better = via < tm[:, q]
+            prev[:, q] = np.where(better, s, prev[:, q])
+            new = np.minimum(via, tm[:, q])
+            changed = changed or not np.array_equal(new, tm[:, q])
+            tm[:, q] = new
+        steps += 1
+        if steps > horizon > -1:
+            break
+    return np.nan_to_num(tm, posinf=MAX_COST), prev
+
+
+def greedy_actions(cost, prev, cur, visited_targets, recv, n_robots):
+    """controller(greedy=True), coverage.py:808-872 without its random fallback: for
+    each robot the nearest (hop count, first index) unvisited target, and the action
+    whose node is the next hop toward it. Returns (actions, needs_random) where
+    needs_random marks robots the reference gives np_random.choice(4) instead."""
+    R = n_robots
+    c = cur - R
+    r = cost[c, :].copy()
+    vis = np.nonzero(visited_targets == 1)[0]
+    r[:, vis] = MAX_COST
+    # quirk (:818): the reference indexes with the (row, col) tuple of np.where on the
+    # (T,1) visited column, so column 0 (the first target) is masked too whenever any
+    # target is visited
+    if len(vis):
+        r[:, 0] = MAX_COST
+    goal = np.argmin(r, axis=1)
+    acts = np.zeros(R, np.int32)
+    rand = np.zeros(R, bool)
+    for i in range(R):
+        if r[i, goal[i]] == MAX_COST or prev[goal[i], c[i]] == -1:
+            rand[i] = True
+            continue
+        step = prev[goal[i], c[i]] + R
+        acts[i] = int(np.nonzero(recv[i] == step)[0][0])
+    return acts, rand

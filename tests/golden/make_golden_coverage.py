@@ -42,6 +42,8 @@ def _episode(cov, n_robots, max_nodes, map_seed, env_seed, n_steps, policy, tag)
         snd.append(np.array(o["senders"]).copy()); rcv.append(np.array(o["receivers"]).copy())
         stp.append(np.array(o["step"]).copy()); vis.append(env.visited[:, 0].copy())
         cls.append(np.array(env.closest_targets).astype(np.int32))
+    if policy == "greedy":  # the reference's own time matrix (construct_time_matrix :621-653)
+        rec.update(graph_cost=env.graph_cost.astype(np.int16), graph_previous=env.graph_previous.astype(np.int16))
     rec.update(actions=np.array(acts), xr=np.array(xs), reward=np.array(rews), done=np.array(dones),
                nodes=np.array(nodes, dtype=np.float32), edges=np.array(edges, dtype=np.float32),
                senders=np.array(snd, dtype=np.int32), receivers=np.array(rcv, dtype=np.int32),
@@ -55,6 +57,7 @@ def gen_coverage():
     _episode(cov, 6, 500, map_seed=3, env_seed=4, n_steps=40, policy="random", tag="r6_random")
     _episode(cov, 6, 500, map_seed=5, env_seed=6, n_steps=30, policy="greedy", tag="r6_greedy")
     _episode(cov, 200, 1000, map_seed=8, env_seed=9, n_steps=12, policy="random", tag="r200_random")
+    _episode(cov, 20, 700, map_seed=12, env_seed=13, n_steps=75, policy="greedy", tag="r20_greedy")
     # the host map generator, pinned separately (coverage.py:516-527)
     mm = importlib.import_module("gym_flock.envs.spatial.make_map")
     maps = {}

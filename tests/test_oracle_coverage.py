@@ -48,3 +48,34 @@ def test_episode_matches_reference(path):
 def test_lattice_matches_reference():
     f = np.load(os.path.join(GOLDEN, "coverage_maps.npz"))
     np.testing.assert_array_equal(oc.generate_lattice(-120, 120, -120, 120), f["lattice"])
+
+
+GREEDY = sorted(glob.glob(os.path.join(GOLDEN, "coverage_r*_greedy.npz")))
+ENV_SEED = {"coverage_r6_greedy.npz": 6, "coverage_r20_greedy.npz": 13}
+
+
+@pytest.mark.parametrize("path", GREEDY, ids=os.path.basename)
+def test_greedy_expert_matches_reference(path):
+    f = np.load(path)
+    R, T = int(f["n_robots"]), int(f["n_targets"])
+    env = oc.CoverageOracle(f["targets"], R, int(f["max_nodes"]))
+    cost, prev = oc.time_matrix(T, env.motion[0] - R, env.motion[1] - R)
+    np.testing.assert_array_equal(cost, f["graph_cost"])
+    np.testing.assert_array_equal(prev, f["graph_previous"])
+    start = oc.closest_targets(f["x0"][:R], f["targets"], R) - R
+    env.reset(start, np.nonzero(f["visited0"][R:] == 0)[0] + R)
+    rs = np.random.RandomState(ENV_SEED[os.path.basename(path)])
+    rs.choice(np.arange(T), size=(R,), replace=False)
+    rs.choice(np.arange(T) + R, size=(int(T * 0.5),), replace=False)
+    n_random = 0
+    for t in range(len(f["actions"])):
+        cur = env.closest()
+        recv = oc.action_receivers(cur, env.nbr, env.cnt, R)
+        a, rand = oc.greedy_actions(cost, prev, cur, env.visited[R:], recv, R)
+        for i in np.nonzero(rand)[0]:
+            a[i] = rs.choice(4)  # the reference's fallback draw, robot order (:864)
+            n_random += 1
+        np.testing.assert_array_equal(a, f["actions"][t])
+        env.step(a)
+    if "r20" in path:
+        assert n_random > 0  # the long episode exercises the random fallback
