@@ -131,8 +131,46 @@ def bench_coverage(args):
                          "traffic": None}}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = coverage_cpu_baseline(targets, R, M, min(args.cpu_seconds, 8.0))
+    line["greedy_expert"] = bench_greedy(v, targets, R, M, B, K, args)
     print(json.dumps(line), flush=True)
     v.close()
+
+
+def bench_greedy(v, targets, R, M, B, K, args):
+    """§8f: the greedy expert (controller(greedy=True)) on the same batch: the per-graph
+    time-matrix build for all B envs, then K expert steps (device controller + step,
+    actions resident; fallback robots keep action 0, no host round trip)."""
+    v.set_targets(targets)  # invalidates every env's time matrix
+    v.sync()
+    t0 = time.perf_counter()
+    v.h.controller_greedy(fetch=False)
+    v.sync()
+    build = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(K):
+        v.h.controller_greedy(fetch=False)
+        v.step(resident=True)
+    v.sync()
+    el = time.perf_counter() - t0
+    out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
+           "expert_step_ms": 1e3 * el / K, "expert_robot_steps_per_s": R * B * K / el}
+    if not args.no_cpu_baseline:
+        from oracle import coverage as oc
+        o = oc.CoverageOracle(targets, R, M)
+        t0 = time.perf_counter()
+        cost, prev = oc.time_matrix(len(targets), o.motion[0] - R, o.motion[1] - R)
+        out["cpu_time_matrix_s_per_env"] = time.perf_counter() - t0
+        rs = np.random.RandomState(0)
+        T = len(targets)
+        o.reset(rs.choice(T, R, replace=False), rs.choice(T, T // 2, replace=False) + R)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            cur = o.closest()
+            a, _ = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+            o.step(a)
+        out["cpu_expert_step_ms_per_env"] = 1e3 * (time.perf_counter() - t0) / 5
+        out["cpu_kind"] = "port (oracle/coverage.py, NumPy, 1 thread)"
+    return out
 
 
 def main():

@@ -1,4 +1,5 @@
 // C-ABI of the Coverage-v0 engine (include/gymflock.h, cov_* functions).
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,6 +29,10 @@ int calloc_dev(T** p, size_t n) {
   if (e != hipSuccess) return cfail(GF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   e = hipMemset(*p, 0, n * sizeof(T));
   if (e != hipSuccess) return cfail(GF_EHIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  // hipMemset may still be running on the null stream, which the handle's non-blocking
+  // stream does not order against: finish it before any kernel writes the buffer
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("hipDeviceSynchronize: ") + hipGetErrorString(e));
   return GF_OK;
 }
 
@@ -46,6 +51,19 @@ struct cov_handle {
   int* err = nullptr;
   std::vector<int> ntg_host;
   bool has_graph = false, has_state = false;
+  // greedy expert (allocated on first use)
+  uint16_t* tm_cost = nullptr;
+  int16_t* tm_prevT = nullptr;
+  uint8_t* tm_flags = nullptr;
+  uint8_t* needs_random = nullptr;
+  int32_t* tm_envsel = nullptr;
+  uint32_t* tm_sched = nullptr;
+  int32_t* tm_nslots = nullptr;
+  int32_t* tm_nlev = nullptr;
+  uint8_t* tm_overflow = nullptr;
+  std::vector<int> n_motion_host;
+  std::vector<char> tm_valid;
+  int64_t tm_wide_envs = 0;  // envs whose matrix needed uint16 entries (diagnostics)
 };
 
 namespace {
@@ -62,7 +80,8 @@ void cov_release(cov_handle* h) {
   gf::CovArgs& a = h->a;
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
-                  a.receivers, a.obs_step, h->err, h->start, h->visited0, h->envsel};
+                  a.receivers, a.obs_step, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_prevT,
+                  h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -75,17 +94,98 @@ int check_err(cov_handle* h) {
   CV_HIP(hipMemcpyAsync(&err, h->err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   CV_HIP(hipStreamSynchronize(h->stream));
   if (!err) return GF_OK;
-  CV_HIP(hipMemset(h->err, 0, sizeof(int)));
+  CV_HIP(hipMemsetAsync(h->err, 0, sizeof(int), h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
   std::string m;
   if (err & 1) m += "a target has more than 4 motion-graph neighbours (coverage.py:257 assert); ";
   if (err & 2) m += "motion edges + 8*n_robots exceed 4*max_nodes (\"Increase MAX_EDGES\", coverage.py:288); ";
   if (err & 4) m += "action outside [0, 4) (coverage.py:189 index); ";
+  if (err & 8) m += "greedy next hop is not among the robot's action targets (IndexError at coverage.py:869); ";
   return cfail(GF_EINVAL, m);
 }
 
 int copy_out(cov_handle* h, void* dst, const void* src, size_t bytes) {
   if (!dst) return GF_OK;
   CV_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  return GF_OK;
+}
+
+// Time matrices of every env whose graph changed since they were last built.
+int ensure_time_matrix(cov_handle* h) {
+  const int B = h->cfg.n_envs, Tm = h->a.Tmax;
+  const int kcap = h->cfg.horizon > -1 ? h->cfg.horizon + 1 : Tm + 1;
+  const int nchunk = (Tm + 63) / 64;
+  const int sched_stride = 4 * Tm * 16 + 16;  // motion edges <= 4 per target, batches <= 16, + prefetch slack
+  if (!h->tm_cost) {
+    int rc;
+    if ((rc = calloc_dev(&h->tm_cost, (size_t)B * Tm * Tm)) || (rc = calloc_dev(&h->tm_prevT, (size_t)B * Tm * Tm)) ||
+        (rc = calloc_dev(&h->tm_flags, (size_t)B * nchunk * kcap)) ||
+        (rc = calloc_dev(&h->needs_random, (size_t)B * h->cfg.n_robots)) || (rc = calloc_dev(&h->tm_envsel, (size_t)B)) ||
+        (rc = calloc_dev(&h->tm_sched, (size_t)B * sched_stride)) || (rc = calloc_dev(&h->tm_nslots, (size_t)B)) ||
+        (rc = calloc_dev(&h->tm_nlev, (size_t)B)) || (rc = calloc_dev(&h->tm_overflow, (size_t)B)))
+      return rc;
+  }
+  std::vector<int32_t> sel;
+  int t_lds = 0, e_max = 0;
+  for (int b = 0; b < B; ++b) {
+    if (h->tm_valid[b]) continue;
+    sel.push_back(b);
+    t_lds = std::max(t_lds, h->ntg_host[b]);
+    e_max = std::max(e_max, h->n_motion_host[b]);
+  }
+  if (sel.empty()) return GF_OK;
+  if (gf::cov_time_matrix_lds_bytes(t_lds, false) > 160 * 1024 ||
+      gf::cov_tm_schedule_lds_bytes(t_lds, e_max) > 160 * 1024)
+    return cfail(GF_EINVAL, "time matrix: (n_targets + 1) * 64 bytes exceed the 160 KB LDS of a CU");
+  gf::CovTmArgs t{};
+  t.R = h->a.R;
+  t.M = h->a.M;
+  t.Tmax = Tm;
+  t.horizon = h->cfg.horizon;
+  t.kcap = kcap;
+  t.nchunk = nchunk;
+  t.t_lds = t_lds;
+  t.envs = h->tm_envsel;
+  t.ntg = h->ntg;
+  t.n_motion = h->a.n_motion;
+  t.senders = h->a.senders;
+  t.receivers = h->a.receivers;
+  t.flags = h->tm_flags;
+  t.cost = h->tm_cost;
+  t.prevT = h->tm_prevT;
+  t.sched = h->tm_sched;
+  t.nslots = h->tm_nslots;
+  t.nlev = h->tm_nlev;
+  t.overflow = h->tm_overflow;
+  t.sched_stride = sched_stride;
+  CV_HIP(hipMemcpyAsync(h->tm_envsel, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  hipError_t e = gf::launch_cov_tm_schedule(t, (int)sel.size(), e_max, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_tm_schedule_kernel: ") + hipGetErrorString(e));
+  // uint8 entries first (twice the waves per CU); envs it cannot bound get uint16
+  e = gf::launch_cov_time_matrix(t, (int)sel.size(), false, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_time_matrix_kernel: ") + hipGetErrorString(e));
+  std::vector<uint8_t> ovf(B);
+  CV_HIP(hipMemcpyAsync(ovf.data(), h->tm_overflow, B, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  std::vector<int32_t> wide;
+  int t_wide = 0;
+  for (int b : sel)
+    if (ovf[b]) {
+      wide.push_back(b);
+      t_wide = std::max(t_wide, h->ntg_host[b]);
+    }
+  if (!wide.empty()) {
+    if (gf::cov_time_matrix_lds_bytes(t_wide, true) > 160 * 1024)
+      return cfail(GF_EINVAL, "time matrix: hop counts above 254 need (n_targets + 1) * 128 bytes of LDS (> 160 KB)");
+    CV_HIP(hipMemsetAsync(h->tm_overflow, 0, B, h->stream));
+    CV_HIP(hipMemcpyAsync(h->tm_envsel, wide.data(), wide.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+    t.t_lds = t_wide;
+    e = gf::launch_cov_time_matrix(t, (int)wide.size(), true, h->stream);
+    if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_time_matrix_kernel: ") + hipGetErrorString(e));
+    CV_HIP(hipStreamSynchronize(h->stream));
+  }
+  h->tm_wide_envs += (int64_t)wide.size();
+  for (int b : sel) h->tm_valid[b] = 1;
   return GF_OK;
 }
 
@@ -100,6 +200,7 @@ int cov_create(const cov_config* cfg, cov_handle** out) {
     return cfail(GF_EINVAL, "need n_robots >= 1, n_envs >= 1, max_nodes > n_robots");
   if (cfg->n_robots > 4096) return cfail(GF_EINVAL, "n_robots > 4096 not supported");
   if (!(cfg->res > 0) || !(cfg->motion_radius > 0)) return cfail(GF_EINVAL, "bad res/motion_radius");
+  if (cfg->horizon < -1) return cfail(GF_EINVAL, "horizon must be >= -1");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return cfail(GF_EHIP, "no HIP device available (libgymflock needs an MI355X)");
@@ -135,6 +236,8 @@ int cov_create(const cov_config* cfg, cov_handle** out) {
   a.ntg = h->ntg;
   a.err = h->err;
   h->ntg_host.assign(B, 0);
+  h->n_motion_host.assign(B, 0);
+  h->tm_valid.assign(B, 0);
   *out = h;
   return GF_OK;
 }
@@ -165,6 +268,8 @@ int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets
   hipError_t e = gf::launch_cov_graph(h->a, h->envsel, (int)sel.size(), h->stream);
   if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_graph_kernel: ") + hipGetErrorString(e));
   if (int rc = check_err(h)) return rc;
+  CV_HIP(hipMemcpy(h->n_motion_host.data(), h->a.n_motion, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+  for (int b = b0; b < b1; ++b) h->tm_valid[b] = 0;
   h->has_graph = true;
   for (int b = 0; b < B; ++b) h->has_graph = h->has_graph && h->ntg_host[b] > 0;
   return GF_OK;
@@ -286,6 +391,70 @@ int cov_get_n_motion(cov_handle* h, int32_t* n_motion) {
   if (int rc = use(h)) return rc;
   if (int rc = copy_out(h, n_motion, h->a.n_motion, (size_t)h->cfg.n_envs * 4)) return rc;
   CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random, int64_t* n_random) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (int rc = use(h)) return rc;
+  if (int rc = ensure_time_matrix(h)) return rc;
+  gf::CovGreedyArgs g{};
+  const gf::CovArgs& a = h->a;
+  g.B = a.B;
+  g.R = a.R;
+  g.Tmax = a.Tmax;
+  g.ntg = h->ntg;
+  g.tgt = h->tgt;
+  g.xr = a.xr;
+  g.dirty = a.dirty;
+  g.cur = a.cur;
+  g.cost = h->tm_cost;
+  g.prevT = h->tm_prevT;
+  g.visited = a.visited;
+  g.nvisited = a.nvisited;
+  g.nbr = a.nbr;
+  g.cnt = a.cnt;
+  g.actions = h->actions;
+  g.needs_random = h->needs_random;
+  g.err = h->err;
+  hipError_t e = gf::launch_cov_greedy(g, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_greedy_kernel: ") + hipGetErrorString(e));
+  if (!actions && !needs_random && !n_random) return GF_OK;
+  const size_t n = (size_t)a.B * a.R;
+  std::vector<uint8_t> mask;
+  uint8_t* rnd = needs_random;
+  if (n_random && !rnd) {
+    mask.resize(n);
+    rnd = mask.data();
+  }
+  if (int rc = copy_out(h, actions, h->actions, n * 4)) return rc;
+  if (int rc = copy_out(h, rnd, h->needs_random, n)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  if (n_random) {
+    int64_t cnt = 0;
+    for (size_t k = 0; k < n; ++k) cnt += rnd[k] ? 1 : 0;
+    *n_random = cnt;
+  }
+  return check_err(h);
+}
+
+int cov_get_time_matrix(cov_handle* h, int env, int32_t* cost, int32_t* prev) {
+  if (!h || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
+  if (!h->has_graph) return cfail(GF_ESTATE, "set the target graph first (cov_set_targets)");
+  if (int rc = use(h)) return rc;
+  if (int rc = ensure_time_matrix(h)) return rc;
+  const size_t Tm = h->a.Tmax, T = h->ntg_host[env];
+  std::vector<uint16_t> c(Tm * Tm);
+  std::vector<int16_t> p(Tm * Tm);
+  CV_HIP(hipMemcpyAsync(c.data(), h->tm_cost + env * Tm * Tm, Tm * Tm * 2, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipMemcpyAsync(p.data(), h->tm_prevT + env * Tm * Tm, Tm * Tm * 2, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  for (size_t i = 0; i < T; ++i)
+    for (size_t j = 0; j < T; ++j) {
+      if (cost) cost[i * T + j] = c[i * Tm + j] == 0xFFFF ? 1000 : c[i * Tm + j];
+      if (prev) prev[i * T + j] = p[j * Tm + i];  // graph_previous[i, j] lives at prevT[j][i]
+    }
   return GF_OK;
 }
 

@@ -1,0 +1,336 @@
+// HIP kernels (gfx950) for Coverage-v0's greedy expert, batched over B envs.
+//
+// Reference (gym_flock/envs/spatial/coverage.py): construct_time_matrix :621-653 and
+// controller(greedy=True) :800-872.
+//
+// Time matrix. The reference relaxes hop counts column-wise over the motion edges in
+// list order, in place (Gauss-Seidel), for all sources at once, and sweeps while some
+// entry changed AND some entry is still infinite, at most horizon+1 sweeps. Rows
+// (sources) are independent within a sweep; only the stop rule couples them. So:
+//   - one wave per 64 sources of one env; each lane owns one source's row, kept in LDS
+//     as uint16 (0xFFFF = inf) in column-major order, so a lane only ever touches its
+//     own entries and a sweep needs no barrier;
+//   - edge order within a sweep: two relaxations commute unless one writes a column
+//     the other reads or writes, so any order that keeps every such pair in list order
+//     gives bit-identical results (tests/test_coverage_greedy_gpu.py checks it against
+//     the reference's matrices). cov_tm_schedule_kernel levels the edge list by those
+//     conflicts and packs each level into batches of 8 mutually independent edges
+//     (padded with no-ops on a dummy column): a batch's 16 column loads and 8 stores
+//     issue back to back, without branches;
+//   - pass A sweeps to the horizon (or to the wave's own fixed point), writes cost rows
+//     and predecessors, and records per sweep whether its rows changed / hold an inf;
+//   - pass B derives the reference's sweep count K* from every chunk's flags; only a
+//     chunk that pass A swept past K* (the env-wide stop came first) is recomputed.
+//
+// Greedy step: one wave per robot scans its node's cost row (coalesced uint16 loads)
+// for the first-index argmin over masked targets, then looks one predecessor up.
+#include "coverage_internal.h"
+
+namespace gf {
+
+namespace {
+
+constexpr int kTmLanes = 64;            // sources per wave (one wave per workgroup)
+constexpr int kBatch = 8;               // independent edges per batch
+constexpr uint32_t kInf = 0xFFFF;  // uint16 cost matrix: unreachable
+constexpr int kMaxCost = 1000;          // MAX_COST :68
+
+// Conflict levels of one env's motion-edge list, then the batched schedule: sched[b]
+// holds nslots[b] (a multiple of kBatch) words s | q << 16 (target-local), level by
+// level, edges of a level in list order, no-op slots s = q = T (the dummy column).
+__global__ __launch_bounds__(64) void cov_tm_schedule_kernel(CovTmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = a.envs[blockIdx.x];
+  const int T = a.ntg[b], E = a.n_motion[b], R = a.R, E4 = 4 * a.M;
+  int* lw = reinterpret_cast<int*>(smem);  // [T] last level writing the column
+  int* lr = lw + T;                          // [T] last level reading it
+  int* level = lr + T;                       // [E]
+  int* fill = level + E;                     // [E + 1] per-level counts, then offsets
+  const int32_t* snd = a.senders + (size_t)b * E4;
+  const int32_t* rcv = a.receivers + (size_t)b * E4;
+  for (int k = threadIdx.x; k < T; k += 64) lw[k] = lr[k] = 0;
+  for (int k = threadIdx.x; k <= E; k += 64) fill[k] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int nlev = 0;
+    for (int e = 0; e < E; ++e) {
+      const int s = snd[e] - R, q = rcv[e] - R;
+      const int L = max(max(lw[s], lw[q]), lr[q]) + 1;  // after every conflicting edge
+      level[e] = L;
+      lw[q] = max(lw[q], L);
+      lr[s] = max(lr[s], L);
+      lr[q] = max(lr[q], L);
+      fill[L - 1] += 1;
+      nlev = max(nlev, L);
+    }
+    int off = 0;
+    for (int L = 0; L < nlev; ++L) {
+      const int n = fill[L];
+      fill[L] = off;
+      off += (n + kBatch - 1) / kBatch * kBatch;
+    }
+    uint32_t* out = a.sched + (size_t)b * a.sched_stride;
+    const uint32_t noop = (uint32_t)T | ((uint32_t)T << 16);
+    for (int k = 0; k < off; ++k) out[k] = noop;
+    for (int e = 0; e < E; ++e) out[fill[level[e] - 1]++] = (uint32_t)(snd[e] - R) | ((uint32_t)(rcv[e] - R) << 16);
+    a.nslots[b] = off;
+    a.nlev[b] = nlev;
+    a.overflow[b] = 0;
+  }
+}
+
+// Per-lane scan of its own row after a sweep: any entry still inf, and the largest
+// finite entry (the uint8 variant's overflow guard).
+template <typename V>
+__device__ __forceinline__ void tm_scan(const V* col, int T, int lane, bool valid, bool& any_inf, uint32_t& mx) {
+  constexpr uint32_t inf = (V)~(V)0;
+  any_inf = false;
+  mx = 0;
+  if (!valid) return;
+  for (int t = 0; t < T; ++t) {
+    const uint32_t v = col[t * kTmLanes + lane];
+    any_inf = any_inf || v == inf;
+    mx = v != inf && v > mx ? v : mx;
+  }
+}
+
+// Time matrix of one 64-source chunk with entries of type V (uint8_t: inf = 255;
+// uint16_t: inf = 0xFFFF). One sweep raises the largest finite entry by at most the
+// schedule's level count (a value moves one hop per level), so the uint8 variant runs a
+// sweep only while max + nlev < 255 and otherwise flags the env for the uint16 rerun.
+template <typename V, bool PASS_B>
+__global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, const uint32_t* __restrict__ sched_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr uint32_t inf = (V)~(V)0;
+  const int b = a.envs[blockIdx.y];
+  const int chunk = blockIdx.x;
+  const int T = a.ntg[b];
+  const int src0 = chunk * kTmLanes;
+  if (src0 >= T) return;  // uniform
+  const int Tm = a.Tmax;
+  const int lane = threadIdx.x;
+  const int src = src0 + lane;
+  const bool valid = src < T;
+  const int kmax = a.horizon > -1 ? a.horizon + 1 : a.kcap;
+  const int nlev = a.nlev[b];
+  uint8_t* flags = a.flags + ((size_t)b * a.nchunk + chunk) * a.kcap;
+  int K = T > 1 ? kmax : 0;
+  if (PASS_B) {
+    if (a.overflow[b]) return;  // the uint16 pass redoes this env
+    // the reference's sweep count: stop after sweep k once no entry of the env changed
+    // or none is infinite (the while test), or after horizon+1 sweeps (the break)
+    const uint8_t* fenv = a.flags + (size_t)b * a.nchunk * a.kcap;
+    const int nch = (T + kTmLanes - 1) / kTmLanes;
+    for (int k = 0; k < kmax && K == kmax && T > 1; ++k) {
+      int f = 0;
+      for (int c = 0; c < nch; ++c) f |= fenv[(size_t)c * a.kcap + k];
+      if (!(f & 1) || !(f & 2)) K = k + 1;
+    }
+    // pass A's output is the state after min(kmax, fixed point) sweeps (a sweep k that
+    // changed nothing means the state after k sweeps is final): redo only if K is less
+    int kvalid = kmax;
+    for (int k = 0; k < kmax; ++k)
+      if (!(flags[k] & 1)) {
+        kvalid = k;
+        break;
+      }
+    if (T <= 1 || K >= kvalid) return;
+  }
+  V* col = reinterpret_cast<V*>(smem);  // [T + 1][64], column T = dummy inf
+  for (int t = 0; t <= T; ++t) col[t * kTmLanes + lane] = (t == src) ? 0 : (V)inf;
+  int16_t* prevT = a.prevT + (size_t)b * Tm * Tm;  // [q][src]
+  if (valid)
+    for (int q = 0; q < T; ++q) prevT[(size_t)q * Tm + src] = -1;
+  const uint32_t* sched = sched_all + (size_t)b * a.sched_stride;
+  const int nslots = a.nslots[b];
+  uint32_t mx = 0;
+  // lanes past T relax too (their rows stay inf, so nothing changes and they never
+  // store a predecessor)
+  for (int sweep = 0; sweep < K; ++sweep) {
+    if (sizeof(V) == 1 && __ballot(mx + (uint32_t)nlev >= inf) != 0) {
+      if (lane == 0) a.overflow[b] = 1;
+      return;
+    }
+    int changed = 0;
+    uint32_t nxt[kBatch];
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k) nxt[k] = sched[k];
+    for (int j = 0; j < nslots; j += kBatch) {
+      uint32_t w[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt[k]);
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) nxt[k] = sched[j + kBatch + k];  // next batch (slack in the stride)
+      uint32_t vs[kBatch], vq[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        vs[k] = col[(w[k] & 0xFFFF) * kTmLanes + lane];
+        vq[k] = col[(w[k] >> 16) * kTmLanes + lane];
+      }
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const uint32_t via = vs[k] + 1u;  // inf + 1 never wins
+        const bool better = via < vq[k];
+        col[(w[k] >> 16) * kTmLanes + lane] = (V)(via < vq[k] ? via : vq[k]);
+        changed |= better ? 1 : 0;
+        if (better) prevT[(size_t)(w[k] >> 16) * Tm + src] = (int16_t)(w[k] & 0xFFFF);
+      }
+    }
+    if (!PASS_B || sizeof(V) == 1) {
+      bool any_inf_lane;
+      tm_scan(col, T, lane, valid, any_inf_lane, mx);
+      if (!PASS_B) {
+        const bool any_changed = __ballot(changed) != 0;
+        const bool any_inf = __ballot(any_inf_lane) != 0;
+        if (lane == 0) flags[sweep] = (any_changed ? 1 : 0) | (any_inf ? 2 : 0);
+        if (!any_changed) {  // a fixed point: later sweeps change nothing
+          for (int k = sweep + 1 + lane; k < a.kcap; k += kTmLanes) flags[k] = any_inf ? 2 : 0;
+          break;
+        }
+      }
+    }
+  }
+  // cost rows, row-major [src][t] as uint16 (inf = 0xFFFF); 4 entries per 8-byte store
+  if (valid) {
+    auto ent = [&](int t) -> uint64_t {
+      const uint32_t v = col[t * kTmLanes + lane];
+      return v == inf ? 0xFFFFull : (uint64_t)v;
+    };
+    uint16_t* row = a.cost + ((size_t)b * Tm + src) * Tm;
+    int t = 0;
+    if ((Tm & 3) == 0)
+      for (; t + 4 <= T; t += 4)
+        *reinterpret_cast<uint64_t*>(row + t) = ent(t) | (ent(t + 1) << 16) | (ent(t + 2) << 32) | (ent(t + 3) << 48);
+    for (; t < T; ++t) row[t] = (uint16_t)ent(t);
+  }
+}
+
+// controller(greedy=True) without the random draws: one wave per robot.
+__global__ __launch_bounds__(256) void cov_greedy_kernel(CovGreedyArgs a) {
+  const int b = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.y * 4 + wave;
+  if (i >= a.R) return;
+  const int R = a.R, Tm = a.Tmax;
+  const int T = a.ntg[b];
+  const double* tg = a.tgt + (size_t)b * Tm * 2;
+  int c;
+  if (a.dirty[b]) {  // robots were placed externally: closest_targets (:427-432)
+    const double px = a.xr[((size_t)b * R + i) * 2], py = a.xr[((size_t)b * R + i) * 2 + 1];
+    double best = __builtin_inf();
+    int arg = T;
+    for (int t = lane; t < T; t += 64) {
+      const double dx = px - tg[2 * t], dy = py - tg[2 * t + 1];
+      const double d = sqrt(dx * dx + dy * dy);
+      if (d < best) {
+        best = d;
+        arg = t;
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ob = __shfl_xor(best, off);
+      const int oa = __shfl_xor(arg, off);
+      if (ob < best || (ob == best && oa < arg)) {
+        best = ob;
+        arg = oa;
+      }
+    }
+    c = arg;
+  } else {
+    c = a.cur[(size_t)b * R + i] - R;
+  }
+  // r = graph_cost[c, :] with visited targets masked (:817-818) — and, the reference
+  // indexing with np.where's (rows, cols) tuple on the (T,1) visited column, target 0
+  // as well whenever any target is visited
+  const uint16_t* row = a.cost + ((size_t)b * Tm + c) * Tm;
+  const uint8_t* vis = a.visited + (size_t)b * Tm;
+  const bool any_vis = a.nvisited[b] > 0;
+  uint32_t key = 0xFFFFFFFFu;
+  auto consider = [&](uint32_t v, uint32_t visited, int t) {
+    if (v == kInf || visited || (t == 0 && any_vis)) v = kMaxCost;
+    const uint32_t kt = (v << 16) | (uint32_t)t;  // min value, then first index (np.argmin)
+    key = kt < key ? kt : key;
+  };
+  int t0 = 0;
+  if ((Tm & 7) == 0) {  // 8 targets per lane per load: 16 B of costs, 8 B of flags
+    for (; t0 + 8 * 64 <= T; t0 += 8 * 64) {
+      const int t = t0 + 8 * lane;
+      const uint4 cv = *reinterpret_cast<const uint4*>(row + t);
+      const uint2 fv = *reinterpret_cast<const uint2*>(vis + t);
+      const uint32_t c4[4] = {cv.x, cv.y, cv.z, cv.w};
+      const uint32_t f2[2] = {fv.x, fv.y};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) consider((c4[k >> 1] >> (16 * (k & 1))) & 0xFFFF, (f2[k >> 2] >> (8 * (k & 3))) & 0xFF, t + k);
+    }
+  }
+  for (int t = t0 + lane; t < T; t += 64) consider(row[t], vis[t], t);
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)key, off);
+    key = o < key ? o : key;
+  }
+  if (lane != 0) return;
+  const int goal = key & 0xFFFF;
+  const int cost = key >> 16;
+  int act = 0;
+  bool rnd = cost == kMaxCost;  // no unvisited target within the horizon (:821-823)
+  if (!rnd) {
+    const int p = a.prevT[((size_t)b * Tm + c) * Tm + goal];  // graph_previous[goal, c]
+    if (p < 0) {
+      rnd = true;  // :863
+    } else {
+      // index of the next hop among the robot's action targets (:869)
+      const int* nb = a.nbr + ((size_t)b * Tm + c) * 4;
+      const int n = a.cnt[(size_t)b * Tm + c];
+      act = -1;
+      for (int k = n - 1; k >= 0; --k)
+        if (nb[k] == p) act = k;
+      if (act < 0) {  // the reference's np.where(..)[0][0] raises IndexError
+        atomicOr(a.err, 8);
+        act = 0;
+      }
+    }
+  }
+  a.actions[(size_t)b * R + i] = act;
+  a.needs_random[(size_t)b * R + i] = rnd ? 1 : 0;
+}
+
+}  // namespace
+
+size_t cov_time_matrix_lds_bytes(int t_lds, bool wide) { return (size_t)(t_lds + 1) * kTmLanes * (wide ? 2 : 1); }
+
+size_t cov_tm_schedule_lds_bytes(int t_lds, int e_max) { return (size_t)(2 * t_lds + 2 * e_max + 1) * 4; }
+
+hipError_t launch_cov_tm_schedule(const CovTmArgs& a, int n_envs_sel, int e_max, hipStream_t s) {
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cov_tm_schedule_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cov_tm_schedule_kernel, dim3(n_envs_sel), dim3(64), cov_tm_schedule_lds_bytes(a.t_lds, e_max), s, a);
+  return hipGetLastError();
+}
+
+template <typename V>
+static hipError_t launch_tm_passes(const CovTmArgs& a, int n_envs_sel, hipStream_t s) {
+  const dim3 grid((a.t_lds + kTmLanes - 1) / kTmLanes, n_envs_sel);
+  const size_t lds = cov_time_matrix_lds_bytes(a.t_lds, sizeof(V) == 2);
+  for (const void* f : {reinterpret_cast<const void*>(&cov_time_matrix_kernel<V, false>),
+                        reinterpret_cast<const void*>(&cov_time_matrix_kernel<V, true>)}) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((cov_time_matrix_kernel<V, false>), grid, dim3(kTmLanes), lds, s, a, a.sched);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((cov_time_matrix_kernel<V, true>), grid, dim3(kTmLanes), lds, s, a, a.sched);
+  return hipGetLastError();
+}
+
+hipError_t launch_cov_time_matrix(const CovTmArgs& a, int n_envs_sel, bool wide, hipStream_t s) {
+  return wide ? launch_tm_passes<uint16_t>(a, n_envs_sel, s) : launch_tm_passes<uint8_t>(a, n_envs_sel, s);
+}
+
+hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(cov_greedy_kernel, dim3(a.B, (a.R + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gf

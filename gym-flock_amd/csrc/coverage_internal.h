@@ -32,6 +32,53 @@ struct CovArgs {
   int* err;               // device error bits: 1 degree > 4, 2 edges overflow, 4 bad action
 };
 
+// Greedy expert (coverage_expert.hip).
+struct CovTmArgs {
+  int R, M, Tmax, horizon;
+  int kcap;                  // flag slots per chunk: horizon+1, or Tmax+1 when unbounded
+  int nchunk;                // (Tmax + 63) / 64
+  int t_lds;                 // largest target count among the selected envs
+  const int32_t* envs;       // selected envs (blockIdx.y)
+  const int32_t* ntg;        // (B)
+  const int32_t* n_motion;   // (B)
+  const int32_t* senders;    // (B,4M): motion edges first (global indices)
+  const int32_t* receivers;  // (B,4M)
+  uint8_t* flags;            // (B,nchunk,kcap): bit 0 changed, bit 1 some entry inf
+  uint16_t* cost;            // (B,Tmax,Tmax) [source][target], 0xFFFF = inf
+  int16_t* prevT;            // (B,Tmax,Tmax) [q][source] = graph_previous[source, q]
+  uint32_t* sched;           // (B,sched_stride) batched edge schedule
+  int32_t* nslots;           // (B) schedule length
+  int32_t* nlev;             // (B) schedule levels
+  uint8_t* overflow;         // (B) the uint8 pass could not bound an entry: rerun wide
+  int sched_stride;
+};
+
+struct CovGreedyArgs {
+  int B, R, Tmax;
+  const int32_t* ntg;
+  const double* tgt;
+  const double* xr;
+  const uint8_t* dirty;
+  const int32_t* cur;
+  const uint16_t* cost;
+  const int16_t* prevT;
+  const uint8_t* visited;
+  const int32_t* nvisited;
+  const int32_t* nbr;
+  const int32_t* cnt;
+  int32_t* actions;        // (B,R)
+  uint8_t* needs_random;   // (B,R)
+  int* err;                // 8: next hop not among the robot's actions
+};
+
+size_t cov_time_matrix_lds_bytes(int t_lds, bool wide);
+size_t cov_tm_schedule_lds_bytes(int t_lds, int e_max);
+hipError_t launch_cov_tm_schedule(const CovTmArgs& a, int n_envs_sel, int e_max, hipStream_t s);
+// Pass A + pass B over the selected envs; wide = uint16 entries (else uint8, which sets
+// overflow[b] for envs it cannot bound).
+hipError_t launch_cov_time_matrix(const CovTmArgs& a, int n_envs_sel, bool wide, hipStream_t s);
+hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s);
+
 size_t cov_step_lds_bytes(int R, int M);
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s);
 hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_t* visited0, hipStream_t s);

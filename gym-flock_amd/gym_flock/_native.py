@@ -45,7 +45,7 @@ class CovConfig(ctypes.Structure):
     _fields_ = [("n_robots", ctypes.c_int32), ("n_envs", ctypes.c_int32),
                 ("max_nodes", ctypes.c_int32), ("episode_length", ctypes.c_int32),
                 ("res", ctypes.c_double), ("motion_radius", ctypes.c_double),
-                ("device", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("horizon", ctypes.c_int32)]
 
 
 COV_ACTIONS_DEVICE = 0x1
@@ -102,6 +102,8 @@ SIGNATURES = {
     "cov_get_visited": [_P, _I, _P],
     "cov_get_n_motion": [_P, _P],
     "cov_sync": [_P],
+    "cov_controller_greedy": [_P, _P, _P, _P],
+    "cov_get_time_matrix": [_P, _I, _P, _P],
     "fe_last_error": [],
     "fe_abi_version": [],
     "fe_diag": [_P, _I, _I, ctypes.POINTER(ctypes.c_double)],
@@ -325,12 +327,12 @@ class CoverageHandle:
     """Owns one cov_handle: B Coverage-v0 envs with R robots, max_nodes padded nodes."""
 
     def __init__(self, n_robots, n_envs=1, max_nodes=500, episode_length=75, res=5.5,
-                 motion_radius=None, device=0):
+                 motion_radius=None, device=0, horizon=10):
         self.lib = load()
         if motion_radius is None:
             motion_radius = res * 1.2
         self.cfg = CovConfig(int(n_robots), int(n_envs), int(max_nodes), int(episode_length),
-                             float(res), float(motion_radius), int(device))
+                             float(res), float(motion_radius), int(device), int(horizon))
         self.n_robots, self.n_envs, self.max_nodes = int(n_robots), int(n_envs), int(max_nodes)
         self.t_max = self.max_nodes - self.n_robots
         h = ctypes.c_void_p()
@@ -407,3 +409,23 @@ class CoverageHandle:
 
     def sync(self):
         check(self.lib.cov_sync(self.h))
+
+    def controller_greedy(self, fetch=True):
+        """Greedy expert actions (B,R) int32 and the (B,R) bool mask of robots the
+        reference hands to np_random.choice(4); the actions also stay resident for
+        step(resident=True). fetch=False leaves both on the device (no sync)."""
+        if not fetch:
+            check(self.lib.cov_controller_greedy(self.h, None, None, None))
+            return None, None
+        a = np.empty((self.n_envs, self.n_robots), np.int32)
+        rnd = np.empty((self.n_envs, self.n_robots), np.uint8)
+        n = ctypes.c_int64()
+        check(self.lib.cov_controller_greedy(self.h, ptr(a), ptr(rnd), ctypes.byref(n)))
+        return a, rnd.astype(bool)
+
+    def time_matrix(self, env, n_targets):
+        """(graph_cost, graph_previous) of one env, each (T,T) int32."""
+        c = np.empty((n_targets, n_targets), np.int32)
+        p = np.empty((n_targets, n_targets), np.int32)
+        check(self.lib.cov_get_time_matrix(self.h, int(env), ptr(c), ptr(p)))
+        return c, p

@@ -2,7 +2,8 @@
 
 Same constructor arguments, `keys`, spaces and methods as the reference
 (`__init__` :83-164, `seed` :166-172, `step` :174-204, `reset` :366-425,
-`closest_targets` :427-432, `controller(random=True)` :805-806). The step — action
+`closest_targets` :427-432, `controller` :800-872 with its random and greedy
+branches, `construct_time_matrix` :621-653). The step — action
 targets, collision-resolved moves, visited/reward and the padded graph observation —
 and the per-graph setup (motion radius graph, static observation) run in
 libgymflock.so (cov_* C-ABI). Host code keeps what the reference draws from its RNGs:
@@ -39,6 +40,9 @@ unvisited_regions = [(-100, 100, -100, 100)]
 start_regions = [(-100, 100, -100, 100)]
 
 
+MAX_COST = 1000  # coverage.py:68
+
+
 class CoverageEnv(Env):
     def __init__(self, n_robots=N_ROBOTS, frac_active_targets=FRAC_ACTIVE, xmax=XMAX, ymax=YMAX,
                  starts=start_regions, unvisiteds=unvisited_regions, init_graph=True,
@@ -72,7 +76,8 @@ class CoverageEnv(Env):
         self.obs_radius = self.res * 1.2
         self.n_actions = N_ACTIONS
         self.device = device
-        self._h = nat.CoverageHandle(n_robots, 1, max_nodes, episode_length, res, self.motion_radius, device)
+        self._h = nat.CoverageHandle(n_robots, 1, max_nodes, episode_length, res, self.motion_radius, device,
+                                     horizon=horizon)
         if init_graph:
             targets, _ = self._generate_targets()
             self._initialize_graph(targets)
@@ -180,11 +185,41 @@ class CoverageEnv(Env):
         return np.r_[np.ones(self.n_robots), self._h.visited(0)[:self.n_targets]].reshape(-1, 1)
 
     def controller(self, random=False, greedy=False, reset_solution=False):
-        """coverage.py:800-806 (random branch). The greedy/VRP experts are not on the
-        step hot path."""
+        """coverage.py:800-872. random: np_random.choice over the 4 actions. greedy: the
+        device expert (time matrix :621-653 built once per graph, nearest unvisited target,
+        next hop from the predecessor matrix); robots it cannot route draw
+        np_random.choice(4) here, in robot order, as the reference does (:863-864).
+        The OR-Tools routing branch (greedy=False) is out of scope: it
+        fails the way the reference does without OR-Tools installed."""
         if random:
             return self.np_random.choice(self.n_actions, size=(self.n_robots, 1))
-        raise NotImplementedError("greedy / VRP expert controllers are not implemented yet")
+        if not greedy:
+            raise AssertionError("Vehicle routing controller is not available if OR-Tools is not imported.")
+        a, rnd = self._h.controller_greedy()
+        a = a[0].copy()
+        for i in np.nonzero(rnd[0])[0]:
+            a[i] = self.np_random.choice(self.n_actions)
+        return a.reshape(self.n_robots, 1).astype(np.int32)
+
+    def construct_time_matrix(self, edge_time=1.0):
+        """coverage.py:621-653 on the device: (time_matrix with inf -> MAX_COST, prev)."""
+        if edge_time != 1.0:
+            raise NotImplementedError("only the reference's uniform edge_time=1.0 is implemented")
+        cost, prev = self._h.time_matrix(0, self.n_targets)
+        return cost.astype(np.float64), prev.astype(np.int64)
+
+    @property
+    def graph_cost(self):
+        return self.construct_time_matrix()[0]
+
+    @property
+    def graph_previous(self):
+        return self.construct_time_matrix()[1]
+
+    @property
+    def graph_diameter(self):
+        c = self.graph_cost
+        return np.max(c[c < MAX_COST])
 
     def render(self, mode='human'):
         pass

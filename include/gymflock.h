@@ -149,6 +149,8 @@ typedef struct cov_config {
   double res;              /* lattice spacing, edge-feature scale (DELTA 5.5, :80)       */
   double motion_radius;    /* res * 1.2 (:136)                                          */
   int32_t device;
+  int32_t horizon;         /* greedy expert: relaxation sweeps - 1 (HORIZON=10, :66);
+                              -1 = until converged                                       */
 } cov_config;
 
 typedef struct cov_handle cov_handle;
@@ -178,6 +180,18 @@ int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes); /* close
 int cov_get_visited(cov_handle* h, int env, uint8_t* visited);
 int cov_get_n_motion(cov_handle* h, int32_t* n_motion);
 int cov_sync(cov_handle* h);
+/* Greedy expert, controller(greedy=True) :800-872. On first use after cov_set_targets
+ * it builds each env's time matrix (construct_time_matrix :621-653) on the device;
+ * then every robot heads for its nearest unvisited target via the predecessor matrix.
+ * The actions stay resident for cov_step(.., COV_ACTIONS_RESIDENT). Robots the
+ * reference hands to np_random.choice(4) (target out of reach, :839-844 and :863-864)
+ * get action 0 and needs_random = 1: draw those on the host in robot order and upload
+ * the patched array with cov_set_actions. actions[B][R], needs_random[B][R] and
+ * n_random may be NULL; with all three NULL the call does not synchronise. */
+int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random, int64_t* n_random);
+/* One env's graph_cost (inf -> MAX_COST=1000, as :651) and graph_previous, each
+ * (T,T) row-major, T = that env's target count; builds the matrix if needed. */
+int cov_get_time_matrix(cov_handle* h, int env, int32_t* cost, int32_t* prev);
 
 /* Diagnostics ---------------------------------------------------------------- */
 const char* fe_last_error(void);

@@ -1,0 +1,211 @@
+"""Parity of the HIP greedy expert (construct_time_matrix :621-653, controller(greedy=True)
+:800-872) with the reference's recorded greedy episodes and the CPU oracle, through the
+C-ABI. Time matrices, predecessors and actions are integers: compared bit-exactly.
+Needs an MI355X."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import coverage as oc
+
+pytestmark = pytest.mark.gpu
+
+nat = pytest.importorskip("gym_flock._native")
+from gym_flock.vec import VecCoverage  # noqa: E402
+
+GREEDY = sorted(glob.glob(os.path.join(GOLDEN, "coverage_r*_greedy.npz")))
+ENV_SEED = {"coverage_r6_greedy.npz": 6, "coverage_r20_greedy.npz": 13}
+MAP_SEED = {"coverage_r6_greedy.npz": 5, "coverage_r20_greedy.npz": 12}
+
+
+def _handle_for(f, horizon=10):
+    R, T, M = int(f["n_robots"]), int(f["n_targets"]), int(f["max_nodes"])
+    h = nat.CoverageHandle(R, 1, M, horizon=horizon)
+    h.set_targets(f["targets"], env=0)
+    return h, R, T, M
+
+
+@pytest.mark.parametrize("path", GREEDY, ids=os.path.basename)
+def test_time_matrix_matches_reference(path):
+    f = np.load(path)
+    h, R, T, M = _handle_for(f)
+    cost, prev = h.time_matrix(0, T)
+    np.testing.assert_array_equal(cost, f["graph_cost"])
+    np.testing.assert_array_equal(prev, f["graph_previous"])
+    h.close()
+
+
+@pytest.mark.parametrize("path", GREEDY, ids=os.path.basename)
+def test_greedy_episode_matches_reference(path):
+    """The whole recorded greedy episode through the handle, random fallbacks drawn on
+    the host from the replayed env RNG."""
+    f = np.load(path)
+    h, R, T, M = _handle_for(f)
+    start = oc.closest_targets(f["x0"][:R], f["targets"], R) - R
+    visited = np.ones((1, M - R), np.uint8)
+    visited[0, :T] = f["visited0"][R:].astype(np.uint8)
+    h.reset(start[None], visited)
+    rs = np.random.RandomState(ENV_SEED[os.path.basename(path)])
+    rs.choice(np.arange(T), size=(R,), replace=False)
+    rs.choice(np.arange(T) + R, size=(int(T * 0.5),), replace=False)
+    for t in range(len(f["actions"])):
+        a, rnd = h.controller_greedy()
+        a = a[0].copy()
+        for i in np.nonzero(rnd[0])[0]:
+            a[i] = rs.choice(4)
+        np.testing.assert_array_equal(a, f["actions"][t])
+        h.step(a[None])
+        np.testing.assert_array_equal(h.robots(0)[1], f["closest"][t])
+    h.close()
+
+
+@pytest.mark.parametrize("path", GREEDY, ids=os.path.basename)
+def test_env_api_greedy_controller(path):
+    """CoverageEnv.controller(greedy=True) with the fixture's seeds reproduces the
+    reference's expert episode, including its np_random fallback draws."""
+    from gym_flock.envs.spatial import CoverageEnv
+    f = np.load(path)
+    name = os.path.basename(path)
+    np.random.seed(MAP_SEED[name])
+    env = CoverageEnv(n_robots=int(f["n_robots"]), nearby_starts=False, max_nodes=int(f["max_nodes"]))
+    env.seed(ENV_SEED[name])
+    np.random.seed(MAP_SEED[name])
+    env.reset()
+    for t in range(len(f["actions"])):
+        a = env.controller(random=False, greedy=True)
+        assert a.shape == (int(f["n_robots"]), 1) and a.dtype == np.int32
+        np.testing.assert_array_equal(a[:, 0], f["actions"][t])
+        _, r, d, _ = env.step(a)
+        assert r == f["reward"][t] and d == f["done"][t]
+    np.testing.assert_array_equal(env.graph_cost, f["graph_cost"])
+    np.testing.assert_array_equal(env.graph_previous, f["graph_previous"])
+    with pytest.raises(AssertionError):
+        env.controller(random=False, greedy=False)  # OR-Tools routing: not available
+    env.close()
+
+
+def _two_clusters():
+    """A disconnected map: two lattice patches 60 m apart (inf entries never clear, so
+    the reference's loop stops on "no change")."""
+    xs, ys = np.meshgrid(np.arange(7) * 5.5, np.arange(5) * 5.5)
+    a = np.stack([xs.ravel(), ys.ravel()], axis=1)
+    return np.concatenate([a, a + np.array([60.0, 0.0])])
+
+
+def _line(n=300):
+    """A 300-target path: hop counts up to 299 exceed the uint8 entries, so the device
+    reruns the env with uint16 entries."""
+    return np.stack([np.arange(n) * 5.5, np.zeros(n)], axis=1)
+
+
+@pytest.mark.parametrize("horizon", [-1, 0, 1, 3, 10])
+@pytest.mark.parametrize("which", ["map", "clusters", "line"])
+def test_time_matrix_horizons_vs_oracle(horizon, which):
+    """Sweep counts set by each arm of the stop rule: the horizon break, no inf left,
+    and no change (disconnected graph), for several horizons including unbounded; the
+    line exercises the wide (uint16) fallback."""
+    if which == "map":
+        from gym_flock.envs.spatial.maps import generate_targets
+        np.random.seed(21)
+        targets = generate_targets()
+    elif which == "clusters":
+        targets = _two_clusters()
+    else:
+        targets = _line()
+    R, M = 8, len(targets) + 8 + 2
+    h = nat.CoverageHandle(R, 1, M, horizon=horizon)
+    h.set_targets(targets, env=0)
+    o = oc.CoverageOracle(targets, R, M)
+    cost, prev = h.time_matrix(0, len(targets))
+    ec, ep = oc.time_matrix(len(targets), o.motion[0] - R, o.motion[1] - R, horizon=horizon)
+    np.testing.assert_array_equal(cost, ec)
+    np.testing.assert_array_equal(prev, ep)
+    h.close()
+
+
+def _greedy_phase(v, maps, R, M, seed, steps):
+    B = len(maps)
+    start, visited = v.reset(seed=seed)
+    orcs, mats = [], []
+    for b in range(B):
+        o = oc.CoverageOracle(maps[b], R, M)
+        T = len(maps[b])
+        o.reset(start[b], np.nonzero(visited[b, :T] == 0)[0] + R)
+        orcs.append(o)
+        mats.append(oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R))
+    rngs = [np.random.RandomState(1000 + b) for b in range(B)]
+    n_rand = 0
+    for t in range(steps):
+        a, rnd = v.h.controller_greedy()
+        for b in range(B):
+            cur = orcs[b].closest()
+            recv = oc.action_receivers(cur, orcs[b].nbr, orcs[b].cnt, R)
+            ea, er = oc.greedy_actions(mats[b][0], mats[b][1], cur, orcs[b].visited[R:], recv, R)
+            np.testing.assert_array_equal(rnd[b], er)
+            np.testing.assert_array_equal(a[b][~er], ea[~er])
+            for i in np.nonzero(er)[0]:
+                a[b, i] = rngs[b].choice(4)
+                n_rand += 1
+        v.step(a)
+        r, d = v.rewards()
+        for b in range(B):
+            _, rr, dd = orcs[b].step(a[b])
+            assert r[b] == rr and d[b] == dd
+    for b in range(B):
+        cost, prev = v.h.time_matrix(b, len(maps[b]))
+        np.testing.assert_array_equal(cost, mats[b][0])
+        np.testing.assert_array_equal(prev, mats[b][1])
+    return n_rand
+
+
+def test_batched_greedy_vs_oracle():
+    """6 envs, each its own map (different target counts, so per-env chunk counts
+    differ), greedy for 20 steps against the oracle with per-env fallback RNGs; then a
+    new graph for env 2 (only its matrix is stale) and another phase."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, R, M = 6, 16, 800
+    maps = []
+    for b in range(B):
+        np.random.seed(300 + b)
+        maps.append(generate_targets())
+    v = VecCoverage(B, R, max_nodes=M)
+    for b in range(B):
+        v.set_targets(maps[b], env=b)
+    _greedy_phase(v, maps, R, M, seed=11, steps=20)
+    np.random.seed(999)
+    maps[2] = generate_targets()
+    v.set_targets(maps[2], env=2)
+    _greedy_phase(v, maps, R, M, seed=12, steps=20)
+    v.close()
+
+
+def test_greedy_resident_actions_and_external_positions():
+    """controller_greedy(fetch=False) leaves the actions on the device for
+    step(resident=True); robots placed off-node use freshly computed closest nodes."""
+    f = np.load(GREEDY[0])
+    h, R, T, M = _handle_for(f)
+    o = oc.CoverageOracle(f["targets"], R, M)
+    cost, prev = oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R)
+    start = np.arange(R) * (T // R)
+    h.reset(start[None], np.zeros((1, M - R), np.uint8))
+    o.reset(start, np.arange(T) + R)
+    xr = f["targets"][start] + np.random.RandomState(4).uniform(-2.0, 2.0, size=(R, 2))
+    h.set_robot_positions(0, xr)
+    o.xr = xr.copy()
+    cur = o.closest()
+    ea, er = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+    assert not er.any()
+    a, rnd = h.controller_greedy()
+    np.testing.assert_array_equal(a[0], ea)
+    for t in range(5):
+        h.controller_greedy(fetch=False)
+        h.step(resident=True)
+        cur = o.closest()
+        ea, er = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+        ea[er] = 0  # the device leaves action 0 where the host would draw
+        o.step(ea)
+        np.testing.assert_array_equal(h.robots(0)[1], o.closest())
+    h.close()
