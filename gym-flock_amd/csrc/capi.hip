@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -81,6 +82,11 @@ struct fe_handle {
   hipEvent_t ag_ev[kBlocks] = {};
   bool ag_pending[kBlocks] = {};
   int last_gather = -1, last_count = 0;
+  // flocking variant (fe_set_variant / fe_set_dt)
+  bool has_variant = false;
+  fe_variant var{};
+  double* dt_env = nullptr;             // (B) per-env dt
+  bool dt_per_env = false;
 };
 
 namespace {
@@ -108,7 +114,7 @@ void release(fe_handle* h) {
   if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather};
+                  h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -160,6 +166,24 @@ gf::StepArgs base_args(fe_handle* h) {
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
   a.lds_pad = h->lds_pad;
+  a.u_scale = h->cfg.action_scalar;
+  a.us_f = a.as_f;
+  a.x_scale = 1.0;
+  if (h->has_variant || h->dt_per_env) {
+    a.variant = 1;
+    a.resident = 0;  // variants run on the tiled kernel
+    if (h->has_variant) {
+      a.n_frozen = h->var.n_frozen;
+      a.n_vel_zero = h->var.n_vel_zero;
+      a.u_scale = h->var.u_scale;
+      a.u_clip = h->var.u_clip;
+      a.x_scale = h->var.x_scale;
+      a.ctrl_clip = h->var.ctrl_clip;
+      a.us_f = static_cast<float>(a.u_scale);
+      a.uc_f = static_cast<float>(a.u_clip);
+    }
+    a.dt_env = h->dt_per_env ? h->dt_env : nullptr;
+  }
   return a;
 }
 
@@ -410,6 +434,35 @@ int fe_step(fe_handle* h, const void* u, int flags) {
     if (int rc = launch_knn_cur(h)) return rc;
   // the host action buffer is borrowed only for this call: wait for its copy, not the step
   if (!(flags & (FE_U_DEVICE | FE_U_EXPERT | FE_U_RESIDENT))) GF_HIP(hipEventSynchronize(h->h2d_ev));
+  return GF_OK;
+}
+
+int fe_set_variant(fe_handle* h, const fe_variant* v) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!v) {
+    h->has_variant = false;
+    return GF_OK;
+  }
+  if (v->n_frozen < 0 || v->n_vel_zero < 0) return fail(GF_EINVAL, "negative agent count");
+  if (!(v->x_scale != 0.0) || !std::isfinite(v->x_scale) || !std::isfinite(v->u_scale))
+    return fail(GF_EINVAL, "x_scale must be finite and non-zero, u_scale finite");
+  h->var = *v;
+  h->has_variant = true;
+  return GF_OK;
+}
+
+int fe_set_dt(fe_handle* h, const double* dt) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!dt) {
+    h->dt_per_env = false;
+    return GF_OK;
+  }
+  if (int rc = use_dev(h)) return rc;
+  if (!h->dt_env)
+    if (int rc = dalloc(&h->dt_env, (size_t)h->cfg.n_envs)) return rc;
+  GF_HIP(hipMemcpyAsync(h->dt_env, dt, (size_t)h->cfg.n_envs * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  h->dt_per_env = true;
   return GF_OK;
 }
 

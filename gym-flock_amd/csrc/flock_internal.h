@@ -34,6 +34,17 @@ struct StepArgs {
   int diag;               // ablation switches (0 in production): 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
                           // unwritten: timing only), 16 skip tile loads (timing only)
+  // Flocking variants (flocking_leader/obstacle/stoch.py). variant == 0 keeps the
+  // FlockingRelative path untouched; otherwise the fields below apply (tiled kernel).
+  int variant;
+  int n_frozen;           // agents [0,n) ignore actions (their mask is 0)
+  int n_vel_zero;         // pairs touching agents [0,n) have zero velocity difference
+  double u_scale;         // the step's action multiplier (action_scalar is the controller's)
+  double u_clip;          // clip actions to +-u_clip before scaling; <= 0: none
+  double x_scale;         // state multiplied before / divided after the update
+  double ctrl_clip;       // controller output clip; <= 0: none
+  float us_f, uc_f;       // float32 copies of u_scale, u_clip
+  const double* dt_env;   // (B) per-env dt of this step, or nullptr (dt)
 };
 
 struct KnnArgs {

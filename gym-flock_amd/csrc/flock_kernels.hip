@@ -64,12 +64,66 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // flocking_relative.py:96-105, in the reference's operation order. With a float32 u
 // the action terms are float32 arithmetic (NumPy keeps u*10.0, *dt, *0.5 in float32)
 // and are widened when added to the float64 state.
-template <bool DYN, bool UF64>
+template <class V>
+__device__ __forceinline__ V clip_sym(V v, V c) {  // np.clip(v, -c, c); NaN stays NaN
+  return v < -c ? -c : (v > c ? c : v);
+}
+
+// The variants' update (oracle/flocking_variants.integrate): optional clip, the
+// step's own action scale, per-env dt, the frozen agents' float64 mask applied after
+// the action arithmetic, and the stochastic env's state scaling around the update.
+template <bool UF64>
+__device__ St load_state_variant(const StepArgs& a, size_t g, double2 p, double2 v) {
+  const int b = static_cast<int>(g / static_cast<size_t>(a.N));
+  const int j = static_cast<int>(g - static_cast<size_t>(b) * a.N);
+  const double dt = a.dt_env ? a.dt_env[b] : a.dt;
+  const double m = j < a.n_frozen ? 0.0 : 1.0;
+  const double S = a.x_scale;
+  const double px = p.x * S, py = p.y * S, vx = v.x * S, vy = v.y * S;
+  double apx, apy, avx, avy;
+  if constexpr (UF64) {
+    const double2 u = reinterpret_cast<const double2*>(a.u)[g];
+    double ux = u.x, uy = u.y;
+    if (a.u_clip > 0) {
+      ux = clip_sym(ux, a.u_clip);
+      uy = clip_sym(uy, a.u_clip);
+    }
+    ux *= a.u_scale;
+    uy *= a.u_scale;
+    apx = (((ux * dt) * dt) * 0.5) * m;
+    apy = (((uy * dt) * dt) * 0.5) * m;
+    avx = (ux * dt) * m;
+    avy = (uy * dt) * m;
+  } else {
+    const float2 u = reinterpret_cast<const float2*>(a.u)[g];
+    const float dtf = static_cast<float>(dt);
+    float ux = u.x, uy = u.y;
+    if (a.u_clip > 0) {
+      ux = clip_sym(ux, a.uc_f);
+      uy = clip_sym(uy, a.uc_f);
+    }
+    ux *= a.us_f;
+    uy *= a.us_f;
+    apx = static_cast<double>(((ux * dtf) * dtf) * 0.5f) * m;
+    apy = static_cast<double>(((uy * dtf) * dtf) * 0.5f) * m;
+    avx = static_cast<double>(ux * dtf) * m;
+    avy = static_cast<double>(uy * dtf) * m;
+  }
+  St s;
+  s.px = ((px + vx * dt) + apx) / S;
+  s.py = ((py + vy * dt) + apy) / S;
+  s.vx = (vx + avx) / S;
+  s.vy = (vy + avy) / S;
+  return s;
+}
+
+template <bool DYN, bool UF64, bool VAR = false>
 __device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
   const double2* xp = reinterpret_cast<const double2*>(a.x_in) + 2 * g;
   const double2 p = xp[0], v = xp[1];
   St s{p.x, p.y, v.x, v.y};
   if constexpr (DYN) {
+    if constexpr (VAR) return load_state_variant<UF64>(a, g, p, v);
     if constexpr (UF64) {
       const double2 u = reinterpret_cast<const double2*>(a.u)[g];
       const double ux = u.x * a.action_scalar, uy = u.y * a.action_scalar;
@@ -151,7 +205,9 @@ __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m,
 #ifndef GF_STEP_MIN_WAVES
 #define GF_STEP_MIN_WAVES 1
 #endif
-template <bool DYN, bool UF64, bool CTRL>
+// VAR: the flocking variants' switches (StepArgs.variant); without it the FlockingRelative
+// path carries none of their instructions.
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
 __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
@@ -175,7 +231,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   const size_t env0 = (size_t)b * N;
 
   // rows owned by this workgroup (post-update state)
-  for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64>(a, env0 + i0 + r);
+  for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
 
   // feature-pass thread mapping: S word-slices per row
   const int S = kThreads / R;
@@ -186,6 +242,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   St me{0, 0, 0, 0};
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
 
+  const int i_row = i0 + fr;  // global row of this thread's feature slice
   // pass 2: features / gradients for the set bits of one tile, ascending j per slice
   auto feature_pass = [&](int j0, int nch) {
     if (!frow || (a.diag & 2)) return;
@@ -206,10 +263,12 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
         const double q1y = dy / rr, q2y = dy / r2;
         const bool isadj = (am >> k) & 1ull;
         if (isadj) {
-          f0 += me.vx - o.vx;
+          // obstacle variant: no velocity difference for pairs touching agents < nvz
+          const bool vz = VAR && (i_row < a.n_vel_zero || j0 + (w << 6) + k < a.n_vel_zero);
+          f0 += vz ? 0.0 : me.vx - o.vx;
           f1 += q1x;
           f2 += q2x;
-          f3 += me.vy - o.vy;
+          f3 += vz ? 0.0 : me.vy - o.vy;
           f4 += q1y;
           f5 += q2y;
         }
@@ -229,7 +288,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
     __syncthreads();  // previous tile fully consumed; rows[] visible on first pass
     float pt = 0.f;
     for (int t = (a.diag & 16) ? tc : tid; t < tc; t += kThreads) {
-      const St s = load_state<DYN, UF64>(a, env0 + j0 + t);
+      const St s = load_state<DYN, UF64, VAR>(a, env0 + j0 + t);
       tile[t] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
       tile32[t] = make_float2(fx, fy);
@@ -423,11 +482,28 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
     }
     if constexpr (CTRL) {
       // centralized: sum over ALL j of (v_i - v_j) = N*v_i - sum_j v_j (:200-208)
-      const double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
-      const double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
+      double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
+      double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
+      if (VAR && a.centralized && a.n_vel_zero > 0) {
+        // obstacle variant: only pairs between free agents count (flocking_obstacle.py:79-80)
+        const int nz = min(a.n_vel_zero, N);
+        double zx = 0, zy = 0;
+        for (int j = 0; j < nz; ++j) {
+          const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
+          zx += s.vx;
+          zy += s.vy;
+        }
+        const bool frozen = i_row < nz;
+        p2 = frozen ? 0.0 : static_cast<double>(N - nz) * me.vx - (Svx - zx);
+        p3 = frozen ? 0.0 : static_cast<double>(N - nz) * me.vy - (Svy - zy);
+      }
       double2 u;
       u.x = clip10(-gx - p2) / a.action_scalar;  // (-p4 - p2), :209-211
       u.y = clip10(-p3 - gy) / a.action_scalar;  // (-p3 - p5)
+      if (VAR && a.ctrl_clip > 0) {  // stochastic variant (flocking_stoch.py:44-45)
+        u.x = clip_sym(u.x, a.ctrl_clip);
+        u.y = clip_sym(u.y, a.ctrl_clip);
+      }
       reinterpret_cast<double2*>(a.ctrl_out)[g] = u;
     }
   }
@@ -445,7 +521,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       }
     } else {
       for (int j = tid; j < N; j += kThreads) {
-        const St s = load_state<DYN, UF64>(a, env0 + j);
+        const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
         const double ex = s.vx - mx, ey = s.vy - my;
         qx += ex * ex;
         qy += ey * ey;
@@ -903,20 +979,26 @@ static hipError_t launch_step_resident_t(const StepArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool DYN, bool UF64, bool CTRL>
-static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
-  if (a.resident) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
+static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   const size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int grid = a.B * a.bpe;
-  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL>), dim3(grid), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR>), dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
+}
+
+template <bool DYN, bool UF64, bool CTRL>
+static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
+  if (a.variant) return launch_step_tiled<DYN, UF64, CTRL, true>(a, s);
+  if (a.resident) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
+  return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
 }
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s) {

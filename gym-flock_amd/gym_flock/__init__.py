@@ -2,7 +2,7 @@
 
 Importing the package registers the env ids it implements with gym (when gym is
 installed), using the reference's ids, entry points and episode limits
-(reference gym_flock/__init__.py:76-99). The per-step work runs in libgymflock.so
+(reference gym_flock/__init__.py:40-94). The per-step work runs in libgymflock.so
 (HIP, gfx950) through a ctypes C-ABI; see include/gymflock.h.
 """
 from gym_flock._spaces import HAVE_GYM
@@ -11,9 +11,13 @@ __version__ = "0.1.0"
 
 # id -> (entry point, max_episode_steps); reference gym_flock/__init__.py
 ENV_IDS = {
-    "FlockingRelative-v0": ("gym_flock.envs.flocking:FlockingRelativeEnv", 1000),  # :95-99
-    "Flocking-v0": ("gym_flock.envs.flocking:FlockingEnv", 1000),                  # :89-93
-    "Coverage-v0": ("gym_flock.envs.spatial:CoverageEnv", 75),                     # :76-80
+    "FlockingRelative-v0": ("gym_flock.envs.flocking:FlockingRelativeEnv", 1000),  # :59-63
+    "Flocking-v0": ("gym_flock.envs.flocking:FlockingEnv", 1000),                  # :53-57
+    "Coverage-v0": ("gym_flock.envs.spatial:CoverageEnv", 75),                     # :40-44
+    "FlockingLeader-v0": ("gym_flock.envs.flocking:FlockingLeaderEnv", 200),        # :65-69
+    "FlockingObstacle-v0": ("gym_flock.envs.flocking:FlockingObstacleEnv", 200),    # :72-76
+    "FlockingStochastic-v0": ("gym_flock.envs.flocking:FlockingStochasticEnv", 500),  # :84-88
+    "FlockingTwoFlocks-v0": ("gym_flock.envs.flocking:FlockingTwoFlocksEnv", 500),  # :90-94
 }
 
 if HAVE_GYM:  # pragma: no cover - gym is not installed in the build image

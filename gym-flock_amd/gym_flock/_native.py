@@ -41,6 +41,12 @@ class FeBuffers(ctypes.Structure):
                 ("knn_obs", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
 
 
+class FeVariant(ctypes.Structure):
+    _fields_ = [("n_frozen", ctypes.c_int32), ("n_vel_zero", ctypes.c_int32),
+                ("u_scale", ctypes.c_double), ("u_clip", ctypes.c_double),
+                ("x_scale", ctypes.c_double), ("ctrl_clip", ctypes.c_double)]
+
+
 class CovConfig(ctypes.Structure):
     _fields_ = [("n_robots", ctypes.c_int32), ("n_envs", ctypes.c_int32),
                 ("max_nodes", ctypes.c_int32), ("episode_length", ctypes.c_int32),
@@ -89,6 +95,8 @@ SIGNATURES = {
     "fe_get_gathered_rewards": [_P, _P],
     "fe_gathered_steps": [_P],
     "fe_comm_destroy": [_P],
+    "fe_set_variant": [_P, _P],
+    "fe_set_dt": [_P, _P],
     "cov_create": [ctypes.POINTER(CovConfig), ctypes.POINTER(_P)],
     "cov_destroy": [_P],
     "cov_set_targets": [_P, _I, _I, _P],
@@ -173,6 +181,26 @@ class FlockHandle:
             self.h = None
 
     __del__ = close
+
+    # -- variants (include/gymflock.h fe_variant)
+    def set_variant(self, n_frozen=0, n_vel_zero=0, u_scale=None, u_clip=0.0, x_scale=1.0,
+                    ctrl_clip=0.0):
+        """Select a flocking variant for later steps; no arguments = FlockingRelative."""
+        v = FeVariant(int(n_frozen), int(n_vel_zero),
+                      float(self.cfg.action_scalar if u_scale is None else u_scale),
+                      float(u_clip or 0.0), float(x_scale), float(ctrl_clip or 0.0))
+        check(self.lib.fe_set_variant(self.h, ctypes.byref(v)))
+
+    def clear_variant(self):
+        check(self.lib.fe_set_variant(self.h, None))
+
+    def set_dt(self, dt):
+        """Per-env dt (B,) for the following steps; None reverts to the config dt."""
+        if dt is None:
+            check(self.lib.fe_set_dt(self.h, None))
+            return
+        d = np.ascontiguousarray(np.broadcast_to(np.asarray(dt, np.float64), (self.n_envs,)))
+        check(self.lib.fe_set_dt(self.h, ptr(d)))
 
     # -- state
     def set_state(self, x, env=None):

@@ -103,7 +103,14 @@ class FlockingRelativeEnv(Env):
                                       self.action_scalar, self.mean_pooling, self.centralized,
                                       self.n_neighbors, self.device)
             self._hkey = key
+            v = self._variant()
+            if v:
+                self._h.set_variant(**v)
         return self._h
+
+    def _variant(self):
+        """fe_variant fields for subclasses that change the step (flocking variants)."""
+        return None
 
     # ------------------------------------------------------------------- state
     @property

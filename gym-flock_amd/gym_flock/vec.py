@@ -12,21 +12,35 @@ from . import _native as nat
 from .init_states import synthetic_batch
 
 
+# fe_variant presets of the registered flocking variants (include/gymflock.h)
+VARIANTS = {
+    "relative": {},
+    "leader": dict(u_scale=1.0, n_frozen=2),                      # flocking_leader.py
+    "obstacle": dict(u_scale=1.0, n_frozen=4, n_vel_zero=4),      # flocking_obstacle.py
+    "stochastic": dict(u_scale=6.0, u_clip=0.5, x_scale=6.0, ctrl_clip=0.5),  # flocking_stoch.py
+    "twoflocks": {},                                              # reset only
+}
+
+
 class VecFlockingRelative:
     """B FlockingRelative-v0 envs of N agents on one GPU.
 
     env_offset: global index of this shard's first env (seeds are env_offset + b),
     so a batch sharded over ranks reproduces the single-device batch.
+    variant: a VARIANTS key or a dict of fe_variant fields (flocking variants).
     """
 
     def __init__(self, n_envs, n_agents, comm_radius=0.9, dt=0.01, v_max=5.0,
                  action_scalar=10.0, mean_pooling=True, centralized=True, n_neighbors=0,
-                 device=0, env_offset=0):
+                 device=0, env_offset=0, variant=None):
         self.n_envs, self.n_agents = int(n_envs), int(n_agents)
         self.v_max = v_max
         self.env_offset = int(env_offset)
         self.h = nat.FlockHandle(n_agents, n_envs, comm_radius, dt, action_scalar,
                                  mean_pooling, centralized, n_neighbors, device)
+        v = VARIANTS[variant] if isinstance(variant, str) else variant
+        if v:
+            self.h.set_variant(**v)
 
     # ------------------------------------------------------------------- state
     def reset(self, seed=0, x=None):
@@ -45,15 +59,18 @@ class VecFlockingRelative:
 
     # ---------------------------------------------------------------- hot path
     def step(self, u=None, controller=False, knn=False, network=True, expert=False,
-             resident=False, device_ptr=None):
+             resident=False, device_ptr=None, dt=None):
         """Advance every env one step.
 
         u: (B,N,2) host actions (float32 or float64 arithmetic like the reference); or
         expert=True to feed back the previous controller() output (closed loop); or
         resident=True to reuse the actions last given to set_actions(); or
         device_ptr=<int> for a device buffer of float32 actions.
+        dt: per-env (B,) time step for this and later steps (the stochastic variant).
         Asynchronous: returns once the launch is queued (host actions are copied first).
         """
+        if dt is not None:
+            self.h.set_dt(dt)
         flags = 0
         if controller:
             flags |= nat.FE_WITH_CONTROLLER

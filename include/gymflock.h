@@ -68,6 +68,24 @@ typedef struct fe_config {
 
 typedef struct fe_handle fe_handle;
 
+/* Flocking variants on the same step. Defaults reproduce
+ * FlockingRelative-v0; the registered variants set (reference files under
+ * gym_flock/envs/flocking/):
+ *   FlockingLeader-v0      u_scale 1, n_frozen 2               (flocking_leader.py:13-15, :21-33)
+ *   FlockingObstacle-v0    u_scale 1, n_frozen 4, n_vel_zero 4 (flocking_obstacle.py:19-21, :34-49, :75-80)
+ *   FlockingStochastic-v0  u_scale 6, u_clip 0.5, x_scale 6, ctrl_clip 0.5, per-step dt
+ *                          (flocking_stoch.py:9-12, :14-36, :39-46; dt via fe_set_dt)
+ *   FlockingTwoFlocks-v0   defaults (only its reset differs, host side)        */
+typedef struct fe_variant {
+  int32_t n_frozen;      /* agents [0,n) ignore actions: their mask is 0 (leaders, obstacles) */
+  int32_t n_vel_zero;    /* pairs touching agents [0,n) have zero velocity difference          */
+  double u_scale;        /* the step's action multiplier (10 = cfg action_scalar by default);
+                            the controller still divides by cfg action_scalar (:211)          */
+  double u_clip;         /* clip actions to +-u_clip before scaling; <= 0: none               */
+  double x_scale;        /* state multiplied before and divided after the update; 1: none     */
+  double ctrl_clip;      /* controller output clip after the /action_scalar; <= 0: none       */
+} fe_variant;
+
 /* Device pointers owned by the handle (valid until fe_destroy). Ping-pong
  * buffers are reported as their CURRENT slot (the one the next getter reads). */
 typedef struct fe_buffers {
@@ -120,6 +138,12 @@ int fe_get_rewards(fe_handle* h, double* dst);               /* (B)   :145-147 *
 int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs); /* (N,k), (N,4k) */
 int fe_device_buffers(fe_handle* h, fe_buffers* out);
 int fe_sync(fe_handle* h);
+/* Select a flocking variant for every later step / controller call (NULL: back to
+ * FlockingRelative). */
+int fe_set_variant(fe_handle* h, const fe_variant* v);
+/* Per-env dt[B] for the following steps (FlockingStochastic-v0 draws one per step,
+ * flocking_stoch.py:24); NULL reverts to cfg dt. */
+int fe_set_dt(fe_handle* h, const double* dt);
 
 /* Multi-GPU metrics path (RCCL over xGMI) ---------------------- */
 /* The env batch is sharded contiguously over ranks (one process per GPU); the

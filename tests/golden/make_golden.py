@@ -182,7 +182,11 @@ def gen_flocking():
 
 if __name__ == "__main__":
     _install_shims()
-    gen_flocking()
+    if "--only-extra" not in sys.argv:
+        gen_flocking()
+    if "--variants" in sys.argv or "--all" in sys.argv:
+        from make_golden_variants import gen_variants  # noqa: E402
+        gen_variants()
     if "--coverage" in sys.argv or "--all" in sys.argv:
         from make_golden_coverage import gen_coverage  # noqa: E402
         gen_coverage()
