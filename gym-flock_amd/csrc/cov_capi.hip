@@ -64,6 +64,10 @@ struct cov_handle {
   std::vector<int> n_motion_host;
   std::vector<char> tm_valid;
   int64_t tm_wide_envs = 0;  // envs whose matrix needed uint16 entries (diagnostics)
+  // wire formats: scratch for host-bound outputs, graph-tuple offsets
+  unsigned char* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  int64_t* goff = nullptr;
 };
 
 namespace {
@@ -81,7 +85,8 @@ void cov_release(cov_handle* h) {
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
                   a.receivers, a.obs_step, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_prevT,
-                  h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow};
+                  h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
+                  h->goff};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -186,6 +191,39 @@ int ensure_time_matrix(cov_handle* h) {
   }
   h->tm_wide_envs += (int64_t)wide.size();
   for (int b : sel) h->tm_valid[b] = 1;
+  return GF_OK;
+}
+
+// Device scratch of at least `bytes` (grown on demand, reused across calls).
+int scratch(cov_handle* h, size_t bytes, unsigned char** out) {
+  if (bytes > h->scratch_bytes) {
+    if (h->scratch) CV_HIP(hipFree(h->scratch));
+    h->scratch = nullptr;
+    h->scratch_bytes = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&h->scratch), bytes) != hipSuccess)
+      return cfail(GF_ENOMEM, "hipMalloc of wire-format scratch failed");
+    h->scratch_bytes = bytes;
+  }
+  *out = h->scratch;
+  return GF_OK;
+}
+
+// Edge counts of the unpack_obs tuple and their exclusive offsets.
+void graph_sizes(const cov_handle* h, bool mask_all, std::vector<int32_t>& ne, std::vector<int64_t>& off) {
+  const int B = h->cfg.n_envs, R = h->cfg.n_robots, M = h->cfg.max_nodes;
+  ne.assign(B, 0);
+  off.assign(B + 1, 0);
+  for (int b = 0; b < B; ++b) {
+    ne[b] = (mask_all || b == 0) ? h->n_motion_host[b] + 8 * R : 4 * M;
+    off[b + 1] = off[b] + ne[b];
+  }
+}
+
+int put(cov_handle* h, void* dst, const void* src, size_t bytes, bool dev_dst, bool dev_src) {
+  if (!dst || !bytes) return GF_OK;
+  const hipMemcpyKind k = dev_dst ? (dev_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
+                                  : (dev_src ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
+  CV_HIP(hipMemcpyAsync(dst, src, bytes, k, h->stream));
   return GF_OK;
 }
 
@@ -456,6 +494,88 @@ int cov_get_time_matrix(cov_handle* h, int env, int32_t* cost, int32_t* prev) {
       if (prev) prev[i * T + j] = p[j * Tm + i];  // graph_previous[i, j] lives at prevT[j][i]
     }
   return GF_OK;
+}
+
+int cov_get_flat_obs(cov_handle* h, void* dst, int flags) {
+  if (!h || !dst) return cfail(GF_EINVAL, "null argument");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (int rc = use(h)) return rc;
+  const bool f32 = flags & COV_FLAT_F32;
+  const size_t bytes = (size_t)h->cfg.n_envs * (15 * (size_t)h->cfg.max_nodes + 1) * (f32 ? 4 : 8);
+  void* out = dst;
+  if (!(flags & COV_OUT_DEVICE)) {
+    unsigned char* sc = nullptr;
+    if (int rc = scratch(h, bytes, &sc)) return rc;
+    out = sc;
+  }
+  hipError_t e = gf::launch_cov_flat_obs(h->a, out, f32, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_flat_obs_kernel: ") + hipGetErrorString(e));
+  if (flags & COV_OUT_DEVICE) return GF_OK;  // stream-ordered; cov_sync before reading
+  CV_HIP(hipMemcpyAsync(dst, out, bytes, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return check_err(h);
+}
+
+int cov_graphs_tuple_sizes(cov_handle* h, int32_t* n_edge, int64_t* total_edges, int flags) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (!h->has_graph) return cfail(GF_ESTATE, "set the target graph first (cov_set_targets)");
+  std::vector<int32_t> ne;
+  std::vector<int64_t> off;
+  graph_sizes(h, flags & COV_MASK_ALL, ne, off);
+  if (n_edge) std::memcpy(n_edge, ne.data(), ne.size() * sizeof(int32_t));
+  if (total_edges) *total_edges = off.back();
+  return GF_OK;
+}
+
+int cov_get_graphs_tuple(cov_handle* h, int32_t* n_node, float* nodes, int32_t* n_edge, float* edges,
+                         int32_t* senders, int32_t* receivers, float* globs, int flags) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if ((edges != nullptr) != (senders != nullptr) || (edges != nullptr) != (receivers != nullptr))
+    return cfail(GF_EINVAL, "edges, senders and receivers go together (all or none)");
+  if (int rc = use(h)) return rc;
+  const bool dev = flags & COV_OUT_DEVICE;
+  const int B = h->cfg.n_envs, M = h->cfg.max_nodes;
+  std::vector<int32_t> ne;
+  std::vector<int64_t> off;
+  graph_sizes(h, flags & COV_MASK_ALL, ne, off);
+  const int64_t total = off.back();
+  if (!h->goff)
+    if (hipMalloc(reinterpret_cast<void**>(&h->goff), (B + 1) * sizeof(int64_t)) != hipSuccess)
+      return cfail(GF_ENOMEM, "hipMalloc of graph offsets failed");
+  CV_HIP(hipMemcpyAsync(h->goff, off.data(), (B + 1) * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+  if (edges) {
+    float* e_out = edges;
+    int32_t *s_out = senders, *r_out = receivers;
+    if (!dev) {
+      unsigned char* sc = nullptr;
+      if (int rc = scratch(h, (size_t)total * 12, &sc)) return rc;
+      e_out = reinterpret_cast<float*>(sc);
+      s_out = reinterpret_cast<int32_t*>(sc + (size_t)total * 4);
+      r_out = reinterpret_cast<int32_t*>(sc + (size_t)total * 8);
+    }
+    hipError_t e = gf::launch_cov_graphs(h->a, h->goff, flags & COV_MASK_ALL, e_out, s_out, r_out, h->stream);
+    if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_graphs_kernel: ") + hipGetErrorString(e));
+    if (!dev) {
+      if (int rc = put(h, edges, e_out, (size_t)total * 4, false, true)) return rc;
+      if (int rc = put(h, senders, s_out, (size_t)total * 4, false, true)) return rc;
+      if (int rc = put(h, receivers, r_out, (size_t)total * 4, false, true)) return rc;
+    }
+  }
+  if (int rc = put(h, nodes, h->a.nodes, (size_t)B * M * 3 * sizeof(float), dev, true)) return rc;
+  std::vector<int32_t> nn(B, M);
+  if (int rc = put(h, n_node, nn.data(), B * sizeof(int32_t), dev, false)) return rc;
+  if (int rc = put(h, n_edge, ne.data(), B * sizeof(int32_t), dev, false)) return rc;
+  std::vector<float> gl(B);
+  if (globs) {
+    std::vector<int64_t> st(B);
+    CV_HIP(hipMemcpyAsync(st.data(), h->a.obs_step, B * sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
+    CV_HIP(hipStreamSynchronize(h->stream));
+    for (int b = 0; b < B; ++b) gl[b] = static_cast<float>(st[b]);
+    if (int rc = put(h, globs, gl.data(), B * sizeof(float), dev, false)) return rc;
+  }
+  CV_HIP(hipStreamSynchronize(h->stream));  // host temporaries above
+  return check_err(h);
 }
 
 int cov_sync(cov_handle* h) {

@@ -80,6 +80,11 @@ hipError_t launch_cov_time_matrix(const CovTmArgs& a, int n_envs_sel, bool wide,
 hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s);
 
 size_t cov_step_lds_bytes(int R, int M);
+// Observation wire formats: the flat FlattenDictWrapper rows (B, 15M+1) and the
+// batched unpack_obs graph tuple (edges compacted at off[b]).
+hipError_t launch_cov_flat_obs(const CovArgs& a, void* dst, bool f32, hipStream_t s);
+hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all, float* edges, int32_t* snd,
+                             int32_t* rcv, hipStream_t s);
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s);
 hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_t* visited0, hipStream_t s);
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s);

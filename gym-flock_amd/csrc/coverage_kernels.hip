@@ -283,7 +283,84 @@ __global__ __launch_bounds__(kCovThreads) void cov_reset_kernel(CovArgs a, const
   }
 }
 
+// FlattenDictWrapper order (reference test.py:33, keys coverage.py:90): nodes (M,3),
+// edges (4M,1), senders (4M), receivers (4M), step (1,1), concatenated per env. The
+// wrapper's np.concatenate promotes to float64; every value here is exact in float32
+// too (the Box the wrapper declares), so both widths are offered.
+template <class V>
+__global__ __launch_bounds__(kCovThreads) void cov_flat_obs_kernel(CovArgs a, V* dst) {
+  const int b = blockIdx.y;
+  const size_t M = a.M, E = 4 * M, L = 15 * M + 1;
+  V* out = dst + (size_t)b * L;
+  const float* nodes = a.nodes + (size_t)b * 3 * M;
+  const float* edges = a.edges + (size_t)b * E;
+  const int32_t* snd = a.senders + (size_t)b * E;
+  const int32_t* rcv = a.receivers + (size_t)b * E;
+  for (size_t k = (size_t)blockIdx.x * kCovThreads + threadIdx.x; k < L; k += (size_t)gridDim.x * kCovThreads) {
+    V v;
+    if (k < 3 * M)
+      v = static_cast<V>(nodes[k]);
+    else if (k < 7 * M)
+      v = static_cast<V>(edges[k - 3 * M]);
+    else if (k < 11 * M)
+      v = static_cast<V>(snd[k - 7 * M]);
+    else if (k < 15 * M)
+      v = static_cast<V>(rcv[k - 11 * M]);
+    else
+      v = static_cast<V>(a.obs_step[b]);
+    out[k] = v;
+  }
+}
+
+// unpack_obs (coverage.py:689-741) on the batch: edges, senders and receivers of every
+// graph concatenated in env order, node indices offset by b*M, padded edges dropped.
+// The reference offsets the senders BEFORE testing them against -1, so only graph 0's
+// padding is dropped (a padded sender of graph b > 0 reads b*M - 1); mask_all drops
+// every graph's padding instead. Graph b's edges start at off[b].
+__global__ __launch_bounds__(kCovThreads) void cov_graphs_kernel(CovArgs a, const int64_t* off, int mask_all,
+                                                                 float* edges_out, int32_t* snd_out, int32_t* rcv_out) {
+  const int b = blockIdx.y;
+  const int M = a.M, E = 4 * M, tail0 = E - 8 * a.R;
+  const int nm = a.n_motion[b];
+  const bool keep_all = !mask_all && b > 0;
+  const float* edges = a.edges + (size_t)b * E;
+  const int32_t* snd = a.senders + (size_t)b * E;
+  const int32_t* rcv = a.receivers + (size_t)b * E;
+  const int64_t base = off[b];
+  const int32_t shift = b * M;
+  for (int k = blockIdx.x * kCovThreads + threadIdx.x; k < E; k += gridDim.x * kCovThreads) {
+    int64_t dst;
+    if (keep_all || k < nm)
+      dst = base + k;
+    else if (k >= tail0)
+      dst = base + nm + (k - tail0);
+    else
+      continue;  // padding (sender -1)
+    edges_out[dst] = edges[k];
+    snd_out[dst] = snd[k] + shift;
+    rcv_out[dst] = rcv[k] + shift;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_cov_flat_obs(const CovArgs& a, void* dst, bool f32, hipStream_t s) {
+  const size_t L = 15 * (size_t)a.M + 1;
+  const dim3 grid((unsigned)((L + 4 * kCovThreads - 1) / (4 * kCovThreads)), a.B);
+  if (f32)
+    hipLaunchKernelGGL(cov_flat_obs_kernel<float>, grid, dim3(kCovThreads), 0, s, a, static_cast<float*>(dst));
+  else
+    hipLaunchKernelGGL(cov_flat_obs_kernel<double>, grid, dim3(kCovThreads), 0, s, a, static_cast<double*>(dst));
+  return hipGetLastError();
+}
+
+hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all, float* edges, int32_t* snd,
+                             int32_t* rcv, hipStream_t s) {
+  const int E = 4 * a.M;
+  const dim3 grid((unsigned)((E + 4 * kCovThreads - 1) / (4 * kCovThreads)), a.B);
+  hipLaunchKernelGGL(cov_graphs_kernel, grid, dim3(kCovThreads), 0, s, a, off, mask_all ? 1 : 0, edges, snd, rcv);
+  return hipGetLastError();
+}
 
 size_t cov_step_lds_bytes(int R, int M) { return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16; }
 

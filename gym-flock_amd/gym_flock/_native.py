@@ -56,6 +56,9 @@ class CovConfig(ctypes.Structure):
 
 COV_ACTIONS_DEVICE = 0x1
 COV_ACTIONS_RESIDENT = 0x2
+COV_OUT_DEVICE = 0x4
+COV_FLAT_F32 = 0x8
+COV_MASK_ALL = 0x10
 
 
 class GymFlockError(RuntimeError):
@@ -112,6 +115,9 @@ SIGNATURES = {
     "cov_sync": [_P],
     "cov_controller_greedy": [_P, _P, _P, _P],
     "cov_get_time_matrix": [_P, _I, _P, _P],
+    "cov_get_flat_obs": [_P, _P, _I],
+    "cov_graphs_tuple_sizes": [_P, _P, _P, _I],
+    "cov_get_graphs_tuple": [_P, _P, _P, _P, _P, _P, _P, _P, _I],
     "fe_last_error": [],
     "fe_abi_version": [],
     "fe_diag": [_P, _I, _I, ctypes.POINTER(ctypes.c_double)],
@@ -450,6 +456,34 @@ class CoverageHandle:
         n = ctypes.c_int64()
         check(self.lib.cov_controller_greedy(self.h, ptr(a), ptr(rnd), ctypes.byref(n)))
         return a, rnd.astype(bool)
+
+    def flat_obs(self, f32=False, device_ptr=None):
+        """(B, 15*max_nodes + 1) rows in FlattenDictWrapper order (float64 like its
+        np.concatenate, or float32). device_ptr: write into that device buffer instead
+        (asynchronous on the handle's stream; returns None)."""
+        flags = COV_FLAT_F32 if f32 else 0
+        if device_ptr is not None:
+            check(self.lib.cov_get_flat_obs(self.h, ctypes.c_void_p(int(device_ptr)), flags | COV_OUT_DEVICE))
+            return None
+        out = np.empty((self.n_envs, 15 * self.max_nodes + 1), np.float32 if f32 else np.float64)
+        check(self.lib.cov_get_flat_obs(self.h, ptr(out), flags))
+        return out
+
+    def graphs_tuple(self, mask_all=False):
+        """unpack_obs (coverage.py:689-741) of the whole batch as host arrays; with
+        mask_all every graph drops its padded edges (the reference drops only graph 0's)."""
+        flags = COV_MASK_ALL if mask_all else 0
+        ne = np.empty(self.n_envs, np.int32)
+        tot = ctypes.c_int64()
+        check(self.lib.cov_graphs_tuple_sizes(self.h, ptr(ne), ctypes.byref(tot), flags))
+        T = int(tot.value)
+        o = dict(n_node=np.empty(self.n_envs, np.int32), nodes=np.empty((self.n_envs * self.max_nodes, 3), np.float32),
+                 n_edge=np.empty(self.n_envs, np.int32), edges=np.empty((T, 1), np.float32),
+                 senders=np.empty(T, np.int32), receivers=np.empty(T, np.int32),
+                 globs=np.empty((self.n_envs, 1), np.float32))
+        check(self.lib.cov_get_graphs_tuple(self.h, ptr(o["n_node"]), ptr(o["nodes"]), ptr(o["n_edge"]), ptr(o["edges"]),
+                                            ptr(o["senders"]), ptr(o["receivers"]), ptr(o["globs"]), flags))
+        return o
 
     def time_matrix(self, env, n_targets):
         """(graph_cost, graph_previous) of one env, each (T,T) int32."""

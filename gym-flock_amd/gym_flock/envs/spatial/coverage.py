@@ -221,6 +221,50 @@ class CoverageEnv(Env):
         c = self.graph_cost
         return np.max(c[c < MAX_COST])
 
+    @staticmethod
+    def get_number_nodes(ob_space, n_node_feat=None):
+        """coverage.py:675-680: node count of a flattened observation space."""
+        if n_node_feat is None:
+            n_node_feat = N_NODE_FEAT
+        return (ob_space.shape[0] - N_GLOB_FEAT) // (MAX_EDGES * (2 + N_EDGE_FEAT) + n_node_feat)
+
+    @staticmethod
+    def get_node_features(n_node_feat=None):
+        """coverage.py:682-687 (always N_NODE_FEAT)."""
+        return N_NODE_FEAT
+
+    @staticmethod
+    def unpack_obs(obs, ob_space, dim_nodes=None):
+        """coverage.py:689-741 without TensorFlow. obs is (B, L) flattened
+        observations; it returns NumPy arrays in the reference's order (batch_size,
+        n_node, nodes, n_edge, edges, senders, receivers, globs). Like the reference,
+        the senders are offset by each graph's first node before the padding test, so
+        only graph 0 drops its padded edges. For the device-side batch use
+        VecCoverage.graphs_tuple()."""
+        if dim_nodes is None:
+            dim_nodes = N_NODE_FEAT
+        obs = np.asarray(obs, dtype=np.float32)
+        n_nodes = (ob_space.shape[0] - N_GLOB_FEAT) // (MAX_EDGES * (2 + N_EDGE_FEAT) + dim_nodes)
+        max_n_edges = n_nodes * MAX_EDGES
+        shapes = ((n_nodes, dim_nodes), (max_n_edges, N_EDGE_FEAT), (max_n_edges, 1), (max_n_edges, 1),
+                  (1, N_GLOB_FEAT))
+        sizes = [int(np.prod(sh)) for sh in shapes]
+        parts = np.split(obs, np.cumsum(sizes)[:-1], axis=1)
+        nodes, edges, senders, receivers, globs = [p.reshape((-1,) + sh) for p, sh in zip(parts, shapes)]
+        batch_size = nodes.shape[0]
+        nodes = nodes.reshape(-1, dim_nodes)
+        n_node = np.full((batch_size,), n_nodes, dtype=np.int32)
+        cum = (np.cumsum(n_node) - n_node).astype(np.float32).reshape(-1, 1, 1)
+        senders = senders + cum
+        receivers = receivers + cum
+        mask = (senders != -1).reshape(batch_size, -1)
+        n_edge = mask.sum(axis=1).astype(np.int32)
+        mask = mask.reshape(-1)
+        edges = edges.reshape(-1, N_EDGE_FEAT)[mask]
+        senders = senders.reshape(-1)[mask].astype(np.int32)
+        receivers = receivers.reshape(-1)[mask].astype(np.int32)
+        return batch_size, n_node, nodes, n_edge, edges, senders, receivers, globs.reshape(batch_size, N_GLOB_FEAT)
+
     def render(self, mode='human'):
         pass
 

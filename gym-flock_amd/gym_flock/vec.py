@@ -167,6 +167,14 @@ class VecCoverage:
     def obs(self, env=0):
         return self.h.obs(env)
 
+    def flat_obs(self, f32=False, device_ptr=None):
+        """Every env's observation as one FlattenDictWrapper row (B, 15*max_nodes + 1)."""
+        return self.h.flat_obs(f32, device_ptr)
+
+    def graphs_tuple(self, mask_all=False):
+        """The batch as unpack_obs's graph tuple (coverage.py:689-741)."""
+        return self.h.graphs_tuple(mask_all)
+
     def sync(self):
         self.h.sync()
 

@@ -217,6 +217,26 @@ int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random
  * (T,T) row-major, T = that env's target count; builds the matrix if needed. */
 int cov_get_time_matrix(cov_handle* h, int env, int32_t* cost, int32_t* prev);
 
+/* Observation wire formats for graph trainers. */
+#define COV_OUT_DEVICE 0x4 /* output pointers are device memory (else host)             */
+#define COV_FLAT_F32   0x8 /* flat rows as float32 (the wrapper's Box dtype), else float64 */
+#define COV_MASK_ALL   0x10 /* graph tuple: drop every graph's padded edges, not only graph
+                               0's as the reference's unpack_obs does (see below)         */
+/* Every env's observation flattened like gym's FlattenDictWrapper over keys
+ * ['nodes','edges','senders','receivers','step'] (coverage.py:90, test.py:33):
+ * dst (B, 15*max_nodes + 1), float64 (np.concatenate's promotion) or float32. */
+int cov_get_flat_obs(cov_handle* h, void* dst, int flags);
+/* unpack_obs (coverage.py:689-741) of the batch without TensorFlow: n_edge[B] and the
+ * total edge count of the tuple cov_get_graphs_tuple writes. The reference masks edges
+ * after offsetting senders by the graph's first node, so only graph 0 drops its padding
+ * (COV_MASK_ALL drops all). */
+int cov_graphs_tuple_sizes(cov_handle* h, int32_t* n_edge, int64_t* total_edges, int flags);
+/* n_node[B] (= max_nodes), nodes (B*max_nodes, 3) f32, n_edge[B], edges (total, 1) f32,
+ * senders/receivers (total) i32 offset by b*max_nodes, globs (B, 1) f32 (step). Any
+ * pointer may be NULL; with COV_OUT_DEVICE all are device pointers. */
+int cov_get_graphs_tuple(cov_handle* h, int32_t* n_node, float* nodes, int32_t* n_edge, float* edges,
+                         int32_t* senders, int32_t* receivers, float* globs, int flags);
+
 /* Diagnostics ---------------------------------------------------------------- */
 const char* fe_last_error(void);
 int fe_abi_version(void);

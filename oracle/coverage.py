@@ -222,3 +222,46 @@ def greedy_actions(cost, prev, cur, visited_targets, recv, n_robots):
         step = prev[goal[i], c[i]] + R
         acts[i] = int(np.nonzero(recv[i] == step)[0][0])
     return acts, rand
+
+
+KEYS = ['nodes', 'edges', 'senders', 'receivers', 'step']  # coverage.py:90
+N_GLOB_FEAT = 1   # coverage.py:59
+MAX_EDGES = 4     # coverage.py:56
+
+
+def flatten_obs(obs):
+    """gym's FlattenDictWrapper.observation (used by the reference's test.py:33; gym
+    itself is not vendored or installed, so this restates its published rule): ravel
+    each value in key order and np.concatenate. The promotion of float32 nodes/edges,
+    int32 senders/receivers and the int64 step gives float64."""
+    return np.concatenate([np.asarray(obs[k]).ravel() for k in KEYS])
+
+
+def unpack_obs(flat, dim_nodes=3):
+    """unpack_obs, coverage.py:689-741, restated in NumPy (the reference needs
+    TensorFlow, which is absent: parity unpinned beyond this restatement). flat is
+    (B, L) float32, as the wrapper's Box declares. The senders are offset by the
+    graph's first node BEFORE the padding test (:718-723), so only graph 0 loses its
+    padded edges. Returns the graph tuple fields."""
+    flat = np.asarray(flat, dtype=np.float32)
+    B, L = flat.shape
+    n_nodes = (L - N_GLOB_FEAT) // (MAX_EDGES * (2 + 1) + dim_nodes)
+    max_n_edges = n_nodes * MAX_EDGES
+    shapes = ((n_nodes, dim_nodes), (max_n_edges, 1), (max_n_edges, 1), (max_n_edges, 1), (1, N_GLOB_FEAT))
+    sizes = [int(np.prod(s)) for s in shapes]
+    parts = np.split(flat, np.cumsum(sizes)[:-1], axis=1)
+    nodes, edges, senders, receivers, globs = [p.reshape((-1,) + s) for p, s in zip(parts, shapes)]
+    nodes = nodes.reshape(-1, dim_nodes)
+    n_node = np.full((B,), n_nodes)
+    cum = (np.cumsum(n_node) - n_node).astype(np.float32).reshape(-1, 1, 1)
+    senders = senders + cum
+    receivers = receivers + cum
+    mask = (senders != -1).reshape(B, -1)
+    n_edge = mask.sum(axis=1)
+    mask = mask.reshape(-1)
+    edges = edges.reshape(-1, 1)[mask]
+    senders = senders.reshape(-1)[mask]
+    receivers = receivers.reshape(-1)[mask]
+    return dict(n_node=n_node.astype(np.int32), nodes=nodes, n_edge=n_edge.astype(np.int32), edges=edges,
+                senders=senders.astype(np.int32), receivers=receivers.astype(np.int32),
+                globs=globs.reshape(B, N_GLOB_FEAT))

@@ -79,3 +79,21 @@ def test_greedy_expert_matches_reference(path):
         env.step(a)
     if "r20" in path:
         assert n_random > 0  # the long episode exercises the random fallback
+
+
+def test_flatten_and_unpack_round_trip():
+    """FlattenDictWrapper rows (test.py:33) of a recorded reference observation and the
+    unpack_obs restatement (coverage.py:689-741) recover it. The reference offsets the
+    senders before its padding test, so only graph 0 drops padding."""
+    f = np.load(os.path.join(GOLDEN, "coverage_r6_random.npz"))
+    M = int(f["max_nodes"])
+    obs = {k: f[k + "0"] for k in oc.KEYS}
+    flat = oc.flatten_obs(obs)
+    assert flat.dtype == np.float64 and flat.shape == (15 * M + 1,)
+    u = oc.unpack_obs(np.stack([flat, flat]))
+    np.testing.assert_array_equal(u["nodes"][:M], obs["nodes"])
+    valid = obs["senders"] != -1
+    assert u["n_edge"][0] == valid.sum() and u["n_edge"][1] == 4 * M
+    np.testing.assert_array_equal(u["senders"][:valid.sum()], obs["senders"][valid])
+    np.testing.assert_array_equal(u["senders"][valid.sum():], obs["senders"] + M)
+    assert u["globs"][0, 0] == obs["step"][0, 0]
