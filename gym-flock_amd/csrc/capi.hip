@@ -285,6 +285,7 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       h->T = t < full ? t : full;
     }
   }
+
   h->bpe = (cfg->n_agents + h->R - 1) / h->R;
   if ((size_t)h->bpe * B > 0x7fffffff) {
     delete h;

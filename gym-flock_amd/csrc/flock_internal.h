@@ -10,6 +10,7 @@ constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float6
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
 constexpr int kResidentRows = 32;   // rows per block of the env-resident kernel
 constexpr int kResidentMax = 1024;  // largest N whose env fits the resident kernel's LDS
+constexpr size_t kStepLdsFloor = 32 * 1024;  // plain step: 5 workgroups per CU (tuning)
 
 // One batched hot-path launch. Pointers are device pointers; all per-env arrays
 // are [B][N][...] contiguous.
@@ -33,7 +34,8 @@ struct StepArgs {
   int lds_pad;            // extra dynamic LDS bytes (occupancy control; tuning knob)
   int diag;               // ablation switches (0 in production): 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
-                          // unwritten: timing only), 16 skip tile loads (timing only)
+                          // unwritten: timing only), 16 skip tile loads (timing only),
+                          // 32 plain blockIdx workgroup order (A/B; default groups an env on one XCD)
   // Flocking variants (flocking_leader/obstacle/stoch.py). variant == 0 keeps the
   // FlockingRelative path untouched; otherwise the fields below apply (tiled kernel).
   int variant;

@@ -243,7 +243,37 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
 
   const int i_row = i0 + fr;  // global row of this thread's feature slice
-  // pass 2: features / gradients for the set bits of one tile, ascending j per slice
+  // one neighbour pair (row fr, tile column c): features and controller gradient
+  auto pair_terms = [&](int j0, int c, bool isadj, bool isnear) {
+    const St o = tile[c];
+    const double dx = me.px - o.px, dy = me.py - o.py;
+    const double r2 = dx * dx + dy * dy;
+    // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
+    // reference's two divisions; far inside the float32 outputs' tolerance)
+    const double ir = 1.0 / r2, irr = ir * ir;
+    const double q1x = dx * irr, q2x = dx * ir;
+    const double q1y = dy * irr, q2y = dy * ir;
+    if (isadj) {
+      // obstacle variant: no velocity difference for pairs touching agents < nvz
+      const bool vz = VAR && (i_row < a.n_vel_zero || j0 + c < a.n_vel_zero);
+      f0 += vz ? 0.0 : me.vx - o.vx;
+      f1 += q1x;
+      f2 += q2x;
+      f3 += vz ? 0.0 : me.vy - o.vy;
+      f4 += q1y;
+      f5 += q2y;
+    }
+    if constexpr (CTRL) {
+      if (isnear && (a.centralized || isadj)) {
+        gx += (-2.0 * q1x) + (2.0 * q2x);
+        gy += (-2.0 * q1y) + (2.0 * q2y);
+      }
+    }
+  };
+
+  // pass 2: features / gradients for the set bits of one tile, ascending j per slice.
+  // (Dealing a row's bits round robin over its S threads balances the slices but its
+  // cursor bookkeeping cost more than it saved: 266 vs 215 us, DESIGN.md.)
   auto feature_pass = [&](int j0, int nch) {
     if (!frow || (a.diag & 2)) return;
     const int wpt = (nch + S - 1) / S;
@@ -255,30 +285,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       while (m) {
         const int k = __builtin_ctzll(m);
         m &= m - 1;
-        const St o = tile[(w << 6) + k];
-        const double dx = me.px - o.px, dy = me.py - o.py;
-        const double r2 = dx * dx + dy * dy;
-        const double rr = r2 * r2;
-        const double q1x = dx / rr, q2x = dx / r2;
-        const double q1y = dy / rr, q2y = dy / r2;
-        const bool isadj = (am >> k) & 1ull;
-        if (isadj) {
-          // obstacle variant: no velocity difference for pairs touching agents < nvz
-          const bool vz = VAR && (i_row < a.n_vel_zero || j0 + (w << 6) + k < a.n_vel_zero);
-          f0 += vz ? 0.0 : me.vx - o.vx;
-          f1 += q1x;
-          f2 += q2x;
-          f3 += vz ? 0.0 : me.vy - o.vy;
-          f4 += q1y;
-          f5 += q2y;
-        }
-        if constexpr (CTRL) {
-          const bool isnear = (nm >> k) & 1ull;
-          if (isnear && (a.centralized || isadj)) {
-            gx += (-2.0 * q1x) + (2.0 * q2x);
-            gy += (-2.0 * q1y) + (2.0 * q2y);
-          }
-        }
+        pair_terms(j0, (w << 6) + k, (am >> k) & 1ull, CTRL && ((nm >> k) & 1ull));
       }
     }
   };
@@ -981,7 +988,11 @@ static hipError_t launch_step_resident_t(const StepArgs& a, hipStream_t s) {
 
 template <bool DYN, bool UF64, bool CTRL, bool VAR>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
-  const size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
+  // the step without the controller runs best at 5 workgroups per CU (6 fit by
+  // registers: 218 vs 215 us at config 2); the controller's heavier feature pass wants
+  // every workgroup it can get, so only the plain step is held to 32 KiB of LDS
+  if (!CTRL && a.lds_pad == 0 && lds < kStepLdsFloor) lds = kStepLdsFloor;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR>),

@@ -29,13 +29,18 @@ variants = {} if os.environ.get("QUICK") else {
     "no_network": (0, nat.FE_NO_NETWORK),
     "compute_only_no_feat": (2, nat.FE_NO_NETWORK),
     "ctrl_fused": (0, nat.FE_WITH_CONTROLLER),
+    "plain_order": (32, 0),
+    "ctrl_no_feature_pass": (2, nat.FE_WITH_CONTROLLER),
+    "ctrl_no_network": (0, nat.FE_WITH_CONTROLLER | nat.FE_NO_NETWORK),
 }
 if os.environ.get("QUICK"):
     variants = {"full": (0, 0), "nt_stores": (4, 0), "ctrl_fused": (0, nat.FE_WITH_CONTROLLER)}
 res = {k: [] for k in list(variants) + ["fill", "fill_nt"]}
+x0 = synthetic_batch(B, N)
 for r in range(ROUNDS):
     for name, (diag, flags) in variants.items():
         h.diag_switches(diag)
+        h.set_state(x0)  # same workload every time (the swarm spreads as it steps)
         h.step(None, nat.FE_U_RESIDENT | flags)
         h.timing_start()
         for _ in range(STEPS):
