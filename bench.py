@@ -28,6 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "gym-flock_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+# (N, envs per GPU, GPUs) -> which BASELINE.json config the run is
+CONFIG_TAG = {(1024, 256, 1): " (BASELINE.json configs[1])", (1024, 256, 8): " (BASELINE.json configs[2])",
+              (8192, 32, 1): " (BASELINE.json configs[4])"}
 
 
 def log(*a):
@@ -61,6 +64,38 @@ def cpu_baseline(n_agents, seconds):
             "sample": "oracle/flocking.py step() (NumPy, float64, 1 thread) on 1 env of N=%d for "
                       "%d steps (%.1f s); same synthetic init and float32 actions as the GPU run"
                       % (n_agents, steps, el)}
+
+
+def cpu_worker(n_agents, seconds, seed):
+    """--cpu-worker: one process of the all-cores baseline (no GPU is touched)."""
+    from oracle import flocking as orc
+    from gym_flock.init_states import synthetic_state
+
+    x = synthetic_state(n_agents, seed)
+    u = np.random.RandomState(1234 + seed).uniform(-1, 1, size=(n_agents, 2)).astype(np.float32)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        x = orc.step(x, u)["x"]
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and steps >= 3:
+            break
+    print(json.dumps({"agent_steps_per_s": n_agents * steps / el, "steps": steps, "seconds": el}), flush=True)
+
+
+def cpu_baseline_all_cores(n_agents, seconds, procs):
+    """`procs` independent single-threaded oracle processes at once
+    (child processes, OMP_NUM_THREADS=1), aggregate agent-steps/s."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(seconds), "--n-agents", str(n_agents)]
+    ps = [subprocess.Popen(cmd + ["--seed", str(k)], stdout=subprocess.PIPE, env=env) for k in range(procs)]
+    rates = []
+    for p in ps:
+        out, _ = p.communicate(timeout=seconds * 10 + 120)
+        if p.returncode == 0:
+            rates.append(json.loads(out.decode().strip().splitlines()[-1])["agent_steps_per_s"])
+    return sum(rates), len(rates)
 
 
 def load_traffic(n_agents, n_envs):
@@ -185,10 +220,17 @@ def main():
                     help="steps per reward all-gather (N>1); each collective carries all those steps")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="processes of the all-cores CPU baseline (default: OMP_NUM_THREADS or 16, "
+                         "the box's CPU share; 0 after the flag = single core only)")
+    ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-controller-line", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-rank path (gloo rendezvous + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
+    if args.cpu_worker is not None:
+        return cpu_worker(args.n_agents, args.cpu_worker, args.seed)
     if args.workload == "coverage":
         return bench_coverage(args)
 
@@ -280,7 +322,7 @@ def main():
         achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         traffic = load_traffic(N, B)
         line = {
-            "metric": "agent-steps/sec (N_agents×N_envs×steps/s), FlockingRelative N=1024",
+            "metric": "agent-steps/sec (N_agents×N_envs×steps/s), FlockingRelative N=%d" % N,
             "value": value,
             "unit": "agent-steps/s",
             "n_gpus": world,
@@ -292,8 +334,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (random-init swarms, SURVEY.md §8d; float32 actions U(-1,1) resident in HBM)",
-            "config": {"workload": "FlockingRelative-v0 step(), N=%d agents x %d envs per GPU "
-                                   "(BASELINE.json configs[1])" % (N, B),
+            "config": {"workload": "FlockingRelative-v0 step(), N=%d agents x %d envs per GPU%s"
+                                   % (N, B, CONFIG_TAG.get((N, B, world), "")),
                        "n_agents": N, "envs_per_gpu": B, "global_envs": world * B,
                        "outputs": "network (N,N) f32 + state_values (N,6) f32 + reward, in HBM",
                        "parallelism": "env-sharded dp%d, RCCL reward all-gather" % world},
@@ -305,7 +347,15 @@ def main():
         line.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline (oracle, 1 core, ~%.0fs)..." % args.cpu_seconds)
-            line["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds)
+            one = cpu_baseline(N, args.cpu_seconds)
+            procs = args.cpu_procs or min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
+            if procs > 1:
+                log("cpu baseline, all cores: %d processes x ~%.0fs..." % (procs, args.cpu_seconds / 2))
+                agg, ok = cpu_baseline_all_cores(N, args.cpu_seconds / 2, procs)
+                one = dict(one, per_core=one["value"], value=agg, cores=ok,
+                           sample=one["sample"] + "; value = %d such processes at once (OMP_NUM_THREADS=1 "
+                                                  "each, %.0f s), summed" % (ok, args.cpu_seconds / 2))
+            line["cpu_baseline"] = one
         print(json.dumps(line), flush=True)
     env.close()
     if dist is not None:

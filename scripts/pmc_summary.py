@@ -25,7 +25,8 @@ def main():
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
-    key = [k for k in f if "flock_step_kernel<true, false, false>" in k][0]
+    # the plain step: <DYN=true, UF64=false, CTRL=false[, VAR=false]>
+    key = [k for k in f if "flock_step_kernel<true, false, false" in k][0]
     fetch_kib = sum(f[key]) / len(f[key])
     write_kib = sum(w[key]) / len(w[key])
     total = (2 * fetch_kib + write_kib) * 1024
