@@ -121,6 +121,7 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   unsigned* claim = reinterpret_cast<unsigned*>(chosen + R);  // (M+31)/32 claim bits
   unsigned* seen = claim + (M + 31) / 32;                      // visited-this-step bits
   int* counter = reinterpret_cast<int*>(seen + (M + 31) / 32);
+  int* first = counter + 4;                                    // M: first claimer of each node
   const int W = (M + 31) / 32;
   const int tid = threadIdx.x;
   const double* tg = a.tgt + (size_t)b * Tm * 2;
@@ -170,27 +171,32 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       chosen[i] = n;
       if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
     }
-    __syncthreads();
     // then, in robot order, a move succeeds unless its node is already claimed; a
-    // blocked robot stays and its node joins the claims (serial in the reference too)
-    if (tid == 0) {
-      for (int i = 0; i < R; ++i) {
+    // blocked robot stays and its node joins the claims. The reference walks the robots
+    // serially; here every robot's outcome is re-evaluated in parallel from the current
+    // guesses (the first claimer of each node by atomicMin) until nothing changes. A
+    // robot's outcome depends only on lower-indexed robots, so after k rounds robots
+    // 0..k-1 are final, and the fixed point is the serial walk's unique result.
+    for (int i = tid; i < R; i += kCovThreads) new_s[i] = chosen[i];  // guess: every move succeeds
+    while (true) {
+      for (int k = tid; k < M; k += kCovThreads) first[k] = INT_MAX;
+      __syncthreads();
+      for (int i = tid; i < R; i += kCovThreads)
+        if (chosen[i] != cur_s[i]) atomicMin(&first[new_s[i]], i);  // a mover claims where it ends
+      __syncthreads();
+      int changed = 0;
+      for (int i = tid; i < R; i += kCovThreads) {
         const int c = cur_s[i], n = chosen[i];
-        if (n == c) {
-          new_s[i] = c;
-          continue;
-        }
-        const unsigned bit = 1u << (n & 31);
-        if (!(claim[n >> 5] & bit)) {
-          claim[n >> 5] |= bit;
-          new_s[i] = n;
-        } else {
-          claim[c >> 5] |= 1u << (c & 31);
-          new_s[i] = c;
+        if (n == c) continue;
+        const bool ok = !(claim[n >> 5] & (1u << (n & 31))) && first[n] >= i;
+        const int v = ok ? n : c;
+        if (v != new_s[i]) {
+          new_s[i] = v;
+          changed = 1;
         }
       }
+      if (!__syncthreads_or(changed)) break;
     }
-    __syncthreads();
   } else {
     for (int i = tid; i < R; i += kCovThreads) new_s[i] = cur_s[i];
     __syncthreads();
@@ -362,7 +368,9 @@ hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all
   return hipGetLastError();
 }
 
-size_t cov_step_lds_bytes(int R, int M) { return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16; }
+size_t cov_step_lds_bytes(int R, int M) {
+  return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16 + (size_t)M * 4;
+}
 
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {
   hipLaunchKernelGGL(cov_graph_kernel, dim3(n), dim3(kCovThreads), 0, s, a, envs, n);
