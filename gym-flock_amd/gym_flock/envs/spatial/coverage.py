@@ -170,6 +170,19 @@ class CoverageEnv(Env):
         self.episode_reward += reward
         return obs, reward, done, {}
 
+    def get_action_edges(self):
+        """coverage.py:206-232: each robot's 4 action targets (its node's out-neighbours in
+        ascending order, padded with its own node) as ((senders, receivers), dists, diff),
+        read from the device observation's action-edge tail."""
+        o = self._h.obs(0)
+        R = self.n_robots
+        base = self.max_edges - 4 * R
+        senders = o["senders"][base:].astype(np.int64)
+        receivers = o["receivers"][base:].astype(np.int64)
+        x = self.x
+        diff = x[senders, :] - x[receivers, :]
+        return (senders, receivers), np.linalg.norm(diff, axis=1), diff
+
     @property
     def closest_targets(self):
         """coverage.py:427-432 (global node indices)."""
@@ -264,6 +277,17 @@ class CoverageEnv(Env):
         senders = senders.reshape(-1)[mask].astype(np.int32)
         receivers = receivers.reshape(-1)[mask].astype(np.int32)
         return batch_size, n_node, nodes, n_edge, edges, senders, receivers, globs.reshape(batch_size, N_GLOB_FEAT)
+
+    @staticmethod
+    def unpack_obs_state(obs, ob_space, state, dim_state, dim_nodes=None):
+        """coverage.py:744-798 without TensorFlow: unpack_obs plus the node features
+        extended by each half of a (B*n_nodes, 2*dim_state) state, giving nodes1 and nodes2."""
+        batch_size, n_node, nodes, n_edge, edges, senders, receivers, globs = CoverageEnv.unpack_obs(
+            obs, ob_space, dim_nodes)
+        st = np.asarray(state, dtype=np.float32).reshape(-1, dim_state * 2)
+        nodes1 = np.concatenate([nodes, st[:, :dim_state]], axis=1)
+        nodes2 = np.concatenate([nodes, st[:, dim_state:]], axis=1)
+        return batch_size, n_node, nodes1, nodes2, n_edge, edges, senders, receivers, globs
 
     def render(self, mode='human'):
         pass

@@ -145,3 +145,35 @@ def test_env_api_reproduces_reference_reset_and_episode():
     with pytest.raises(IndexError):
         env.step(np.full((6, 1), 4))
     env.close()
+
+
+def test_env_get_action_edges_and_unpack_state():
+    """get_action_edges (coverage.py:206-232) from the device observation, and the
+    NumPy unpack_obs_state (:744-798) on a flattened observation."""
+    from gym_flock.envs.spatial import CoverageEnv
+    f = np.load(os.path.join(GOLDEN, "coverage_r6_random.npz"))
+    np.random.seed(3)
+    env = CoverageEnv(n_robots=6, nearby_starts=False, max_nodes=500)
+    env.seed(4)
+    np.random.seed(3)
+    env.reset()
+    env.step(f["actions"][0].reshape(-1, 1))
+    (snd, rcv), dists, diff = env.get_action_edges()
+    R = 6
+    o = oc.CoverageOracle(f["targets"], R, 500)
+    cur = f["closest"][0]
+    np.testing.assert_array_equal(snd, np.repeat(np.arange(R), 4))
+    np.testing.assert_array_equal(rcv, oc.action_receivers(cur, o.nbr, o.cnt, R).reshape(-1))
+    x = np.vstack([f["xr"][0], f["targets"]])
+    np.testing.assert_array_equal(diff, x[snd] - x[rcv])
+    np.testing.assert_array_equal(dists, np.linalg.norm(x[snd] - x[rcv], axis=1))
+    flat = oc.flatten_obs(env._h.obs(0))[None].astype(np.float32)
+
+    class Space:
+        shape = flat.shape[1:]
+    state = np.arange(500 * 4, dtype=np.float32).reshape(500, 4)
+    out = CoverageEnv.unpack_obs_state(flat, Space(), state, 2)
+    assert out[2].shape == (500, 5) and out[3].shape == (500, 5)
+    np.testing.assert_array_equal(out[2][:, 3:], state[:, :2])
+    np.testing.assert_array_equal(out[3][:, 3:], state[:, 2:])
+    env.close()
