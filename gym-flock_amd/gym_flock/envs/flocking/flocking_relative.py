@@ -169,6 +169,20 @@ class FlockingRelativeEnv(Env):
             centralized = self.centralized
         return self._handle().controller(centralized)[0]
 
+    def potential_grad(self, pos_diff, r2):
+        """:214-226 on caller-supplied arrays (the step's own gradient runs fused in the
+        device controller): -2 d / r2^2 + 2 d / r2, zero where r2 > comm_radius."""
+        grad = -2.0 * np.divide(pos_diff, np.multiply(r2, r2)) + 2 * np.divide(pos_diff, r2)
+        grad[r2 > self.comm_radius] = 0
+        return grad
+
+    def potential(self, r2):
+        """:228-232 on a caller-supplied (N,N) r2: Turner potential summed over pairs."""
+        p = np.reciprocal(r2) + np.log(r2)
+        p[r2 > self.comm_radius2] = self.vr
+        np.fill_diagonal(p, 0)
+        return np.sum(np.sum(p))
+
     # ------------------------------------------------------------------- reset
     def _accept(self, x):
         """:177-184 on the device: min degree >= 2 and min pairwise distance >= 0.1."""
