@@ -226,6 +226,7 @@ def main():
     ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-controller-line", action="store_true")
+    ap.add_argument("--no-packed-line", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-rank path (gloo rendezvous + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
@@ -315,6 +316,34 @@ def main():
             ec = float(t.item())
         extra["step_with_controller"] = {"value": world * B * N * K / ec, "unit": "agent-steps/s",
                                          "ms_per_step": 1e3 * ec / K}
+
+    # packed output mode: adjacency bits + degree instead of the dense rows
+    if not args.no_packed_line:
+        env.reset(seed=0)
+        env.step(resident=True, network="packed")
+        barrier()
+        env.h.timing_start()
+        t4 = time.perf_counter()
+        for _ in range(K):
+            env.step(resident=True, network="packed")
+        env.sync()
+        t5 = time.perf_counter()
+        pk_ms, _ = env.h.timing_stop()
+        barrier()
+        ep = t5 - t4
+        if dist is not None:
+            import torch
+            t = torch.tensor([ep], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ep = float(t.item())
+        wn = (N + 63) // 64
+        pk_bytes = B * (8 * N * wn + 4 * N + 96 * N + 8)
+        extra["packed_network"] = {
+            "value": world * B * N * K / ep, "unit": "agent-steps/s", "ms_per_step": 1e3 * ep / K,
+            "kernel_ms": pk_ms, "algorithmic_bytes_per_launch": pk_bytes,
+            "achieved_GBs": pk_bytes / (pk_ms * 1e-3) / 1e9 if pk_ms > 0 else None,
+            "note": "adjacency as bits (N*ceil(N/64)*8 B) + int32 degree per env instead of the dense "
+                    "float32 network; the pair work, not HBM, bounds this mode"}
 
     if rank == 0:
         value = world * B * N * K / elapsed

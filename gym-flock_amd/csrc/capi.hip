@@ -87,6 +87,10 @@ struct fe_handle {
   fe_variant var{};
   double* dt_env = nullptr;             // (B) per-env dt
   bool dt_per_env = false;
+  // packed output mode (FE_PACKED_NETWORK)
+  uint64_t* adj_bits = nullptr;         // (B,N,Wn)
+  int32_t* pdeg = nullptr;              // (B,N)
+  bool has_packed = false;
 };
 
 namespace {
@@ -114,7 +118,8 @@ void release(fe_handle* h) {
   if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env};
+                  h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
+                  h->adj_bits, h->pdeg};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -143,6 +148,20 @@ int next_reward_slot(fe_handle* h) {
     GF_HIP(hipStreamWaitEvent(h->stream, h->ag_ev[blk], 0));
     h->ag_pending[blk] = false;
   }
+  return GF_OK;
+}
+
+// Packed-output buffers on first use (FE_PACKED_NETWORK).
+int packed_outputs(fe_handle* h, int flags, gf::StepArgs& a) {
+  if (!(flags & FE_PACKED_NETWORK)) return GF_OK;
+  const size_t Wn = (h->cfg.n_agents + 63) / 64;
+  if (!h->adj_bits) {
+    if (int rc = dalloc(&h->adj_bits, h->BN * Wn)) return rc;
+    if (int rc = dalloc(&h->pdeg, h->BN)) return rc;
+  }
+  a.adj_bits = h->adj_bits;
+  a.degree_out = h->pdeg;
+  h->has_packed = true;
   return GF_OK;
 }
 
@@ -380,6 +399,7 @@ int fe_compute_helpers(fe_handle* h, int flags) {
   a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
+  if (int rc = packed_outputs(h, flags, a)) return rc;
   if (int rc = timed_launch(h, a, false, false, ctrl)) return rc;
   if (ctrl) {
     h->ccur ^= 1;
@@ -425,6 +445,7 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
+  if (int rc = packed_outputs(h, flags, a)) return rc;
   if (int rc = timed_launch(h, a, true, uf64, ctrl)) return rc;
   h->cur ^= 1;
   if (ctrl) h->ccur ^= 1;
@@ -546,6 +567,23 @@ int fe_get_network_rows(fe_handle* h, int env, int row0, int nrows, float* dst) 
   return d2h(h, dst, h->net + (env * N + row0) * N, (size_t)nrows * N * 4);
 }
 
+int fe_get_network_packed(fe_handle* h, int env, uint64_t* bits, int32_t* degree) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_packed) return fail(GF_ESTATE, "no FE_PACKED_NETWORK step yet");
+  if (int rc = use_dev(h)) return rc;
+  const size_t N = h->cfg.n_agents, Wn = (N + 63) / 64;
+  if (bits) {
+    const size_t n = N * Wn;
+    if (int rc = env < 0 ? d2h(h, bits, h->adj_bits, h->BN * Wn * 8) : d2h(h, bits, h->adj_bits + env * n, n * 8))
+      return rc;
+  }
+  if (degree) {
+    if (int rc = env < 0 ? d2h(h, degree, h->pdeg, h->BN * 4) : d2h(h, degree, h->pdeg + env * N, N * 4)) return rc;
+  }
+  return GF_OK;
+}
+
 int fe_get_controls(fe_handle* h, int env, double* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
   if (int rc = check_env(h, env)) return rc;
@@ -591,6 +629,8 @@ int fe_device_buffers(fe_handle* h, fe_buffers* out) {
   out->knn_idx = h->knn_idx;
   out->knn_obs = h->knn_obs;
   out->stream = h->stream;
+  out->adj_bits = h->adj_bits;
+  out->degree = h->pdeg;
   return GF_OK;
 }
 

@@ -47,6 +47,8 @@ struct StepArgs {
   double ctrl_clip;       // controller output clip; <= 0: none
   float us_f, uc_f;       // float32 copies of u_scale, u_clip
   const double* dt_env;   // (B) per-env dt of this step, or nullptr (dt)
+  uint64_t* adj_bits;     // (B,N,Wn) packed adjacency or nullptr
+  int32_t* degree_out;    // (B,N) degrees or nullptr (with adj_bits)
 };
 
 struct KnnArgs {

@@ -421,8 +421,15 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
     }
     for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
-    if (frow && fs == 0)
+    if (frow && fs == 0) {
       inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
+      if (a.degree_out) a.degree_out[env0 + i0 + fr] = deg;
+    }
+  }
+  // packed output: the block's R x Wn adjacency words are one contiguous range
+  if (a.adj_bits) {
+    uint64_t* dst = a.adj_bits + (env0 + i0) * (size_t)Wn;
+    for (int k = tid; k < nrows * Wn; k += kThreads) dst[k] = adj[k];
   }
   __syncthreads();
 
@@ -1008,7 +1015,7 @@ static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if (a.variant) return launch_step_tiled<DYN, UF64, CTRL, true>(a, s);
-  if (a.resident) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
+  if (a.resident && !a.adj_bits) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
   return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
 }
 

@@ -24,6 +24,7 @@ FE_WITH_KNN = 0x10
 FE_NO_NETWORK = 0x20
 FE_NO_STATE_VALUES = 0x40
 FE_U_RESIDENT = 0x80
+FE_PACKED_NETWORK = 0x100
 
 
 class FeConfig(ctypes.Structure):
@@ -38,7 +39,8 @@ class FeBuffers(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("state_values", ctypes.c_void_p),
                 ("network", ctypes.c_void_p), ("controls", ctypes.c_void_p),
                 ("rewards", ctypes.c_void_p), ("knn_idx", ctypes.c_void_p),
-                ("knn_obs", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+                ("knn_obs", ctypes.c_void_p), ("stream", ctypes.c_void_p),
+                ("adj_bits", ctypes.c_void_p), ("degree", ctypes.c_void_p)]
 
 
 class FeVariant(ctypes.Structure):
@@ -87,6 +89,7 @@ SIGNATURES = {
     "fe_get_state_values": [_P, _I, _P],
     "fe_get_network": [_P, _I, _P],
     "fe_get_network_rows": [_P, _I, _I, _I, _P],
+    "fe_get_network_packed": [_P, _I, _P, _P],
     "fe_get_controls": [_P, _I, _P],
     "fe_get_rewards": [_P, _P],
     "fe_get_knn": [_P, _I, _P, _P],
@@ -289,6 +292,16 @@ class FlockHandle:
         out = np.empty((nrows, self.n_agents), np.float32)
         check(self.lib.fe_get_network_rows(self.h, int(env), int(row0), int(nrows), ptr(out)))
         return out
+
+    def network_packed(self, env=None):
+        """(bits uint64 [(B,)N,ceil(N/64)], degree int32 [(B,)N]) of the last
+        FE_PACKED_NETWORK step; adj(i,j) = bits[i, j//64] >> (j%64) & 1."""
+        wn = (self.n_agents + 63) // 64
+        lead = (self.n_envs,) if env is None else ()
+        bits = np.empty(lead + (self.n_agents, wn), np.uint64)
+        deg = np.empty(lead + (self.n_agents,), np.int32)
+        check(self.lib.fe_get_network_packed(self.h, -1 if env is None else int(env), ptr(bits), ptr(deg)))
+        return bits, deg
 
     def controls(self, env=None):
         shape = (self.n_envs, self.n_agents, 2) if env is None else (self.n_agents, 2)

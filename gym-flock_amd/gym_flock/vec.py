@@ -62,6 +62,8 @@ class VecFlockingRelative:
              resident=False, device_ptr=None, dt=None):
         """Advance every env one step.
 
+        network: True (dense (N,N) rows), False (none), "packed" (adjacency bits +
+        degree only) or "both".
         u: (B,N,2) host actions (float32 or float64 arithmetic like the reference); or
         expert=True to feed back the previous controller() output (closed loop); or
         resident=True to reuse the actions last given to set_actions(); or
@@ -76,7 +78,11 @@ class VecFlockingRelative:
             flags |= nat.FE_WITH_CONTROLLER
         if knn:
             flags |= nat.FE_WITH_KNN
-        if not network:
+        if network == "packed":  # adjacency bits + degree instead of the dense (N,N) rows
+            flags |= nat.FE_PACKED_NETWORK | nat.FE_NO_NETWORK
+        elif network == "both":
+            flags |= nat.FE_PACKED_NETWORK
+        elif not network:
             flags |= nat.FE_NO_NETWORK
         if expert:
             self.h.step(None, flags | nat.FE_U_EXPERT)
@@ -102,6 +108,10 @@ class VecFlockingRelative:
 
     def rewards(self):
         return self.h.rewards()
+
+    def network_packed(self, env=None):
+        """Adjacency bits and degrees of the last step(network="packed" or "both")."""
+        return self.h.network_packed(env)
 
     def controls(self, env=None):
         return self.h.controls(env)

@@ -53,6 +53,10 @@ enum gf_status {
 #define FE_NO_STATE_VALUES 0x40 /* skip the (N,6) state_values write              */
 #define FE_U_RESIDENT      0x80 /* u := the handle's action buffer as last set by
                                    fe_set_actions (already in HBM; u ignored)     */
+#define FE_PACKED_NETWORK 0x100 /* also write the adjacency as bits (B,N,ceil(N/64))
+                                   uint64 + degree (B,N) int32, the packed output
+                                   mode; with FE_NO_NETWORK the
+                                   dense (N,N) write is skipped: 32x fewer bytes  */
 
 typedef struct fe_config {
   int32_t n_agents;      /* N  (flocking_relative.py:38; params_from_cfg :74)      */
@@ -97,6 +101,8 @@ typedef struct fe_buffers {
   int32_t* knn_idx;      /* (B,N,k) int32 or NULL                                */
   float* knn_obs;        /* (B,N,4k) float32 or NULL                             */
   void* stream;          /* hipStream_t of the handle                            */
+  uint64_t* adj_bits;    /* (B,N,ceil(N/64)) packed adjacency or NULL (FE_PACKED_NETWORK) */
+  int32_t* degree;       /* (B,N) neighbour counts or NULL (FE_PACKED_NETWORK)   */
 } fe_buffers;
 
 /* Lifecycle ---------------------------------------------------------------- */
@@ -133,6 +139,10 @@ int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists,
 int fe_get_state_values(fe_handle* h, int env, float* dst);  /* (N,6) :128-129 */
 int fe_get_network(fe_handle* h, int env, float* dst);       /* (N,N) :131-134 */
 int fe_get_network_rows(fe_handle* h, int env, int row0, int nrows, float* dst);
+/* Packed output of the last FE_PACKED_NETWORK step: bit j%64 of word j/64 of row i is
+ * adj(i,j) (r2 < comm_radius^2, :117); the network is adj/max(degree,1) (:120-122).
+ * env < 0: all envs. Either pointer may be NULL. */
+int fe_get_network_packed(fe_handle* h, int env, uint64_t* bits, int32_t* degree);
 int fe_get_controls(fe_handle* h, int env, double* dst);     /* (N,2) :210-211 */
 int fe_get_rewards(fe_handle* h, double* dst);               /* (B)   :145-147 */
 int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs); /* (N,k), (N,4k) */

@@ -303,3 +303,29 @@ def test_env_resident_kernel_parity(monkeypatch):
         for b in range(B):
             check_against_oracle(h, x0[b], u[b], b)
         h.close()
+
+
+@pytest.mark.parametrize("n", [100, 1030])
+def test_packed_network_vs_oracle(n):
+    """FE_PACKED_NETWORK: adjacency bits and degrees (the packed output mode) match the
+    oracle bit for bit, alone or next to the dense rows."""
+    from gym_flock.vec import VecFlockingRelative
+    B = 3
+    x0 = synthetic_batch(B, n, seed0=500 + n)
+    u = np.random.RandomState(n).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    v = VecFlockingRelative(B, n)
+    for mode in ("both", "packed"):
+        v.reset(x=x0)
+        v.step(u, network=mode)
+        bits, deg = v.network_packed()
+        assert bits.shape == (B, n, (n + 63) // 64) and bits.dtype == np.uint64
+        for b in range(B):
+            ref = orc.step(x0[b], u[b])
+            adj = np.unpackbits(bits[b].view(np.uint8), axis=1, bitorder="little")[:, :n].astype(bool)
+            np.testing.assert_array_equal(adj, ref["adj"])
+            np.testing.assert_array_equal(deg[b], ref["deg"])
+            np.testing.assert_array_equal(v.get_state()[b], ref["x"])
+            close_sv(v.state_values(b), ref["state_values"])
+            if mode == "both":
+                np.testing.assert_array_equal(v.network(b), ref["network"].astype(np.float32))
+    v.close()
