@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -357,6 +358,33 @@ int fe_set_state(fe_handle* h, const double* x) {
   h->has_state = true;
   h->has_ctrl = h->has_obs = h->has_knn = false;
   return GF_OK;
+}
+
+int fe_reset_synthetic(fe_handle* h, uint64_t seed, double v_max) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (seed + (uint64_t)h->cfg.n_envs > 0x100000000ull) return fail(GF_EINVAL, "seed + n_envs must fit in 32 bits");
+  const int N = h->cfg.n_agents, B = h->cfg.n_envs;
+  std::vector<double> x((size_t)B * N * 4);
+  const double r_max = std::sqrt(static_cast<double>(N));
+  for (int b = 0; b < B; ++b) {
+    std::mt19937 mt(static_cast<uint32_t>(seed + b));  // RandomState(seed + b): init_genrand
+    auto uniform = [&](double lo, double hi) {          // random_sample (53-bit), then lo + (hi-lo)*u
+      const uint32_t a = mt() >> 5, c = mt() >> 6;
+      return lo + (hi - lo) * ((a * 67108864.0 + c) / 9007199254740992.0);
+    };
+    double* e = x.data() + (size_t)b * N * 4;
+    std::vector<double> len(N);
+    for (int i = 0; i < N; ++i) len[i] = std::sqrt(uniform(0.0, r_max));
+    for (int i = 0; i < N; ++i) {
+      const double ang = M_PI * uniform(0.0, 2.0);
+      e[4 * i] = len[i] * std::cos(ang);
+      e[4 * i + 1] = len[i] * std::sin(ang);
+    }
+    const double b0 = uniform(-v_max, v_max), b1 = uniform(-v_max, v_max);
+    for (int i = 0; i < N; ++i) e[4 * i + 2] = uniform(-v_max, v_max) + b0;
+    for (int i = 0; i < N; ++i) e[4 * i + 3] = uniform(-v_max, v_max) + b1;
+  }
+  return fe_set_state(h, x.data());
 }
 
 int fe_set_state_env(fe_handle* h, int env, const double* x) {

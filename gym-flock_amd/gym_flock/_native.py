@@ -90,6 +90,7 @@ SIGNATURES = {
     "fe_get_network": [_P, _I, _P],
     "fe_get_network_rows": [_P, _I, _I, _I, _P],
     "fe_get_network_packed": [_P, _I, _P, _P],
+    "fe_reset_synthetic": [_P, ctypes.c_uint64, ctypes.c_double],
     "fe_get_controls": [_P, _I, _P],
     "fe_get_rewards": [_P, _P],
     "fe_get_knn": [_P, _I, _P, _P],
@@ -212,6 +213,10 @@ class FlockHandle:
         check(self.lib.fe_set_dt(self.h, ptr(d)))
 
     # -- state
+    def reset_synthetic(self, seed=0, v_max=5.0):
+        """Synthetic init of every env in the library (fe_reset_synthetic)."""
+        check(self.lib.fe_reset_synthetic(self.h, int(seed), float(v_max)))
+
     def set_state(self, x, env=None):
         x = np.ascontiguousarray(x, dtype=np.float64)
         if env is None:

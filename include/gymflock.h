@@ -113,6 +113,12 @@ int fe_get_config(const fe_handle* h, fe_config* out);
 /* State ---------------------------------------------------------------------- */
 int fe_set_state(fe_handle* h, const double* x);            /* env.x = ... (:189) */
 int fe_set_state_env(fe_handle* h, int env, const double* x);  /* one env's (N,4) */
+/* Synthetic init (reset()'s distribution without the rejection loop,
+ * :164-175): env b is drawn from MT19937 seeded with seed + b in NumPy
+ * RandomState's order (length, angle, bias, vx, vy), with r_max = sqrt(N). The
+ * uniforms are NumPy's bit for bit; cos/sin come from the C library, so positions
+ * may differ from NumPy's in the last ulp. */
+int fe_reset_synthetic(fe_handle* h, uint64_t seed, double v_max);
 int fe_get_state(fe_handle* h, double* x);                  /* env.x (B,N,4) */
 int fe_get_state_env(fe_handle* h, int env, double* x);     /* one env's (N,4) */
 

@@ -329,3 +329,16 @@ def test_packed_network_vs_oracle(n):
             if mode == "both":
                 np.testing.assert_array_equal(v.network(b), ref["network"].astype(np.float32))
     v.close()
+
+
+def test_reset_synthetic_matches_numpy_draws():
+    """fe_reset_synthetic reproduces synthetic_batch (NumPy RandomState(seed + b)):
+    velocities bit-exact (same uniforms), positions to the last ulp of cos/sin."""
+    B, n = 4, 300
+    h = nat.FlockHandle(n, B)
+    h.reset_synthetic(seed=17)
+    ref = synthetic_batch(B, n, seed0=17)
+    x = h.get_state()
+    np.testing.assert_array_equal(x[..., 2:], ref[..., 2:])
+    np.testing.assert_allclose(x[..., :2], ref[..., :2], rtol=4e-16, atol=1e-300)
+    h.close()
