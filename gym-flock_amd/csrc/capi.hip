@@ -152,17 +152,29 @@ int next_reward_slot(fe_handle* h) {
   return GF_OK;
 }
 
-// Packed-output buffers on first use (FE_PACKED_NETWORK).
-int packed_outputs(fe_handle* h, int flags, gf::StepArgs& a) {
-  if (!(flags & FE_PACKED_NETWORK)) return GF_OK;
-  const size_t Wn = (h->cfg.n_agents + 63) / 64;
-  if (!h->adj_bits) {
-    if (int rc = dalloc(&h->adj_bits, h->BN * Wn)) return rc;
+// Packed-output buffers on first use: adjacency bits (FE_PACKED_NETWORK, or the kNN
+// step) and their degrees.
+int packed_outputs(fe_handle* h, bool bits, bool deg, gf::StepArgs& a) {
+  if (bits && !h->adj_bits)
+    if (int rc = dalloc(&h->adj_bits, h->BN * ((h->cfg.n_agents + 63) / 64))) return rc;
+  if ((bits || deg) && !h->pdeg)
     if (int rc = dalloc(&h->pdeg, h->BN)) return rc;
-  }
-  a.adj_bits = h->adj_bits;
-  a.degree_out = h->pdeg;
-  h->has_packed = true;
+  if (bits) a.adj_bits = h->adj_bits;
+  if (bits || deg) a.degree_out = h->pdeg;
+  return GF_OK;
+}
+
+// Flocking-v0: the step also writes this state's adjacency bits and degrees, from which
+// the kNN kernel that follows ranks each agent's neighbours.
+int knn_mode(const fe_handle* h, int flags) {
+  return ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0) ? 1 : 0;
+}
+
+int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a) {
+  const int km = knn_mode(h, flags);
+  const bool packed = flags & FE_PACKED_NETWORK;
+  if (int rc = packed_outputs(h, packed || km == 1, false, a)) return rc;
+  if (packed) h->has_packed = true;
   return GF_OK;
 }
 
@@ -227,9 +239,13 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a, bool dyn, bool uf64, bool 
   return GF_OK;
 }
 
-int launch_knn_cur(fe_handle* h) {
+// kNN of the current state; uses_adj: the last launch wrote this state's adjacency
+// (packed outputs), which lets agents with >= k neighbours rank only those.
+int launch_knn_cur(fe_handle* h, int mode) {
   gf::KnnArgs k{};
   k.x = h->x[h->cur];
+  k.adj_bits = mode == 1 ? h->adj_bits : nullptr;
+  k.degree = mode == 1 ? h->pdeg : nullptr;
   k.idx = h->knn_idx;
   k.obs = h->knn_obs;
   k.N = h->cfg.n_agents;
@@ -427,15 +443,16 @@ int fe_compute_helpers(fe_handle* h, int flags) {
   a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
-  if (int rc = packed_outputs(h, flags, a)) return rc;
+  const int km = knn_mode(h, flags);
+  if (int rc = prepare_outputs(h, flags, a)) return rc;
   if (int rc = timed_launch(h, a, false, false, ctrl)) return rc;
   if (ctrl) {
     h->ccur ^= 1;
     h->has_ctrl = true;
   }
   h->has_obs = true;
-  if ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0)
-    if (int rc = launch_knn_cur(h)) return rc;
+  if (km)
+    if (int rc = launch_knn_cur(h, km)) return rc;
   return GF_OK;
 }
 
@@ -473,15 +490,16 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
-  if (int rc = packed_outputs(h, flags, a)) return rc;
+  const int km = knn_mode(h, flags);
+  if (int rc = prepare_outputs(h, flags, a)) return rc;
   if (int rc = timed_launch(h, a, true, uf64, ctrl)) return rc;
   h->cur ^= 1;
   if (ctrl) h->ccur ^= 1;
   h->has_ctrl = ctrl;
   h->has_obs = true;
   h->has_knn = false;
-  if ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0)
-    if (int rc = launch_knn_cur(h)) return rc;
+  if (km)
+    if (int rc = launch_knn_cur(h, km)) return rc;
   // the host action buffer is borrowed only for this call: wait for its copy, not the step
   if (!(flags & (FE_U_DEVICE | FE_U_EXPERT | FE_U_RESIDENT))) GF_HIP(hipEventSynchronize(h->h2d_ev));
   return GF_OK;
@@ -636,7 +654,7 @@ int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs) {
   if (int rc = use_dev(h)) return rc;
   if (!h->has_knn) {
     if (!h->has_state) return fail(GF_ESTATE, "state not set");
-    if (int rc = launch_knn_cur(h)) return rc;
+    if (int rc = launch_knn_cur(h, 0)) return rc;  // no adjacency of this state at hand
   }
   const size_t K = h->cfg.n_neighbors, N = h->cfg.n_agents;
   const size_t off = env < 0 ? 0 : env * N;

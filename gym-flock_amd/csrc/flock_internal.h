@@ -11,6 +11,9 @@ constexpr int kTileDefault = 512;   // default tile (measured best, see step_til
 constexpr int kResidentRows = 32;   // rows per block of the env-resident kernel
 constexpr int kResidentMax = 1024;  // largest N whose env fits the resident kernel's LDS
 constexpr size_t kStepLdsFloor = 32 * 1024;  // plain step: 5 workgroups per CU (tuning)
+constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
+constexpr int kKnnFewSlow = 16;     // kNN: up to this many full-scan rows per workgroup
+                                    // go wave-cooperative, more go one row per thread
 
 // One batched hot-path launch. Pointers are device pointers; all per-env arrays
 // are [B][N][...] contiguous.
@@ -48,7 +51,7 @@ struct StepArgs {
   float us_f, uc_f;       // float32 copies of u_scale, u_clip
   const double* dt_env;   // (B) per-env dt of this step, or nullptr (dt)
   uint64_t* adj_bits;     // (B,N,Wn) packed adjacency or nullptr
-  int32_t* degree_out;    // (B,N) degrees or nullptr (with adj_bits)
+  int32_t* degree_out;    // (B,N) degrees or nullptr
 };
 
 struct KnnArgs {
@@ -56,6 +59,8 @@ struct KnnArgs {
   int32_t* idx;           // (B,N,K)
   float* obs;             // (B,N,4K)
   int N, B, K;
+  const uint64_t* adj_bits;  // (B,N,Wn) adjacency of x from the step, or nullptr
+  const int32_t* degree;     // (B,N) with adj_bits
 };
 
 struct StatsArgs {

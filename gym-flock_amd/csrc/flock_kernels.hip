@@ -145,6 +145,25 @@ __device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
   return s;
 }
 
+// Sorted insertion of (r2, j) into a K-list; ties go to the lower index (stable).
+template <int K>
+__device__ __forceinline__ void knn_insert(double (&kr)[K], int (&kj)[K], double r2, int j) {
+  if (r2 < kr[K - 1] || (r2 == kr[K - 1] && j < kj[K - 1])) {
+    double cr = r2;
+    int cj = j;
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+      const bool sw = (cr < kr[m]) || (cr == kr[m] && cj < kj[m]);
+      const double tr = sw ? kr[m] : cr;
+      const int tj = sw ? kj[m] : cj;
+      kr[m] = sw ? cr : kr[m];
+      kj[m] = sw ? cj : kj[m];
+      cr = tr;
+      cj = tj;
+    }
+  }
+}
+
 __device__ __forceinline__ double clip10(double v) {  // np.clip(v, -10, 10); NaN stays NaN
   return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v);
 }
@@ -815,20 +834,32 @@ __global__ __launch_bounds__(kThreads) void flock_step_resident_kernel(StepArgs 
 }
 
 // ---------------------------------------------------------------------------------
-// Flocking-v0 observation (flocking.py:20-25): the K smallest r2 per row, ties to the
-// lower index (the reference's argsort is unstable), self has r2=inf.
-// One thread per row keeps a sorted (r2, j) list in registers; the env's positions
-// stream through LDS and are read as wave-uniform broadcasts.
-template <int K>
+// Flocking-v0 observation (flocking.py:20-25): the K nearest agents by r2 (self
+// excluded by its infinite r2). One thread per agent. When the step left this
+// state's adjacency behind (adj_bits) and the agent has at least K neighbours, its K
+// nearest are all neighbours (every non-neighbour is farther: r2 >= comm_radius^2 >
+// any neighbour's), so only its ~deg set bits are ranked. Every other agent (few: the
+// swarm's sparse rim) is ranked by its whole wave: lanes scan columns lane, lane+64,
+// ... into lane-local K-lists, and K rounds of a wave-wide (r2, j) minimum merge them.
+template <int K, bool LDS>
 __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
-  __shared__ double2 tile[kTileMax];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N;
   const int bpe = (N + kThreads - 1) / kThreads;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / bpe;
   const int i = (L - b * bpe) * kThreads + threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const bool vi = i < N;
   const double* xb = a.x + (size_t)b * N * 4;
+  // positions: the whole env staged in LDS (N <= kKnnLdsMax), else read from L2
+  const double2* gpos = reinterpret_cast<const double2*>(xb);
+  double2* lpos = reinterpret_cast<double2*>(smem);
+  if (LDS) {
+    for (int t = threadIdx.x; t < N; t += kThreads) lpos[t] = gpos[2 * (size_t)t];
+    __syncthreads();
+  }
+  auto pos = [&](int j) -> double2 { return LDS ? lpos[j] : gpos[2 * (size_t)j]; };
   double pxi = 0, pyi = 0;
   if (vi) {
     pxi = xb[4 * (size_t)i];
@@ -841,37 +872,88 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
     kr[m] = __builtin_inf();
     kj[m] = INT_MAX;
   }
-  for (int j0 = 0; j0 < N; j0 += kTileMax) {
-    const int tc = min(kTileMax, N - j0);
-    __syncthreads();
-    for (int t = threadIdx.x; t < tc; t += kThreads)
-      tile[t] = reinterpret_cast<const double2*>(xb)[2 * (size_t)(j0 + t)];
-    __syncthreads();
-    if (vi) {
-      for (int t = 0; t < tc; ++t) {
-        const int j = j0 + t;
-        const double2 p = tile[t];
+  const size_t g = (size_t)b * N + i;
+  const bool fast = vi && a.adj_bits && a.degree[g] >= K;
+  if (fast) {  // rank the neighbours only
+    const int Wn = (N + 63) >> 6;
+    const uint64_t* bits = a.adj_bits + g * Wn;
+    for (int w = 0; w < Wn; ++w) {
+      uint64_t m = bits[w];
+      while (m) {
+        const int j = (w << 6) + __builtin_ctzll(m);
+        m &= m - 1;
+        const double2 p = pos(j);
         const double dx = pxi - p.x, dy = pyi - p.y;
-        const double r2 = (j == i) ? __builtin_inf() : dx * dx + dy * dy;
-        if (r2 < kr[K - 1] || (r2 == kr[K - 1] && j < kj[K - 1])) {
-          double cr = r2;
-          int cj = j;
+        knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
+      }
+    }
+  }
+  // Agents the neighbour ranking cannot serve: when a workgroup holds only a few, its
+  // waves rank each of them together (lanes scan columns lane, lane+64, ... into
+  // lane-local lists, then K rounds of a wave-wide (r2, j) minimum merge them); when it
+  // holds many (a dispersed swarm), every thread scans its own row, which keeps the
+  // lanes busy on distinct rows.
+  const int nslow = __syncthreads_count(vi && !fast);
+  if (nslow > kKnnFewSlow) {
+    for (int j0 = 0; j0 < N; j0 += 64) {
+      if (vi && !fast) {
+        const int tc = min(64, N - j0);
+        for (int t = 0; t < tc; ++t) {
+          const int j = j0 + t;
+          const double2 p = pos(j);
+          const double dx = pxi - p.x, dy = pyi - p.y;
+          knn_insert<K>(kr, kj, (j == i) ? __builtin_inf() : dx * dx + dy * dy, j);
+        }
+      }
+    }
+  } else {
+    uint64_t todo = __ballot(vi && !fast);
+    while (todo) {  // wave-cooperative full scan, one row at a time
+      const int l = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int row = __shfl(i, l);
+      const double px = __shfl(pxi, l), py = __shfl(pyi, l);
+      double lr[K];
+      int lj[K];
 #pragma unroll
-          for (int m = 0; m < K; ++m) {
-            const bool sw = (cr < kr[m]) || (cr == kr[m] && cj < kj[m]);
-            const double tr = sw ? kr[m] : cr;
-            const int tj = sw ? kj[m] : cj;
-            kr[m] = sw ? cr : kr[m];
-            kj[m] = sw ? cj : kj[m];
-            cr = tr;
-            cj = tj;
+      for (int m = 0; m < K; ++m) {
+        lr[m] = __builtin_inf();
+        lj[m] = INT_MAX;
+      }
+      for (int j = lane; j < N; j += 64) {
+        const double2 p = pos(j);
+        const double dx = px - p.x, dy = py - p.y;
+        knn_insert<K>(lr, lj, (j == row) ? __builtin_inf() : dx * dx + dy * dy, j);
+      }
+#pragma unroll
+      for (int m = 0; m < K; ++m) {
+        double br = lr[0];
+        int bj = lj[0];
+        for (int o = 32; o > 0; o >>= 1) {
+          const double orr = __shfl_xor(br, o);
+          const int oj = __shfl_xor(bj, o);
+          if (orr < br || (orr == br && oj < bj)) {
+            br = orr;
+            bj = oj;
           }
+        }
+        if (lane == l) {
+          kr[m] = br;
+          kj[m] = bj;
+        }
+        if (lj[0] == bj) {  // the winner's lane pops its head (columns are disjoint per lane)
+#pragma unroll
+          for (int q = 0; q + 1 < K; ++q) {
+            lr[q] = lr[q + 1];
+            lj[q] = lj[q + 1];
+          }
+          lr[K - 1] = __builtin_inf();
+          lj[K - 1] = INT_MAX;
         }
       }
     }
   }
   if (!vi) return;
-  const size_t g = (size_t)b * N + i;
   const double2* xi = reinterpret_cast<const double2*>(xb) + 2 * (size_t)i;
   const double2 pi = xi[0], vv = xi[1];
 #pragma unroll
@@ -1015,7 +1097,7 @@ static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if (a.variant) return launch_step_tiled<DYN, UF64, CTRL, true>(a, s);
-  if (a.resident && !a.adj_bits) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
+  if (a.resident && !a.adj_bits && !a.degree_out) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
   return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
 }
 
@@ -1029,9 +1111,16 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
   const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
+  const bool lds = a.N <= kKnnLdsMax;
+  const size_t bytes = lds ? (size_t)a.N * 16 : 0;  // the env's positions
   switch (a.K) {
-#define GF_KNN_CASE(k) \
-  case k: hipLaunchKernelGGL(flock_knn_kernel<k>, dim3(grid), dim3(kThreads), 0, s, a); break;
+#define GF_KNN_CASE(k)                                                                            \
+  case k:                                                                                         \
+    if (lds)                                                                                      \
+      hipLaunchKernelGGL((flock_knn_kernel<k, true>), dim3(grid), dim3(kThreads), bytes, s, a);  \
+    else                                                                                          \
+      hipLaunchKernelGGL((flock_knn_kernel<k, false>), dim3(grid), dim3(kThreads), 0, s, a);     \
+    break;
     GF_KNN_CASE(1) GF_KNN_CASE(2) GF_KNN_CASE(3) GF_KNN_CASE(4) GF_KNN_CASE(5) GF_KNN_CASE(6)
     GF_KNN_CASE(7) GF_KNN_CASE(8) GF_KNN_CASE(10) GF_KNN_CASE(12) GF_KNN_CASE(16)
 #undef GF_KNN_CASE
