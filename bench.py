@@ -28,6 +28,10 @@ sys.path.insert(0, os.path.join(ROOT, "gym-flock_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+# HIP events bracket every TIMING_EVERY-th step launch in the timed region (roofline
+# kernel time); an event pair keeps that launch from overlapping its neighbours, so
+# timing every launch would add ~7 us to every step's wall time
+TIMING_EVERY = 8
 # (N, envs per GPU, GPUs) -> which BASELINE.json config the run is
 CONFIG_TAG = {(1024, 256, 1): " (BASELINE.json configs[1])", (1024, 256, 8): " (BASELINE.json configs[2])",
               (8192, 32, 1): " (BASELINE.json configs[4])"}
@@ -276,7 +280,7 @@ def main():
 
     run(W)
     barrier()
-    env.h.timing_start()
+    env.h.timing_start(every=TIMING_EVERY)
     t0 = time.perf_counter()
     run(K)
     env.sync()
@@ -322,7 +326,7 @@ def main():
         env.reset(seed=0)
         env.step(resident=True, network="packed")
         barrier()
-        env.h.timing_start()
+        env.h.timing_start(every=TIMING_EVERY)
         t4 = time.perf_counter()
         for _ in range(K):
             env.step(resident=True, network="packed")

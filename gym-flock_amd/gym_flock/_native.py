@@ -336,8 +336,9 @@ class FlockHandle:
         check(self.lib.fe_sync(self.h))
 
     # -- timing (bench)
-    def timing_start(self):
-        check(self.lib.fe_kernel_timing(self.h, 1, None, None))
+    def timing_start(self, every=1):
+        """Time every `every`-th step launch with HIP events (fe_kernel_timing)."""
+        check(self.lib.fe_kernel_timing(self.h, int(every), None, None))
 
     def timing_stop(self):
         ms, n = ctypes.c_double(), ctypes.c_int64()

@@ -256,8 +256,10 @@ int cov_get_graphs_tuple(cov_handle* h, int32_t* n_node, float* nodes, int32_t* 
 /* Diagnostics ---------------------------------------------------------------- */
 const char* fe_last_error(void);
 int fe_abi_version(void);
-/* Average device time (ms) of the dominant step kernel over the launches since the
- * last reset, measured with HIP events on the handle's stream (bench roofline). */
+/* Average device time (ms) of the step kernel, measured with HIP events on the
+ * handle's stream (bench roofline). enable >= 1 starts timing every enable-th launch
+ * (events keep a sampled launch from overlapping its neighbours); 0 reads and stops;
+ * -1 reads and keeps timing. */
 int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches);
 /* Diagnostics for roofline work: what = 0/1 times `reps` launches of a float4
  * plain/non-temporal fill of the network buffer (the write-bandwidth ceiling);
