@@ -342,3 +342,40 @@ def test_reset_synthetic_matches_numpy_draws():
     np.testing.assert_array_equal(x[..., 2:], ref[..., 2:])
     np.testing.assert_allclose(x[..., :2], ref[..., :2], rtol=4e-16, atol=1e-300)
     h.close()
+
+
+def test_degenerate_states_match_oracle():
+    """Edge states: coincident agents (r2 = 0: the reference's 0/0 features are NaN),
+    agents exactly on the comm-radius boundary, coordinates above the float32
+    prefilter's range (every pair decided in float64), and a non-finite agent."""
+    n = 40
+    rs = np.random.RandomState(9)
+    base = rs.uniform(-2, 2, size=(n, 4))
+    cases = []
+    x = base.copy()
+    x[1, :2] = x[0, :2]  # coincident pair
+    cases.append(x)
+    x = base.copy()
+    x[:, 1] = 0.0
+    x[:, 0] = np.arange(n) * 0.9  # neighbours exactly 0.9 apart: r2 = 0.81 is not < 0.81
+    cases.append(x)
+    x = base.copy()
+    x[:, :2] += 3.0e5  # |coordinates| beyond the float32 band's validity
+    cases.append(x)
+    x = base.copy()
+    x[5, 0] = np.inf
+    cases.append(x)
+    for x0 in cases:
+        u = rs.uniform(-1, 1, size=(n, 2)).astype(np.float32)
+        h = nat.FlockHandle(n, 1)
+        h.set_state(x0[None])
+        h.step(u[None], nat.FE_WITH_CONTROLLER)
+        with np.errstate(all="ignore"):
+            ref = orc.step(x0, u, with_controller=True)
+        np.testing.assert_array_equal(h.get_state(0), ref["x"])
+        np.testing.assert_array_equal(h.network(0) > 0, ref["adj"])
+        sv = h.state_values(0)
+        np.testing.assert_array_equal(np.isnan(sv), np.isnan(ref["state_values"].astype(np.float32)))
+        ok = ~np.isnan(ref["state_values"])
+        np.testing.assert_allclose(sv[ok], ref["state_values"][ok], rtol=1e-5, atol=1e-9)
+        h.close()
