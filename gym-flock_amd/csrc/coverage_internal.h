@@ -29,6 +29,7 @@ struct CovArgs {
   int32_t* senders;       // (B,4M)
   int32_t* receivers;     // (B,4M)
   int64_t* obs_step;      // (B)
+  double* axy;            // (B,Tmax,4,2) coordinates of each node's 4 action targets
   int* err;               // device error bits: 1 degree > 4, 2 edges overflow, 4 bad action
 };
 

@@ -100,7 +100,18 @@ __global__ __launch_bounds__(kCovThreads) void cov_graph_kernel(CovArgs a, const
     nodes[3 * k + 1] = (k >= R && k < R + T) ? 1.0f : 0.0f;
     nodes[3 * k + 2] = 0.0f;
   }
-  if (tid == 0) a.n_motion[b] = n_motion;
+  // coordinates of every node's 4 action targets (padding = the node itself), so a
+  // step reads a moved robot's new action edges in one round trip
+  double2* axy = reinterpret_cast<double2*>(a.axy) + (size_t)b * Tm * 4;
+  for (int k = tid; k < 4 * T; k += kCovThreads) {
+    const int t = k >> 2, ac = k & 3;
+    const int q = ac < cnt[t] ? nbr[4 * t + ac] : t;
+    axy[k] = make_double2(tg[2 * q], tg[2 * q + 1]);
+  }
+  if (tid == 0) {
+    a.n_motion[b] = n_motion;
+    a.dirty[b] = 1;  // a new graph: the next pass recomputes nodes and action edges
+  }
 }
 
 // Action targets of a robot on node c (global): its out-neighbours, padded with c.
@@ -110,6 +121,14 @@ __device__ __forceinline__ int action_node(const int32_t* nbr, const int32_t* cn
 }
 
 // One step (or, with a.actions == nullptr, the observation that reset() returns).
+//
+// Two dependent global round trips per env. (1) Each robot's node, action, and the 4
+// action targets its node offers: the observation tail written by the previous pass
+// already lists them (coverage.py:206-232), so the chosen node needs no neighbour
+// lookup. (2) After the LDS-only claim resolution, each robot that moved reads its new
+// node's position, visited flag, neighbours and their coordinates (cov_graph_kernel's
+// table) together, and rewrites its 8 tail edges; a robot that stayed keeps its edges.
+// After an external placement, a new graph or a reset, everything is recomputed.
 __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -127,9 +146,14 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   const double* tg = a.tgt + (size_t)b * Tm * 2;
   const int32_t* nbr = a.nbr + (size_t)b * Tm * 4;
   const int32_t* cnt = a.cnt + (size_t)b * Tm;
+  const double2* axy = reinterpret_cast<const double2*>(a.axy) + (size_t)b * Tm * 4;
   double* xr = a.xr + (size_t)b * R * 2;
   int32_t* cur = a.cur + (size_t)b * R;
   uint8_t* vis = a.visited + (size_t)b * Tm;
+  int32_t* snd = a.senders + (size_t)b * E;
+  int32_t* rcv = a.receivers + (size_t)b * E;
+  float* edg = a.edges + (size_t)b * E;
+  const int base = E - 8 * R;  // action edges: [base, base+4R) target->robot, then robot->target
 
   for (int k = tid; k < W; k += kCovThreads) {
     claim[k] = 0u;
@@ -138,8 +162,13 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   if (tid == 0) *counter = 0;
   // closest_targets (:427-432): cached node unless the robots were placed externally
   const bool dirty = a.dirty[b] != 0;
+  const bool full = dirty || !a.actions;  // recompute every robot's action edges
+  const int32_t* act = a.actions ? a.actions + (size_t)b * R : nullptr;
   for (int i = tid; i < R; i += kCovThreads) {
     int c = cur[i];
+    int ai = act ? act[i] : 0;
+    int4 offer = make_int4(0, 0, 0, 0);
+    if (act && !dirty) offer = *reinterpret_cast<const int4*>(snd + base + 4 * i);
     if (dirty) {
       const double px = xr[2 * i], py = xr[2 * i + 1];
       double best = __builtin_inf();
@@ -154,23 +183,21 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       c += R;
     }
     cur_s[i] = c;
-  }
-  __syncthreads();
-
-  if (a.actions) {
-    // step (:184-200): chosen node per robot; robots that stay claim first
-    const int32_t* act = a.actions + (size_t)b * R;
-    for (int i = tid; i < R; i += kCovThreads) {
-      int ai = act[i];
+    if (act) {
+      // step (:184-200): the node the action points at; robots that stay claim first
       if (ai < 0 || ai >= 4) {
         atomicOr(a.err, 4);
         ai = 0;
       }
-      const int c = cur_s[i];
-      const int n = action_node(nbr, cnt, c, ai, R);
+      const int n = dirty ? action_node(nbr, cnt, c, ai, R)
+                          : (ai == 0 ? offer.x : ai == 1 ? offer.y : ai == 2 ? offer.z : offer.w);
       chosen[i] = n;
       if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
     }
+  }
+  __syncthreads();
+
+  if (act) {
     // then, in robot order, a move succeeds unless its node is already claimed; a
     // blocked robot stays and its node joins the claims. The reference walks the robots
     // serially; here every robot's outcome is re-evaluated in parallel from the current
@@ -202,17 +229,32 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     __syncthreads();
   }
 
-  // move (:198) and visit (:265-266, :359): count nodes that flip to visited
+  // move (:198), visit (:265-266, :359) and the observation tail (:259-323)
   float* nodes = a.nodes + (size_t)b * M * 3;
   for (int i = tid; i < R; i += kCovThreads) {
     const int n = new_s[i];
-    if (n != cur_s[i]) {  // a robot that does not move keeps its position (:198)
-      xr[2 * i] = tg[2 * (n - R)];
-      xr[2 * i + 1] = tg[2 * (n - R) + 1];
-    }
-    cur[i] = n;
     const int t = n - R;
-    if (!vis[t]) {
+    const bool moved = n != cur_s[i];
+    cur[i] = n;
+    if (!moved && !full) continue;  // same node, same position: its edges stand
+    // one round trip: position, visited flag, action targets and their coordinates
+    double px, py;
+    if (moved) {  // a robot that does not move keeps its position (:198)
+      px = tg[2 * t];
+      py = tg[2 * t + 1];
+    } else {
+      px = xr[2 * i];
+      py = xr[2 * i + 1];
+    }
+    const uint8_t was = vis[t];
+    const int4 q4 = *reinterpret_cast<const int4*>(nbr + 4 * t);
+    const int nc = cnt[t];
+    const double2 c0 = axy[4 * t], c1 = axy[4 * t + 1], c2 = axy[4 * t + 2], c3 = axy[4 * t + 3];
+    if (moved) {
+      xr[2 * i] = px;
+      xr[2 * i + 1] = py;
+    }
+    if (!was) {
       const unsigned old = atomicOr(&seen[n >> 5], 1u << (n & 31));
       if (!(old & (1u << (n & 31)))) {
         vis[t] = 1;
@@ -220,26 +262,22 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
         atomicAdd(counter, 1);
       }
     }
+    const int qs[4] = {q4.x, q4.y, q4.z, q4.w};
+    const double2 cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int ac = 0; ac < 4; ++ac) {
+      const int q = ac < nc ? qs[ac] + R : n;
+      const float d = static_cast<float>(dist2d(px, py, cs[ac].x, cs[ac].y) / a.res);
+      const int k = 4 * i + ac;
+      snd[base + k] = q;
+      snd[base + 4 * R + k] = i;
+      rcv[base + k] = i;
+      rcv[base + 4 * R + k] = q;
+      edg[base + k] = d;
+      edg[base + 4 * R + k] = d;
+    }
   }
   __syncthreads();
-
-  // observation tail (:259-323): 4 action edges per robot, both directions
-  int32_t* snd = a.senders + (size_t)b * E;
-  int32_t* rcv = a.receivers + (size_t)b * E;
-  float* edg = a.edges + (size_t)b * E;
-  const int base = E - 8 * R;
-  for (int k = tid; k < 4 * R; k += kCovThreads) {
-    const int i = k >> 2, ac = k & 3;
-    const int c = new_s[i];
-    const int q = action_node(nbr, cnt, c, ac, R);
-    const float d = static_cast<float>(dist2d(xr[2 * i], xr[2 * i + 1], tg[2 * (q - R)], tg[2 * (q - R) + 1]) / a.res);
-    snd[base + k] = q;
-    snd[base + 4 * R + k] = i;
-    rcv[base + k] = i;
-    rcv[base + 4 * R + k] = q;
-    edg[base + k] = d;
-    edg[base + 4 * R + k] = d;
-  }
   if (tid == 0) {
     const int newly = *counter;
     const int nv = a.nvisited[b] + newly;
