@@ -122,6 +122,14 @@ SIGNATURES = {
     "cov_get_flat_obs": [_P, _P, _I],
     "cov_graphs_tuple_sizes": [_P, _P, _P, _I],
     "cov_get_graphs_tuple": [_P, _P, _P, _P, _P, _P, _P, _P, _I],
+    "gu_create": [_I, ctypes.POINTER(_P)],
+    "gu_destroy": [_P],
+    "gu_radius_edges": [_P, _P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_double, _I,
+                        ctypes.POINTER(ctypes.c_int64)],
+    "gu_k_edges": [_P, ctypes.c_int32, _P, ctypes.c_int32, _P, ctypes.c_int32, _I, _I,
+                   ctypes.POINTER(ctypes.c_int64)],
+    "gu_get_edges": [_P, _P, _P, _P, _P],
+    "gu_nodes_within_radius": [_P, _P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_double, _P],
     "fe_last_error": [],
     "fe_abi_version": [],
     "fe_diag": [_P, _I, _I, ctypes.POINTER(ctypes.c_double)],
@@ -510,3 +518,64 @@ class CoverageHandle:
         p = np.empty((n_targets, n_targets), np.int32)
         check(self.lib.cov_get_time_matrix(self.h, int(env), ptr(c), ptr(p)))
         return c, p
+
+
+class GraphUtils:
+    """Owns one gu_graph context: the radius / k-nearest graph helpers of
+    gym_flock/envs/spatial/utils.py (:8-24, :27-39, :60-88) on the device."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.gu_create(device, ctypes.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def _pos(p):
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        if p.ndim != 2 or p.shape[1] != 2:
+            raise ValueError("positions must be (n, 2), got %s" % (p.shape,))
+        return p
+
+    def _edges(self, n):
+        E = int(n.value)
+        snd = np.empty(E, np.int32)
+        rcv = np.empty(E, np.int32)
+        r = np.empty(E, np.float64)
+        diff = np.empty(2 * E, np.float64)
+        check(self.lib.gu_get_edges(self.h, ptr(snd), ptr(rcv), ptr(r), ptr(diff)))
+        return snd, rcv, r, diff
+
+    def radius_edges(self, rad, pos1, pos2=None, self_loops=False):
+        """(senders, receivers, r, diff) with diff = every dx then every dy."""
+        p1 = self._pos(pos1)
+        p2 = None if pos2 is None else self._pos(pos2)
+        n = ctypes.c_int64()
+        check(self.lib.gu_radius_edges(self.h, ptr(p1), len(p1), ptr(p2), 0 if p2 is None else len(p2),
+                                       float(rad), int(bool(self_loops)), ctypes.byref(n)))
+        return self._edges(n)
+
+    def k_edges(self, k, pos1, pos2=None, self_loops=False, allow_nearest=False):
+        p1 = self._pos(pos1)
+        p2 = None if pos2 is None else self._pos(pos2)
+        n = ctypes.c_int64()
+        check(self.lib.gu_k_edges(self.h, int(k), ptr(p1), len(p1), ptr(p2), 0 if p2 is None else len(p2),
+                                  int(bool(self_loops)), int(bool(allow_nearest)), ctypes.byref(n)))
+        return self._edges(n)
+
+    def nodes_within_radius(self, rad, pos1, pos2):
+        p1, p2 = self._pos(pos1), self._pos(pos2)
+        valid = np.empty(len(p2), np.uint8)
+        check(self.lib.gu_nodes_within_radius(self.h, ptr(p1), len(p1), ptr(p2), len(p2), float(rad), ptr(valid)))
+        return valid.astype(bool)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -253,6 +253,33 @@ int cov_graphs_tuple_sizes(cov_handle* h, int32_t* n_edge, int64_t* total_edges,
 int cov_get_graphs_tuple(cov_handle* h, int32_t* n_node, float* nodes, int32_t* n_edge, float* edges,
                          int32_t* senders, int32_t* receivers, float* globs, int flags);
 
+/* Graph helpers of gym_flock/envs/spatial/utils.py ------
+ * A context owns device scratch and the last edge list. Positions are host float64
+ * (n, 2) arrays; pos2 == NULL means pos2 = pos1 (the reference's pos2=None), with the
+ * diagonal as the self pair. Edges come out in np.nonzero's row-major order. */
+typedef struct gu_graph gu_graph;
+int gu_create(int device, gu_graph** out);
+int gu_destroy(gu_graph* g);
+/* _get_graph_edges(rad, pos1, pos2=None, self_loops=False), utils.py:8-24: pairs with
+ * r = |pos1[i] - pos2[j]| != 0 and not r > rad. *n_edges = their count. */
+int gu_radius_edges(gu_graph* g, const double* pos1, int32_t n1, const double* pos2, int32_t n2, double rad,
+                    int self_loops, int64_t* n_edges);
+/* _get_k_edges(k, pos1, pos2=None, self_loops=False, allow_nearest=False),
+ * utils.py:60-88: per row the k smallest r (allow_nearest), or the k+1 smallest minus
+ * the row's argmin. Equal distances at the k-th boundary go to the lower column (numpy
+ * leaves that choice to its selection algorithm). GF_EINVAL where np.argpartition
+ * raises (kth >= row length). */
+int gu_k_edges(gu_graph* g, int32_t k, const double* pos1, int32_t n1, const double* pos2, int32_t n2,
+               int self_loops, int allow_nearest, int64_t* n_edges);
+/* The last result: senders/receivers (E) i32, r (E) f64, diff (2E) f64 = every edge's
+ * dx, then every dy (the reference's np.hstack of the two difference columns). Any
+ * pointer may be NULL. */
+int gu_get_edges(gu_graph* g, int32_t* senders, int32_t* receivers, double* r, double* diff);
+/* _nodes_within_radius(rad, pos1, pos2), utils.py:27-39: valid[j] = 1 when the column
+ * sum of r (r > rad zeroed) over pos1 is > 0. */
+int gu_nodes_within_radius(gu_graph* g, const double* pos1, int32_t n1, const double* pos2, int32_t n2, double rad,
+                           uint8_t* valid);
+
 /* Diagnostics ---------------------------------------------------------------- */
 const char* fe_last_error(void);
 int fe_abi_version(void);

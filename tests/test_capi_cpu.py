@@ -16,13 +16,13 @@ HEADER = os.path.join(ROOT, "include", "gymflock.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+((?:fe|cov)_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+((?:fe|cov|gu)_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_declares_the_abi():
     syms = declared_symbols()
     for s in ("fe_create", "fe_step", "fe_controller", "fe_get_network", "fe_allgather_rewards",
-              "cov_create", "cov_step", "cov_reset", "cov_get_obs"):
+              "cov_create", "cov_step", "cov_reset", "cov_get_obs", "gu_radius_edges", "gu_k_edges"):
         assert s in syms
 
 
@@ -165,3 +165,18 @@ def test_coverage_create_validates_arguments():
     for cfg in (nat.CovConfig(0, 1, 500, 75, 5.5, 6.6, 0), nat.CovConfig(6, 1, 6, 75, 5.5, 6.6, 0),
                 nat.CovConfig(6, 0, 500, 75, 5.5, 6.6, 0), nat.CovConfig(6, 1, 500, 75, -1.0, 6.6, 0)):
         assert lib.cov_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.GF_EINVAL
+
+
+def test_reference_module_paths_import():
+    """Callers import envs and helpers by the reference's module paths."""
+    import importlib
+    from gym_flock.envs.flocking import variants
+    for mod, cls in (("flocking_leader", "FlockingLeaderEnv"), ("flocking_obstacle", "FlockingObstacleEnv"),
+                     ("flocking_stoch", "FlockingStochasticEnv"), ("flocking_twoflocks", "FlockingTwoFlocksEnv")):
+        m = importlib.import_module("gym_flock.envs.flocking." + mod)
+        assert getattr(m, cls) is getattr(variants, cls)
+    u = importlib.import_module("gym_flock.envs.spatial.utils")
+    for fn in ("_get_graph_edges", "_get_k_edges", "_get_pos_diff", "_nodes_within_radius"):
+        assert callable(getattr(u, fn))
+    p = np.arange(6.0).reshape(3, 2)
+    assert u._get_pos_diff(p).shape == (3, 3, 2) and u._get_pos_diff(p, p[:2]).shape == (3, 2, 2)
