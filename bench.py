@@ -152,22 +152,30 @@ def bench_coverage(args):
     for _ in range(W):
         v.step(resident=True)
     v.sync()
+    v.h.timing_start(every=TIMING_EVERY)
     t0 = time.perf_counter()
     for _ in range(K):
         v.step(resident=True)
     v.sync()
     el = time.perf_counter() - t0
+    kernel_ms, launches = v.h.timing_stop()
+    # algorithmic bytes per env-step: the 8R-edge observation tail (sender, receiver,
+    # edge: 12 B each) + per robot its action, node, position, visited flag and 4
+    # action-target coordinates + the reward/done/step words
     per_env = 8 * R * 12 + R * (16 + 4 + 4 + 4 + 16) + 16
+    achieved = B * per_env / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     line = {"metric": "robot-steps/sec (N_robots x N_envs x steps/s), Coverage-v0 R=200",
             "value": R * B * K / el, "unit": "robot-steps/s", "n_gpus": 1, "steps": K, "warmup": W,
             "ms_per_step": 1e3 * el / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (generated map, random starts/unvisited/actions)",
             "config": {"workload": "Coverage-v0 step(), R=200 robots, T=%d targets, max_nodes %d, %d envs "
                                    "(BASELINE.json configs[3])" % (len(targets), M, B)},
-            "roofline": {"bound": "latency", "note": "one workgroup per env; the collision pass is serial "
-                         "in robot order like the reference", "achieved": B * per_env / (el / K) / 1e9,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B * per_env / (el / K) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": None}}
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "cov_step_kernel",
+                         "kernel_ms": kernel_ms, "launches_timed": launches,
+                         "algorithmic_bytes_per_launch": B * per_env,
+                         "note": "latency-limited, not bandwidth-limited: one workgroup per env, two dependent "
+                                 "global round trips and the claim resolution per step (DESIGN.md)"}}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = coverage_cpu_baseline(targets, R, M, min(args.cpu_seconds, 8.0))
     line["greedy_expert"] = bench_greedy(v, targets, R, M, B, K, args)

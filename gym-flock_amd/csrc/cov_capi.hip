@@ -68,6 +68,12 @@ struct cov_handle {
   unsigned char* scratch = nullptr;
   size_t scratch_bytes = 0;
   int64_t* goff = nullptr;
+  // step-kernel timing (cov_kernel_timing): HIP events around every stride-th launch
+  bool timing = false;
+  int timing_stride = 1;
+  int64_t timing_count = 0;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
 };
 
 namespace {
@@ -89,6 +95,7 @@ void cov_release(cov_handle* h) {
                   h->goff};
   for (void* p : bufs)
     if (p) hipFree(p);
+  for (hipEvent_t e : h->ev) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
 }
@@ -361,9 +368,48 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     CV_HIP(hipMemcpyAsync(h->actions, actions, n * 4, hipMemcpyHostToDevice, h->stream));
     a.actions = h->actions;
   }
+  const bool sample = h->timing && (h->timing_count++ % h->timing_stride) == 0;
+  if (sample) {
+    if (h->ev_used + 2 > h->ev.size()) {
+      for (int k = 0; k < 64; ++k) {
+        hipEvent_t ev;
+        CV_HIP(hipEventCreate(&ev));
+        h->ev.push_back(ev);
+      }
+    }
+    CV_HIP(hipEventRecord(h->ev[h->ev_used], h->stream));
+  }
   hipError_t e = gf::launch_cov_step(a, h->stream);
   if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
+  if (sample) {
+    CV_HIP(hipEventRecord(h->ev[h->ev_used + 1], h->stream));
+    h->ev_used += 2;
+  }
   if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT))) CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launches) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (int rc = use(h)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  if (enable >= 1) {  // start: time every enable-th step launch
+    h->ev_used = 0;
+    h->timing = true;
+    h->timing_stride = enable;
+    h->timing_count = 0;
+    return GF_OK;
+  }
+  double tot = 0;
+  for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
+    float ms = 0;
+    CV_HIP(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
+    tot += ms;
+  }
+  const int64_t n = (int64_t)(h->ev_used / 2);
+  if (avg_ms) *avg_ms = n ? tot / n : 0.0;
+  if (launches) *launches = n;
+  if (enable == 0) h->timing = false;
   return GF_OK;
 }
 

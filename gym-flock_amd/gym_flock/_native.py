@@ -134,6 +134,7 @@ SIGNATURES = {
     "fe_abi_version": [],
     "fe_diag": [_P, _I, _I, ctypes.POINTER(ctypes.c_double)],
     "fe_kernel_timing": [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
+    "cov_kernel_timing": [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
 }
 _RESTYPE = {"fe_last_error": ctypes.c_char_p}
 
@@ -406,6 +407,15 @@ class CoverageHandle:
             self.h = None
 
     __del__ = close
+
+    def timing_start(self, every=1):
+        """Time every `every`-th step launch with HIP events (cov_kernel_timing)."""
+        check(self.lib.cov_kernel_timing(self.h, int(every), None, None))
+
+    def timing_stop(self):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        check(self.lib.cov_kernel_timing(self.h, 0, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
 
     def set_targets(self, targets, env=-1):
         t = np.ascontiguousarray(targets, dtype=np.float64)

@@ -288,6 +288,8 @@ int fe_abi_version(void);
  * (events keep a sampled launch from overlapping its neighbours); 0 reads and stops;
  * -1 reads and keeps timing. */
 int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches);
+/* The same for cov_step_kernel on a Coverage handle. */
+int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launches);
 /* Diagnostics for roofline work: what = 0/1 times `reps` launches of a float4
  * plain/non-temporal fill of the network buffer (the write-bandwidth ceiling);
  * what = 0x100 | bits sets ablation switches on later step launches (0x100 clears). */
