@@ -159,17 +159,44 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     claim[k] = 0u;
     seen[k] = 0u;
   }
+  if (a.actions)
+    for (int k = tid; k < M; k += kCovThreads) first[k] = INT_MAX;
   if (tid == 0) *counter = 0;
-  // closest_targets (:427-432): cached node unless the robots were placed externally
+  // the env's words, loaded up front so none of them costs a round trip of its own
   const bool dirty = a.dirty[b] != 0;
+  const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
   const bool full = dirty || !a.actions;  // recompute every robot's action edges
   const int32_t* act = a.actions ? a.actions + (size_t)b * R : nullptr;
+  // One robot per thread (R <= kCovThreads): the data of the node a robot will end on
+  // (if it moves: the chosen node; in a full pass: its node) is loaded right after the
+  // chosen node is known, so that round trip runs under the claim resolution.
+  const bool one = R <= kCovThreads;
+  int pn = -1;  // node whose data is in the registers below
+  double ptx = 0, pty = 0;
+  uint8_t pwas = 0;
+  int4 pq4 = make_int4(0, 0, 0, 0);
+  int pnc = 0;
+  double2 pc0{}, pc1{}, pc2{}, pc3{};
+  auto load_node = [&](int t, double& x, double& y, uint8_t& was, int4& q4, int& nc, double2& c0, double2& c1,
+                       double2& c2, double2& c3) {
+    x = tg[2 * t];
+    y = tg[2 * t + 1];
+    was = vis[t];
+    q4 = *reinterpret_cast<const int4*>(nbr + 4 * t);
+    nc = cnt[t];
+    c0 = axy[4 * t];
+    c1 = axy[4 * t + 1];
+    c2 = axy[4 * t + 2];
+    c3 = axy[4 * t + 3];
+  };
   for (int i = tid; i < R; i += kCovThreads) {
     int c = cur[i];
     int ai = act ? act[i] : 0;
-    int4 offer = make_int4(0, 0, 0, 0);
-    if (act && !dirty) offer = *reinterpret_cast<const int4*>(snd + base + 4 * i);
+    // the 4 action targets offered at the robot's node: the tail of the last observation
+    // (read whether or not the env is dirty, so it is not a dependent load)
+    const int4 offer = act ? *reinterpret_cast<const int4*>(snd + base + 4 * i) : make_int4(0, 0, 0, 0);
     if (dirty) {
+      // closest_targets (:427-432): the robots were placed externally
       const double px = xr[2 * i], py = xr[2 * i + 1];
       double best = __builtin_inf();
       c = 0;
@@ -183,16 +210,21 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       c += R;
     }
     cur_s[i] = c;
+    int n = c;
     if (act) {
       // step (:184-200): the node the action points at; robots that stay claim first
       if (ai < 0 || ai >= 4) {
         atomicOr(a.err, 4);
         ai = 0;
       }
-      const int n = dirty ? action_node(nbr, cnt, c, ai, R)
-                          : (ai == 0 ? offer.x : ai == 1 ? offer.y : ai == 2 ? offer.z : offer.w);
+      n = dirty ? action_node(nbr, cnt, c, ai, R)
+                : (ai == 0 ? offer.x : ai == 1 ? offer.y : ai == 2 ? offer.z : offer.w);
       chosen[i] = n;
       if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
+    }
+    if (one && (n != c || full)) {
+      pn = n;
+      load_node(n - R, ptx, pty, pwas, pq4, pnc, pc0, pc1, pc2, pc3);
     }
   }
   __syncthreads();
@@ -204,25 +236,89 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     // guesses (the first claimer of each node by atomicMin) until nothing changes. A
     // robot's outcome depends only on lower-indexed robots, so after k rounds robots
     // 0..k-1 are final, and the fixed point is the serial walk's unique result.
-    for (int i = tid; i < R; i += kCovThreads) new_s[i] = chosen[i];  // guess: every move succeeds
-    while (true) {
-      for (int k = tid; k < M; k += kCovThreads) first[k] = INT_MAX;
-      __syncthreads();
-      for (int i = tid; i < R; i += kCovThreads)
-        if (chosen[i] != cur_s[i]) atomicMin(&first[new_s[i]], i);  // a mover claims where it ends
-      __syncthreads();
-      int changed = 0;
-      for (int i = tid; i < R; i += kCovThreads) {
-        const int c = cur_s[i], n = chosen[i];
-        if (n == c) continue;
-        const bool ok = !(claim[n >> 5] & (1u << (n & 31))) && first[n] >= i;
-        const int v = ok ? n : c;
-        if (v != new_s[i]) {
-          new_s[i] = v;
-          changed = 1;
+    if (R <= 4 * 64) {
+      // One wave, up to 4 robots per lane kept in registers; only first[] is in LDS.
+      // A wave's LDS operations complete in order, so a round needs no workgroup
+      // barrier, only waits for its own LDS operations.
+      if (tid < 64) {
+        // wait for this wave's LDS operations only (a fence would also wait for the
+        // node prefetch still in flight from global memory)
+        auto lds_fence = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+        // four named robots, not an array: an array indexed in a loop stays in scratch
+        struct Rb {
+          int i, c, n, v;
+          bool mv, fr;
+        };
+        auto init = [&](Rb& r, int i) {
+          r.i = i;
+          const bool valid = i < R;
+          r.c = valid ? cur_s[i] : 0;
+          r.n = valid ? chosen[i] : 0;
+          r.mv = valid && r.n != r.c;
+          r.fr = r.mv && !(claim[r.n >> 5] & (1u << (r.n & 31)));  // not a stayer's node
+          r.v = r.n;  // guess: every move succeeds
+        };
+        // branch-free rounds: a robot that does not move adds INT_MAX (no-op) and clears
+        // its own node, which no mover's test reads (movers onto it are blocked by its
+        // stay claim; robots past R sit on node 0, a robot slot no target uses)
+        auto put = [&](const Rb& r) { atomicMin(&first[r.v], r.mv ? r.i : INT_MAX); };
+        auto eval = [&](Rb& r, int f) {
+          const int v = (r.fr && f >= r.i) ? r.n : r.c;  // r.fr implies r.mv
+          const bool ch = v != r.v;
+          r.v = v;
+          return ch;
+        };
+        auto clear = [&](const Rb& r) {  // a mover's claim sits on its chosen node or its own
+          first[r.n] = INT_MAX;
+          first[r.c] = INT_MAX;
+        };
+        Rb r0, r1, r2, r3;
+        init(r0, tid);
+        init(r1, tid + 64);
+        init(r2, tid + 128);
+        init(r3, tid + 192);
+        while (true) {
+          put(r0), put(r1), put(r2), put(r3);
+          lds_fence();
+          const int f0 = first[r0.n], f1 = first[r1.n], f2 = first[r2.n], f3 = first[r3.n];
+          // all four evaluated (no short circuit)
+          const int changed = int(eval(r0, f0)) | int(eval(r1, f1)) | int(eval(r2, f2)) | int(eval(r3, f3));
+          if (!__any(changed)) break;
+          lds_fence();
+          clear(r0), clear(r1), clear(r2), clear(r3);
+          lds_fence();
         }
+        if (r0.i < R) new_s[r0.i] = r0.v;
+        if (r1.i < R) new_s[r1.i] = r1.v;
+        if (r2.i < R) new_s[r2.i] = r2.v;
+        if (r3.i < R) new_s[r3.i] = r3.v;
       }
-      if (!__syncthreads_or(changed)) break;
+      __syncthreads();
+    } else {
+      for (int i = tid; i < R; i += kCovThreads) new_s[i] = chosen[i];  // guess: every move succeeds
+      while (true) {
+        __syncthreads();
+        for (int i = tid; i < R; i += kCovThreads)
+          if (chosen[i] != cur_s[i]) atomicMin(&first[new_s[i]], i);
+        __syncthreads();
+        int changed = 0;
+        for (int i = tid; i < R; i += kCovThreads) {
+          const int c = cur_s[i], n = chosen[i];
+          if (n == c) continue;
+          const bool ok = !(claim[n >> 5] & (1u << (n & 31))) && first[n] >= i;
+          const int v = ok ? n : c;
+          if (v != new_s[i]) {
+            new_s[i] = v;
+            changed = 1;
+          }
+        }
+        if (!__syncthreads_or(changed)) break;
+        for (int i = tid; i < R; i += kCovThreads)
+          if (chosen[i] != cur_s[i]) {
+            first[chosen[i]] = INT_MAX;
+            first[cur_s[i]] = INT_MAX;
+          }
+      }
     }
   } else {
     for (int i = tid; i < R; i += kCovThreads) new_s[i] = cur_s[i];
@@ -237,22 +333,22 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     const bool moved = n != cur_s[i];
     cur[i] = n;
     if (!moved && !full) continue;  // same node, same position: its edges stand
-    // one round trip: position, visited flag, action targets and their coordinates
     double px, py;
-    if (moved) {  // a robot that does not move keeps its position (:198)
-      px = tg[2 * t];
-      py = tg[2 * t + 1];
-    } else {
-      px = xr[2 * i];
-      py = xr[2 * i + 1];
+    uint8_t was;
+    int4 q4;
+    int nc;
+    double2 c0, c1, c2, c3;
+    if (n == pn) {
+      px = ptx, py = pty, was = pwas, q4 = pq4, nc = pnc, c0 = pc0, c1 = pc1, c2 = pc2, c3 = pc3;
+    } else {  // R > kCovThreads, or a blocked robot in a full pass
+      load_node(t, px, py, was, q4, nc, c0, c1, c2, c3);
     }
-    const uint8_t was = vis[t];
-    const int4 q4 = *reinterpret_cast<const int4*>(nbr + 4 * t);
-    const int nc = cnt[t];
-    const double2 c0 = axy[4 * t], c1 = axy[4 * t + 1], c2 = axy[4 * t + 2], c3 = axy[4 * t + 3];
     if (moved) {
       xr[2 * i] = px;
       xr[2 * i + 1] = py;
+    } else {  // a robot that does not move keeps its position (:198)
+      px = xr[2 * i];
+      py = xr[2 * i + 1];
     }
     if (!was) {
       const unsigned old = atomicOr(&seen[n >> 5], 1u << (n & 31));
@@ -280,13 +376,12 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   __syncthreads();
   if (tid == 0) {
     const int newly = *counter;
-    const int nv = a.nvisited[b] + newly;
+    const int nv = nv0 + newly;
     a.nvisited[b] = nv;
-    const int sc = a.step_counter[b];
-    a.obs_step[b] = sc;
-    a.step_counter[b] = sc + 1;
+    a.obs_step[b] = sc0;
+    a.step_counter[b] = sc0 + 1;
     a.reward[b] = static_cast<double>(newly);
-    a.done[b] = (sc + 1 == a.episode_length || nv == T) ? 1 : 0;
+    a.done[b] = (sc0 + 1 == a.episode_length || nv == T) ? 1 : 0;
     a.dirty[b] = 0;
   }
 }

@@ -177,3 +177,28 @@ def test_env_get_action_edges_and_unpack_state():
     np.testing.assert_array_equal(out[2][:, 3:], state[:, :2])
     np.testing.assert_array_equal(out[3][:, 3:], state[:, 2:])
     env.close()
+
+
+@pytest.mark.parametrize("R", [64, 255, 256, 300])
+def test_crowded_grid_claims_vs_oracle(R):
+    """Dense robots on a 25x25 grid (long claim chains), at the one-wave claim path's
+    limits (R = 64, 255, 256 robots: up to 4 per lane) and past them (R = 300 takes the
+    multi-wave path); 25 random steps against the oracle."""
+    xs, ys = np.meshgrid(np.arange(25) * 5.5, np.arange(25) * 5.5)
+    targets = np.stack([ys.ravel(), xs.ravel()], axis=1)
+    M = 1300
+    h = nat.CoverageHandle(R, 1, M)
+    h.set_targets(targets, env=0)
+    o = oc.CoverageOracle(targets, R, M)
+    rs = np.random.RandomState(R)
+    start = rs.choice(len(targets), R, replace=False)
+    h.reset(start[None], np.zeros((1, M - R), np.uint8))
+    o.reset(start, np.arange(len(targets)) + R)
+    for t in range(25):
+        a = rs.randint(0, 4, size=R)
+        h.step(a[None])
+        obs, rr, dd = o.step(a)
+        assert_obs(h.obs(0), {k + "0": val for k, val in obs.items()})
+        np.testing.assert_array_equal(h.robots(0)[1], o.closest())
+        assert h.rewards()[0][0] == rr
+    h.close()
