@@ -18,11 +18,12 @@ x0 = synthetic_batch(B, N)
 u = np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
 alg = B * (4 * N * N + 96 * N + 8)
 
-configs = {}
+configs, extra = {}, {}
 for spec in sys.argv[1:] or ["tiled:GYMFLOCK_FRONT=0", "front:GYMFLOCK_FRONT=1"]:
     name, _, kv = spec.partition(":")
     env = dict(p.split("=") for p in kv.split(",") if p)
     diag = int(env.pop("diag", 0))
+    extra[name] = int(env.pop("flags", "0"), 0)  # extra fe_step flags, e.g. 0x20 = FE_NO_NETWORK
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     h = nat.FlockHandle(N, B)
@@ -43,10 +44,10 @@ for r in range(ROUNDS):
     for c, h in configs.items():
         for f, flags in flags_list.items():
             h.set_state(x0)
-            h.step(None, flags)
+            h.step(None, flags | extra[c])
             h.timing_start()
             for _ in range(STEPS):
-                h.step(None, flags)
+                h.step(None, flags | extra[c])
             ms, n = h.timing_stop()
             res[(c, f)].append(ms)
 for (c, f), v in res.items():

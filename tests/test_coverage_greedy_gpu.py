@@ -209,3 +209,18 @@ def test_greedy_resident_actions_and_external_positions():
         o.step(ea)
         np.testing.assert_array_equal(h.robots(0)[1], o.closest())
     h.close()
+
+
+def test_mixed_width_batch_greedy_vs_oracle():
+    """One batch with a 33x33 grid (1089 targets, more than one 512-target sweep of the
+    row scan) and the 300-target line (hop counts past 254: the uint16 rerun), greedy
+    against the oracle."""
+    xs, ys = np.meshgrid(np.arange(33) * 5.5, np.arange(33) * 5.5)
+    grid = np.stack([xs.ravel(), ys.ravel()], axis=1)
+    maps = [grid, _line()]
+    R, M = 8, 1100
+    v = VecCoverage(2, R, max_nodes=M)
+    for b in range(2):
+        v.set_targets(maps[b], env=b)
+    _greedy_phase(v, maps, R, M, seed=5, steps=15)
+    v.close()
