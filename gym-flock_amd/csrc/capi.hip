@@ -71,6 +71,10 @@ struct fe_handle {
   // kernel timing (bench roofline)
   int diag = 0;                         // ablation switches for every step launch
   int lds_pad = 0;                      // occupancy tuning (GYMFLOCK_LDS_PAD)
+  int split = 0;                        // split-phase step kernel (opt-in GYMFLOCK_SPLIT=1; slower)
+  int T_split = 512;                    // its phase-B tile (GYMFLOCK_SPLIT_TILE)
+  int store_fast[2] = {0, 1};           // fast network store loop, plain step / with controller
+                                        // (GYMFLOCK_STORE_FAST=<plain><ctrl>, e.g. "01")
   bool timing = false;
   int timing_stride = 1;                // sample every timing_stride-th launch
   int64_t timing_count = 0;
@@ -200,6 +204,8 @@ gf::StepArgs base_args(fe_handle* h) {
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
   a.lds_pad = h->lds_pad;
+  a.split = h->split && h->cfg.n_agents <= gf::kSplitMax;
+  if (a.split) a.T = h->T_split;
   a.u_scale = h->cfg.action_scalar;
   a.us_f = a.as_f;
   a.x_scale = 1.0;
@@ -221,7 +227,9 @@ gf::StepArgs base_args(fe_handle* h) {
   return a;
 }
 
-int timed_launch(fe_handle* h, const gf::StepArgs& a, bool dyn, bool uf64, bool ctrl) {
+int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
+  gf::StepArgs a = a_in;
+  a.store_fast = h->store_fast[ctrl ? 1 : 0];
   // a sampled launch is bracketed by two events (which also keep it from overlapping
   // its neighbours, so sampling every launch costs the stream ~7 us per step)
   const bool sample = h->timing && (h->timing_count++ % h->timing_stride) == 0;
@@ -319,6 +327,20 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     gf::step_resident_geometry(cfg->n_agents, cfg->n_envs, target, &h->spe, &h->rps);
   }
   if (const char* e = getenv("GYMFLOCK_LDS_PAD")) h->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
+  if (const char* e = getenv("GYMFLOCK_SPLIT")) h->split = atoi(e) != 0;
+  {
+    const int full = ((cfg->n_agents + 63) / 64) * 64;
+    int t = 512;
+    if (const char* e = getenv("GYMFLOCK_SPLIT_TILE")) {
+      const int v = atoi(e);
+      if (v >= 64 && v <= gf::kTileMax && v % 64 == 0) t = v;
+    }
+    h->T_split = t < full ? t : full;
+  }
+  if (const char* e = getenv("GYMFLOCK_STORE_FAST")) {
+    if (e[0] == '0' || e[0] == '1') h->store_fast[0] = e[0] - '0';
+    if (e[0] && (e[1] == '0' || e[1] == '1')) h->store_fast[1] = e[1] - '0';
+  }
   if (const char* e = getenv("GYMFLOCK_TILE")) {
     const int t = atoi(e);
     if (t >= 64 && t <= gf::kTileMax && t % 64 == 0) {

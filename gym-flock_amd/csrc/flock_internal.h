@@ -10,7 +10,7 @@ constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float6
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
 constexpr int kResidentRows = 32;   // rows per block of the env-resident kernel
 constexpr int kResidentMax = 1024;  // largest N whose env fits the resident kernel's LDS
-constexpr size_t kStepLdsFloor = 32 * 1024;  // plain step: 5 workgroups per CU (tuning)
+constexpr int kSplitMax = 2048;     // largest N of the split-phase kernel (float32 env in LDS)
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many full-scan rows per workgroup
                                     // go wave-cooperative, more go one row per thread
@@ -35,10 +35,12 @@ struct StepArgs {
   int resident;           // 1: env-resident kernel (N <= kResidentMax)
   int spe, rps;           // resident kernel: slices per env, rows per slice
   int lds_pad;            // extra dynamic LDS bytes (occupancy control; tuning knob)
+  int split;              // 1: split-phase kernel (N <= kSplitMax, see flock_step_split_kernel)
+  int store_fast;         // network rows by the fast bit-extract loop (N % 1024 == 0)
   int diag;               // ablation switches (0 in production): 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
                           // unwritten: timing only), 16 skip tile loads (timing only),
-                          // 32 plain blockIdx workgroup order (A/B; default groups an env on one XCD)
+                          // 64 / 128 generic / fast network store loop (A/B)
   // Flocking variants (flocking_leader/obstacle/stoch.py). variant == 0 keeps the
   // FlockingRelative path untouched; otherwise the fields below apply (tiled kernel).
   int variant;
@@ -76,6 +78,7 @@ struct StatsArgs {
 int step_rows_per_block(int N);
 int step_tile(int N);
 size_t step_lds_bytes(int N, int R, int T, bool ctrl);
+size_t split_lds_bytes(int N, int R, int T, bool ctrl);
 size_t step_resident_lds_bytes(int N, bool ctrl);
 void step_resident_geometry(int N, int B, int target_wgs, int* spe, int* rps);
 

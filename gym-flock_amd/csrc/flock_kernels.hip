@@ -218,12 +218,191 @@ __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m,
   w1 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m >> 32), l, static_cast<int>(w1)));
 }
 
+// Split-phase kernel LDS: one region that holds the env's float32 positions in phase A
+// and a float64 tile of T agents in phase B, then the adjacency (and controller) bits.
+__host__ __device__ inline size_t split_region_bytes(int N, int T) {
+  const size_t p = (size_t)N * 8, t = (size_t)T * sizeof(St);
+  return ((p > t ? p : t) + 15) & ~static_cast<size_t>(15);
+}
+
+// Dense network rows adj/deg of one row block (flocking_relative.py:120-122), 16-byte
+// stores (1 KiB per wave instruction); the block's rows are one contiguous range
+// starting at global row grow0.
+__device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint64_t* adj, const float* inv,
+                                                   int Wn, size_t grow0, int nrows, int wid, int lane) {
+  const int N = a.N;
+  const bool vec4 = (N & 3) == 0;
+  // wave w writes the contiguous rows [w*R/4, (w+1)*R/4): the 4 waves' concurrent
+  // stores land R/4 rows apart (212 vs 215 us with rows w, w+4, ... at config 2)
+  const int per = (nrows + 3) >> 2;
+  // fast form (N % 1024 == 0): every lane owns float4 columns lane + 64m of a row, so
+  // its nibble sits at a fixed bit offset of 32-bit words 8 apart; four words are read
+  // ahead and each float becomes sign-extended bit & bits(1/deg) (2 VALU per float).
+  // The host picks it per kernel (StepArgs.store_fast; diag 64 / 128 force it off / on).
+  const bool fast = (N & 1023) == 0 && !(a.diag & (4 | 64)) && (a.store_fast || (a.diag & 128));
+  const unsigned* bits32 = reinterpret_cast<const unsigned*>(adj);
+  const int hl = lane & 15;
+  const int wsel = 2 * (lane >> 4) + (hl >> 3);  // 32-bit word of column block m = 0
+  const int o0 = (hl & 7) << 2;                  // bit offset of this lane's nibble
+  for (int m = 0; m < per; ++m) {
+    const int r = wid * per + m;
+    if (r >= nrows) break;
+    const float iv = inv[r];
+    const uint64_t* bits = adj + (size_t)r * Wn;
+    float* rowp = a.network + (grow0 + r) * (size_t)N;
+    if (fast) {
+      const int ivb = __float_as_int(iv);
+      const unsigned* wr = bits32 + (size_t)r * 2 * Wn + wsel;
+      f4v* dst = reinterpret_cast<f4v*>(rowp) + lane;
+#pragma unroll 1
+      for (int c = 0; c < (N >> 8); c += 4) {
+        int w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = static_cast<int>(wr[8 * (c + k)]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f4v v = {__int_as_float(__builtin_amdgcn_sbfe(w[k], o0, 1) & ivb),
+                         __int_as_float(__builtin_amdgcn_sbfe(w[k], o0 + 1, 1) & ivb),
+                         __int_as_float(__builtin_amdgcn_sbfe(w[k], o0 + 2, 1) & ivb),
+                         __int_as_float(__builtin_amdgcn_sbfe(w[k], o0 + 3, 1) & ivb)};
+          dst[64 * (c + k)] = v;
+        }
+      }
+    } else if (vec4) {
+      f4v* r4 = reinterpret_cast<f4v*>(rowp);
+      const int nq = N >> 2;
+      for (int q = lane; q < nq; q += 64) {
+        const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
+        const f4v v = {(nib & 1u) ? iv : 0.0f, (nib & 2u) ? iv : 0.0f, (nib & 4u) ? iv : 0.0f,
+                       (nib & 8u) ? iv : 0.0f};
+        if (a.diag & 4)
+          __builtin_nontemporal_store(v, &r4[q]);
+        else
+          r4[q] = v;
+      }
+    } else {
+      for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
+    }
+  }
+}
+
+// Per-row outputs of a row block once its features are summed: the S slices of each
+// row combined, state_values (:124-129), the updated state, the controller (:194-226)
+// and, by the env's first block, the reward (instant_cost :145-147). `writer` = the
+// thread holding slice 0 of a valid row.
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
+__device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile, double* red, const St& me,
+                                              double f0, double f1, double f2, double f3, double f4,
+                                              double f5, double gx, double gy, double svx, double svy, int b,
+                                              int i0, int i_row, bool writer, int S, int tid) {
+  const int N = a.N, T = a.T;
+  const size_t env0 = (size_t)b * N;
+  // combine the S slices of each row (xor butterfly: identical bits in every lane)
+  for (int o = 1; o < S; o <<= 1) {
+    f0 += __shfl_xor(f0, o);
+    f1 += __shfl_xor(f1, o);
+    f2 += __shfl_xor(f2, o);
+    f3 += __shfl_xor(f3, o);
+    f4 += __shfl_xor(f4, o);
+    f5 += __shfl_xor(f5, o);
+    if constexpr (CTRL) {
+      gx += __shfl_xor(gx, o);
+      gy += __shfl_xor(gy, o);
+    }
+  }
+
+  const double Svx = block_sum(svx, red);
+  const double Svy = block_sum(svy, red);
+
+  if (writer) {
+    const size_t g = env0 + i_row;
+    if (a.state_values) {
+      float* sv = a.state_values + g * 6;
+      sv[0] = static_cast<float>(f0);
+      sv[1] = static_cast<float>(f1);
+      sv[2] = static_cast<float>(f2);
+      sv[3] = static_cast<float>(f3);
+      sv[4] = static_cast<float>(f4);
+      sv[5] = static_cast<float>(f5);
+    }
+    if constexpr (DYN) {
+      double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
+      xo[0] = double2{me.px, me.py};
+      xo[1] = double2{me.vx, me.vy};
+    }
+    if constexpr (CTRL) {
+      // centralized: sum over ALL j of (v_i - v_j) = N*v_i - sum_j v_j (:200-208)
+      double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
+      double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
+      if (VAR && a.centralized && a.n_vel_zero > 0) {
+        // obstacle variant: only pairs between free agents count (flocking_obstacle.py:79-80)
+        const int nz = min(a.n_vel_zero, N);
+        double zx = 0, zy = 0;
+        for (int j = 0; j < nz; ++j) {
+          const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
+          zx += s.vx;
+          zy += s.vy;
+        }
+        const bool frozen = i_row < nz;
+        p2 = frozen ? 0.0 : static_cast<double>(N - nz) * me.vx - (Svx - zx);
+        p3 = frozen ? 0.0 : static_cast<double>(N - nz) * me.vy - (Svy - zy);
+      }
+      double2 u;
+      u.x = clip10(-gx - p2) / a.action_scalar;  // (-p4 - p2), :209-211
+      u.y = clip10(-p3 - gy) / a.action_scalar;  // (-p3 - p5)
+      if (VAR && a.ctrl_clip > 0) {  // stochastic variant (flocking_stoch.py:44-45)
+        u.x = clip_sym(u.x, a.ctrl_clip);
+        u.y = clip_sym(u.y, a.ctrl_clip);
+      }
+      reinterpret_cast<double2*>(a.ctrl_out)[g] = u;
+    }
+  }
+
+  // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
+  // first row block; single-tile envs read the velocities from the LDS tile
+  if (a.reward && i0 == 0) {
+    const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
+    double qx = 0, qy = 0;
+    if (N <= T) {
+      for (int t = tid; t < N; t += kThreads) {
+        const double ex = tile[t].vx - mx, ey = tile[t].vy - my;
+        qx += ex * ex;
+        qy += ey * ey;
+      }
+    } else {
+      for (int j = tid; j < N; j += kThreads) {
+        const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
+        const double ex = s.vx - mx, ey = s.vy - my;
+        qx += ex * ex;
+        qy += ey * ey;
+      }
+    }
+    const double Qx = block_sum(qx, red);
+    const double Qy = block_sum(qy, red);
+    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // The fused step: DYN = apply dynamics (step) or not (compute_helpers on the current
 // state: reset / standalone controller), UF64 = action dtype, CTRL = also controller().
 #ifndef GF_STEP_MIN_WAVES
 #define GF_STEP_MIN_WAVES 1
 #endif
+// Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
+// wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
+// its HW_ID / XCC_ID, for scripts/phase_timeline.py. Product builds compile it out.
+#ifdef GF_STAMPS
+__device__ unsigned long long gf_stamp_buf[8192 * 16];
+#define GF_STAMP(k)                                                                     \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                          \
+      gf_stamp_buf[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();           \
+  } while (0)
+#else
+#define GF_STAMP(k) ((void)0)
+#endif
+
 // VAR: the flocking variants' switches (StepArgs.variant); without it the FlockingRelative
 // path carries none of their instructions.
 template <bool DYN, bool UF64, bool CTRL, bool VAR>
@@ -248,6 +427,14 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const size_t env0 = (size_t)b * N;
+  GF_STAMP(0);
+#ifdef GF_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    gf_stamp_buf[blockIdx.x * 16 + 15] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+  }
+#endif
 
   // rows owned by this workgroup (post-update state)
   for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
@@ -312,6 +499,8 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   for (int j0 = 0; j0 < N; j0 += T) {
     const int tc = min(T, N - j0);
     __syncthreads();  // previous tile fully consumed; rows[] visible on first pass
+    [[maybe_unused]] const int ti = j0 / T;
+    if (ti == 0) GF_STAMP(1);
     float pt = 0.f;
     for (int t = (a.diag & 16) ? tc : tid; t < tc; t += kThreads) {
       const St s = load_state<DYN, UF64, VAR>(a, env0 + j0 + t);
@@ -332,6 +521,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
     }
     const float Pt = block_max(pt, redf);  // also the barrier that publishes the tile
+    if (ti < 2) GF_STAMP(2 + 3 * ti);
 
     // pass 1: adjacency (and controller "near") bits. A wave takes 128 columns (lane
     // j and j+64, packed float32 math) and loops over the block's rows; the compare
@@ -423,10 +613,14 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       }
     }
     __syncthreads();
+    if (ti < 2) GF_STAMP(3 + 3 * ti);
 
     // pass 2 (features) of every tile but the last runs here; the last tile's runs
     // after the network stores are issued, so the stores drain under it.
-    if (j0 + T < N) feature_pass(j0, nch);
+    if (j0 + T < N) {
+      feature_pass(j0, nch);
+      if (ti < 1) GF_STAMP(4);
+    }
   }
   const int jl = ((N - 1) / T) * T;  // first column of the last tile (still in LDS)
   const int nchl = (N - jl + 63) >> 6;
@@ -451,124 +645,261 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
     for (int k = tid; k < nrows * Wn; k += kThreads) dst[k] = adj[k];
   }
   __syncthreads();
+  GF_STAMP(7);
 
-  // pass 3: dense network rows adj/deg, 16-byte stores (1 KiB per wave instruction);
-  // the block's R rows are one contiguous R*N*4-byte range
-  if (a.network) {
-    const bool vec4 = (N & 3) == 0;
-    // wave w writes the contiguous rows [w*R/4, (w+1)*R/4): the 4 waves' concurrent
-    // stores land R/4 rows apart (212 vs 215 us with rows w, w+4, ... at config 2)
-    const int per = (nrows + 3) >> 2;
-    for (int m = 0; m < per; ++m) {
-      const int r = wid * per + m;
-      if (r >= nrows) break;
-      const float iv = inv[r];
-      const uint64_t* bits = adj + (size_t)r * Wn;
-      float* rowp = a.network + (env0 + i0 + r) * (size_t)N;
-      if (vec4) {
-        f4v* r4 = reinterpret_cast<f4v*>(rowp);
-        const int nq = N >> 2;
-        for (int q = lane; q < nq; q += 64) {
-          const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
-          const f4v v = {(nib & 1u) ? iv : 0.0f, (nib & 2u) ? iv : 0.0f, (nib & 4u) ? iv : 0.0f,
-                         (nib & 8u) ? iv : 0.0f};
-          if (a.diag & 4)
-            __builtin_nontemporal_store(v, &r4[q]);
-          else
-            r4[q] = v;
-        }
-      } else {
-        for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
-      }
-    }
-  }
+  if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
 
+  GF_STAMP(8);
   feature_pass(jl, nchl);
+  GF_STAMP(9);
 
-  // combine the S slices of each row (xor butterfly: identical bits in every lane)
-  for (int o = 1; o < S; o <<= 1) {
-    f0 += __shfl_xor(f0, o);
-    f1 += __shfl_xor(f1, o);
-    f2 += __shfl_xor(f2, o);
-    f3 += __shfl_xor(f3, o);
-    f4 += __shfl_xor(f4, o);
-    f5 += __shfl_xor(f5, o);
-    if constexpr (CTRL) {
-      gx += __shfl_xor(gx, o);
-      gy += __shfl_xor(gy, o);
-    }
+  step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
+                                      frow && fs == 0, S, tid);
+  GF_STAMP(10);
+#if defined(GF_STAMPS) && GF_STAMPS >= 2
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GF_STAMP(11);
+#endif
+}
+
+// ---------------------------------------------------------------------------------
+// Split-phase form of the same step (N <= kSplitMax): everything the network rows need
+// comes first and everything else after their stores are issued.
+//   A: the env's float32 positions (one load round trip, the rows included), pass 1
+//      over every column, degrees, the network stores;
+//   B: float64 tiles of the env over the same LDS (the positions are dead by then), the
+//      feature / controller pass, the per-row outputs and the reward.
+// A workgroup thus reaches its stores after one load and one bit pass instead of three
+// dependent loads and two bit passes with a feature pass between them; its phase-B loads
+// queue behind its own stores, which is time its stores drain anyway. Same numerics as
+// flock_step_kernel (float32 prefilter + float64 band decisions, float64 features in
+// ascending column order per slice).
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
+__global__ __launch_bounds__(kThreads) void flock_step_split_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, R = a.R, T = a.T;
+  const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
+  const size_t region = split_region_bytes(N, T);
+  float2* pos32 = reinterpret_cast<float2*>(smem);              // A: float32 positions, N
+  St* tile = reinterpret_cast<St*>(smem);                       // B: float64 state, T
+  uint64_t* adj = reinterpret_cast<uint64_t*>(smem + region);   // R x Wn adjacency bits
+  uint64_t* nearb = adj + (size_t)R * Wn;                       // R x Wn controller bits
+  double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)R * Wn : 0));
+  float* redf = reinterpret_cast<float*>(red + 4);
+  float* inv = reinterpret_cast<float*>(red + 8);
+
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = L / a.bpe;
+  const int i0 = (L - b * a.bpe) * R;
+  const int nrows = min(R, N - i0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const size_t env0 = (size_t)b * N;
+  GF_STAMP(0);
+#ifdef GF_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    gf_stamp_buf[blockIdx.x * 16 + 15] = (static_cast<unsigned long long>(xcc) << 32) | hw;
   }
+#endif
 
-  const double Svx = block_sum(svx, red);
-  const double Svy = block_sum(svy, red);
+  // ---- phase A: positions of the whole env, float32 (post-update state)
+  float pt = 0.f;
+  for (int t = (a.diag & 16) ? N : tid; t < N; t += kThreads) {
+    const St s = load_state<DYN, UF64, VAR>(a, env0 + t);
+    const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
+    pos32[t] = make_float2(fx, fy);
+    pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
+  }
+  const float Pt = block_max(pt, redf);  // also the barrier that publishes pos32
+  GF_STAMP(2);
+  float rx32 = 0.f, ry32 = 0.f;  // lane r: row r's float32 position
+  if (lane < nrows) {
+    const float2 p = pos32[i0 + lane];
+    rx32 = p.x;
+    ry32 = p.y;
+  }
+  const float Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
 
-  if (frow && fs == 0) {
-    const size_t g = env0 + i0 + fr;
-    if (a.state_values) {
-      float* sv = a.state_values + g * 6;
-      sv[0] = static_cast<float>(f0);
-      sv[1] = static_cast<float>(f1);
-      sv[2] = static_cast<float>(f2);
-      sv[3] = static_cast<float>(f3);
-      sv[4] = static_cast<float>(f4);
-      sv[5] = static_cast<float>(f5);
+  // pass 1 over every column of the env (flock_step_kernel's pass 1 with j0 = 0)
+  const int npair = (Wn + 1) >> 1;
+  const float pu = uniform_f(Pr) + uniform_f(Pt);
+  Band ba{-__builtin_inff(), __builtin_inff()}, bn = ba;  // huge/non-finite: all exact
+  if (pu < 1.0e5f) {
+    const double delta = ldexp(static_cast<double>(pu) * (1.0 + 1e-6) + 4.0, -20);
+    ba = make_band(a.cr2, delta);
+    bn = make_band(a.cr, delta);
+  }
+  ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
+  bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
+  for (int cp = (a.diag & 8) ? npair : wid; cp < npair; cp += 4) {
+    const int ca = cp << 1;
+    const bool has_b = ca + 1 < Wn;
+    const int jta = (ca << 6) + lane, jtb = jta + 64;
+    const bool va = jta < N, vb = jtb < N;
+    // columns past the env sit far away: never adjacent, never in the band
+    const float2 qa = va ? pos32[jta] : make_float2(1.0e18f, 1.0e18f);
+    const float2 qb = vb ? pos32[jtb] : make_float2(1.0e18f, 1.0e18f);
+    const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
+    unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
+    uint64_t band = 0;
+    for (int r = 0; r < nrows; ++r) {
+      const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+      const f2v dx = xi - qx, dy = yi - qy;
+      const f2v d2 = dx * dx + dy * dy;
+      const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+      const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+      band |= (Aa ^ Ma) | (Ab ^ Mb);
+      put_lane(wa0, wa1, Aa, r);
+      put_lane(wb0, wb1, Ab, r);
+      if constexpr (CTRL) {
+        const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+        const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+        band |= (Na ^ NMa) | (Nb ^ NMb);
+        put_lane(na0, na1, Na, r);
+        put_lane(nb0, nb1, Nb, r);
+      }
     }
-    if constexpr (DYN) {
-      double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
-      xo[0] = double2{me.px, me.py};
-      xo[1] = double2{me.vx, me.vy};
-    }
-    if constexpr (CTRL) {
-      // centralized: sum over ALL j of (v_i - v_j) = N*v_i - sum_j v_j (:200-208)
-      double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
-      double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
-      if (VAR && a.centralized && a.n_vel_zero > 0) {
-        // obstacle variant: only pairs between free agents count (flocking_obstacle.py:79-80)
-        const int nz = min(a.n_vel_zero, N);
-        double zx = 0, zy = 0;
-        for (int j = 0; j < nz; ++j) {
-          const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
-          zx += s.vx;
-          zy += s.vy;
+    if (band) {  // rare: some pair is within the float32 error band of a threshold;
+                 // the float64 states come from global memory (L2) here
+      const St oa = va ? load_state<DYN, UF64, VAR>(a, env0 + jta) : St{1.0e300, 1.0e300, 0, 0};
+      const St ob = vb ? load_state<DYN, UF64, VAR>(a, env0 + jtb) : St{1.0e300, 1.0e300, 0, 0};
+      for (int r = 0; r < nrows; ++r) {
+        const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+        const f2v dx = xi - qx, dy = yi - qy;
+        const f2v d2 = dx * dx + dy * dy;
+        const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+        const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+        uint64_t Na = 0, Nb = 0, NMa = 0, NMb = 0;
+        if constexpr (CTRL) {
+          Na = __ballot(d2.x <= bn.lo);
+          Nb = __ballot(d2.y <= bn.lo);
+          NMa = __ballot(!(d2.x > bn.hi));
+          NMb = __ballot(!(d2.y > bn.hi));
         }
-        const bool frozen = i_row < nz;
-        p2 = frozen ? 0.0 : static_cast<double>(N - nz) * me.vx - (Svx - zx);
-        p3 = frozen ? 0.0 : static_cast<double>(N - nz) * me.vy - (Svy - zy);
+        if ((Aa ^ Ma) | (Ab ^ Mb) | (Na ^ NMa) | (Nb ^ NMb)) {
+          const St ri = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
+          const double dxa = ri.px - oa.px, dya = ri.py - oa.py;
+          const double dxb = ri.px - ob.px, dyb = ri.py - ob.py;
+          const double r2a = dxa * dxa + dya * dya, r2b = dxb * dxb + dyb * dyb;
+          put_lane(wa0, wa1, Aa | (__ballot(r2a < a.cr2) & (Aa ^ Ma)), r);
+          put_lane(wb0, wb1, Ab | (__ballot(r2b < a.cr2) & (Ab ^ Mb)), r);
+          if constexpr (CTRL) {
+            put_lane(na0, na1, Na | (__ballot(r2a <= a.cr) & (Na ^ NMa)), r);
+            put_lane(nb0, nb1, Nb | (__ballot(r2b <= a.cr) & (Nb ^ NMb)), r);
+          }
+        }
       }
-      double2 u;
-      u.x = clip10(-gx - p2) / a.action_scalar;  // (-p4 - p2), :209-211
-      u.y = clip10(-p3 - gy) / a.action_scalar;  // (-p3 - p5)
-      if (VAR && a.ctrl_clip > 0) {  // stochastic variant (flocking_stoch.py:44-45)
-        u.x = clip_sym(u.x, a.ctrl_clip);
-        u.y = clip_sym(u.y, a.ctrl_clip);
+    }
+    if (lane < nrows) {
+      // the diagonal (self, r2 = 0 here; inf in the reference) is never a neighbour
+      const int dl = i0 + lane - (ca << 6);
+      const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
+      const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
+      uint64_t* arow = adj + (size_t)lane * Wn + ca;
+      arow[0] = ((static_cast<uint64_t>(wa1) << 32) | wa0) & ka;
+      if (has_b) arow[1] = ((static_cast<uint64_t>(wb1) << 32) | wb0) & kb;
+      if constexpr (CTRL) {
+        uint64_t* nrow = nearb + (size_t)lane * Wn + ca;
+        nrow[0] = ((static_cast<uint64_t>(na1) << 32) | na0) & ka;
+        if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
       }
-      reinterpret_cast<double2*>(a.ctrl_out)[g] = u;
     }
   }
+  __syncthreads();
+  GF_STAMP(6);
 
-  // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
-  // first row block; single-tile envs read the velocities from the LDS tile
-  if (a.reward && i0 == 0) {
-    const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
-    double qx = 0, qy = 0;
-    if (N <= T) {
-      for (int t = tid; t < N; t += kThreads) {
-        const double ex = tile[t].vx - mx, ey = tile[t].vy - my;
-        qx += ex * ex;
-        qy += ey * ey;
-      }
-    } else {
-      for (int j = tid; j < N; j += kThreads) {
-        const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
-        const double ex = s.vx - mx, ey = s.vy - my;
-        qx += ex * ex;
-        qy += ey * ey;
+  // feature-pass thread mapping: S word-slices per row
+  const int S = kThreads / R;
+  const int fr = tid / S, fs = tid - fr * S;
+  const bool frow = fr < nrows;
+  // degree of each row -> 1/deg for the mean-pooled network (:120-122)
+  {
+    int deg = 0;
+    if (frow) {
+      const int wpt = (Wn + S - 1) / S;
+      const int wb = fs * wpt, we = min(Wn, wb + wpt);
+      for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
+    }
+    for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
+    if (frow && fs == 0) {
+      inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
+      if (a.degree_out) a.degree_out[env0 + i0 + fr] = deg;
+    }
+  }
+  if (a.adj_bits) {
+    uint64_t* dst = a.adj_bits + (env0 + i0) * (size_t)Wn;
+    for (int k = tid; k < nrows * Wn; k += kThreads) dst[k] = adj[k];
+  }
+  __syncthreads();
+  GF_STAMP(7);
+  if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
+  GF_STAMP(8);
+
+  // ---- phase B: float64 tiles over the region, features / gradients of set bits
+  double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
+  double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
+  const int i_row = i0 + fr;
+  const St me = frow ? load_state<DYN, UF64, VAR>(a, env0 + i_row) : St{0, 0, 0, 0};
+  for (int j0 = 0; j0 < N; j0 += T) {
+    const int tc = min(T, N - j0);
+    __syncthreads();  // pos32 / the previous tile fully consumed
+    for (int t = tid; t < tc; t += kThreads) {
+      const St s = load_state<DYN, UF64, VAR>(a, env0 + j0 + t);
+      tile[t] = s;
+      svx += s.vx;
+      svy += s.vy;
+    }
+    __syncthreads();
+    if (!frow || (a.diag & 2)) continue;
+    const int nch = (tc + 63) >> 6;
+    const int wpt = (nch + S - 1) / S;
+    const int wb = fs * wpt, we = min(nch, wb + wpt);
+    for (int w = wb; w < we; ++w) {
+      const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
+      const uint64_t nm = CTRL ? nearb[(size_t)fr * Wn + (j0 >> 6) + w] : 0ull;
+      uint64_t m = am | nm;
+      while (m) {
+        const int k = __builtin_ctzll(m);
+        m &= m - 1;
+        const int c = (w << 6) + k;
+        const bool isadj = (am >> k) & 1ull;
+        const St o = tile[c];
+        const double dx = me.px - o.px, dy = me.py - o.py;
+        const double r2 = dx * dx + dy * dy;
+        // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
+        // reference's two divisions; far inside the float32 outputs' tolerance)
+        const double ir = 1.0 / r2, irr = ir * ir;
+        const double q1x = dx * irr, q2x = dx * ir;
+        const double q1y = dy * irr, q2y = dy * ir;
+        if (isadj) {
+          // obstacle variant: no velocity difference for pairs touching agents < nvz
+          const bool vz = VAR && (i_row < a.n_vel_zero || j0 + c < a.n_vel_zero);
+          f0 += vz ? 0.0 : me.vx - o.vx;
+          f1 += q1x;
+          f2 += q2x;
+          f3 += vz ? 0.0 : me.vy - o.vy;
+          f4 += q1y;
+          f5 += q2y;
+        }
+        if constexpr (CTRL) {
+          if (((nm >> k) & 1ull) && (a.centralized || isadj)) {
+            gx += (-2.0 * q1x) + (2.0 * q2x);
+            gy += (-2.0 * q1y) + (2.0 * q2y);
+          }
+        }
       }
     }
-    const double Qx = block_sum(qx, red);
-    const double Qy = block_sum(qy, red);
-    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
   }
+  GF_STAMP(9);
+  step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
+                                      frow && fs == 0, S, tid);
+  GF_STAMP(10);
+#if defined(GF_STAMPS) && GF_STAMPS >= 2
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GF_STAMP(11);
+#endif
 }
 
 // ---------------------------------------------------------------------------------
@@ -1027,9 +1358,10 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
 
 // ----------------------------------------------------------------------------- host
 // Geometry measured on MI355X (scripts/ablate.py, N=1024 x 256 envs): 32-row blocks
-// with 512-agent LDS tiles keep ~5 workgroups per CU resident, which is what hides the
-// per-block load/compute latency under the network stores (fewer resident workgroups
-// were markedly slower).
+// with 512-agent LDS tiles (25.2 KiB of LDS, 77 VGPRs) keep 6 workgroups per CU
+// resident, which is what hides the per-block load/compute latency under the network
+// stores: 190 us at 6 per CU, 193 at 5, 211 at 4 (scripts/occprobe.hip measures what
+// fits: <= 26 KiB -> 6, 27-31 KiB -> 5, 32 KiB -> 4).
 int step_rows_per_block(int N) {
   const int words = (N + 63) / 64;
   int R = 32;
@@ -1049,6 +1381,12 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 + 15) / 16) * 16;
   return s;
+}
+
+size_t split_lds_bytes(int N, int R, int T, bool ctrl) {
+  const size_t Wn = (N + 63) / 64;
+  return split_region_bytes(N, T) + (size_t)R * Wn * 8 * (ctrl ? 2 : 1) + 8 * sizeof(double) +
+         (((size_t)R * 4 + 15) / 16) * 16;
 }
 
 size_t step_resident_lds_bytes(int N, bool ctrl) {
@@ -1081,12 +1419,24 @@ static hipError_t launch_step_resident_t(const StepArgs& a, hipStream_t s) {
 }
 
 template <bool DYN, bool UF64, bool CTRL, bool VAR>
+static hipError_t launch_step_split(const StepArgs& a, hipStream_t s) {
+  const size_t lds = split_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_split_kernel<DYN, UF64, CTRL, VAR>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int grid = a.B * a.bpe;
+  hipLaunchKernelGGL((flock_step_split_kernel<DYN, UF64, CTRL, VAR>), dim3(grid), dim3(kThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
+  if (a.split && a.N <= kSplitMax) return launch_step_split<DYN, UF64, CTRL, VAR>(a, s);
   size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
-  // the step without the controller runs best at 5 workgroups per CU (6 fit by
-  // registers: 218 vs 215 us at config 2); the controller's heavier feature pass wants
-  // every workgroup it can get, so only the plain step is held to 32 KiB of LDS
-  if (!CTRL && a.lds_pad == 0 && lds < kStepLdsFloor) lds = kStepLdsFloor;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR>),
@@ -1154,6 +1504,13 @@ hipError_t launch_fill(void* p, size_t bytes, bool nt, hipStream_t s) {
     hipLaunchKernelGGL(diag_fill_kernel<false>, dim3(grid), dim3(kThreads), 0, s, (f4v*)p, n4);
   return hipGetLastError();
 }
+
+#ifdef GF_STAMPS
+extern "C" __attribute__((visibility("default"))) int fe_diag_stamps(unsigned long long* dst, int n) {
+  if (n > 8192 * 16) n = 8192 * 16;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(gf_stamp_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
   const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
