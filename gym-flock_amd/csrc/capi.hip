@@ -743,8 +743,8 @@ int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches
 int fe_diag(fe_handle* h, int what, int reps, double* avg_ms) {
   if (!h || reps < 1) return fail(GF_EINVAL, "bad argument");
   if (int rc = use_dev(h)) return rc;
-  if (what >= 0x100) {  // set ablation switches for subsequent step launches
-    h->diag = what & 0xff;
+  if (what >= 0x10000) {  // set ablation switches (low 16 bits) for subsequent step launches
+    h->diag = what & 0xffff;
     return GF_OK;
   }
   hipEvent_t e0, e1;

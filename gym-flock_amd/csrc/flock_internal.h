@@ -40,7 +40,9 @@ struct StepArgs {
   int diag;               // ablation switches (0 in production): 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
                           // unwritten: timing only), 16 skip tile loads (timing only),
-                          // 64 / 128 generic / fast network store loop (A/B)
+                          // 64 / 128 generic / fast network store loop (A/B), 256 no
+                          // per-row outputs, 512 no reward, 1024 constant network rows
+                          // (timing only)
   // Flocking variants (flocking_leader/obstacle/stoch.py). variant == 0 keeps the
   // FlockingRelative path untouched; otherwise the fields below apply (tiled kernel).
   int variant;

@@ -250,6 +250,11 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
     const float iv = inv[r];
     const uint64_t* bits = adj + (size_t)r * Wn;
     float* rowp = a.network + (grow0 + r) * (size_t)N;
+    if (a.diag & 1024) {  // timing only: constant rows, no bit reads
+      f4v* r4 = reinterpret_cast<f4v*>(rowp);
+      for (int q = lane; q < (N >> 2); q += 64) r4[q] = f4v{iv, 0.f, iv, 0.f};
+      continue;
+    }
     if (fast) {
       const int ivb = __float_as_int(iv);
       const unsigned* wr = bits32 + (size_t)r * 2 * Wn + wsel;
@@ -314,7 +319,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
   const double Svx = block_sum(svx, red);
   const double Svy = block_sum(svy, red);
 
-  if (writer) {
+  if (writer && !(a.diag & 256)) {  // diag 256: skip the per-row outputs (timing only)
     const size_t g = env0 + i_row;
     if (a.state_values) {
       float* sv = a.state_values + g * 6;
@@ -360,7 +365,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 
   // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
   // first row block; single-tile envs read the velocities from the LDS tile
-  if (a.reward && i0 == 0) {
+  if (a.reward && i0 == 0 && !(a.diag & 512)) {  // diag 512: skip the reward (timing only)
     const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
     double qx = 0, qy = 0;
     if (N <= T) {

@@ -360,7 +360,7 @@ class FlockHandle:
         return ms.value
 
     def diag_switches(self, bits):
-        check(self.lib.fe_diag(self.h, 0x100 | int(bits), 1, None))
+        check(self.lib.fe_diag(self.h, 0x10000 | int(bits), 1, None))
 
     # -- RCCL metrics path
     @staticmethod

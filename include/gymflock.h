@@ -292,7 +292,8 @@ int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches
 int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launches);
 /* Diagnostics for roofline work: what = 0/1 times `reps` launches of a float4
  * plain/non-temporal fill of the network buffer (the write-bandwidth ceiling);
- * what = 0x100 | bits sets ablation switches on later step launches (0x100 clears). */
+ * what = 0x10000 | bits (16 bits) sets ablation switches on later step launches
+ * (0x10000 clears). */
 int fe_diag(fe_handle* h, int what, int reps, double* avg_ms);
 
 #ifdef __cplusplus
