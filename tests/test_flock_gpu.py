@@ -305,6 +305,41 @@ def test_env_resident_kernel_parity(monkeypatch):
         h.close()
 
 
+def test_split_kernel_parity(monkeypatch):
+    """The opt-in split-phase step kernel (GYMFLOCK_SPLIT=1: float32 env positions, pass 1
+    over every column, stores, then float64 tiles for the features) matches the oracle,
+    with and without the controller, on ragged and tile-spanning sizes."""
+    monkeypatch.setenv("GYMFLOCK_SPLIT", "1")
+    for n, B in ((100, 3), (1024, 2), (1030, 2), (2048, 1)):
+        x0 = synthetic_batch(B, n, seed0=11 * n)
+        u = np.random.RandomState(n + 1).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+        for ctrl in (False, True):
+            h = nat.FlockHandle(n, B)
+            h.set_state(x0)
+            h.step(u, nat.FE_WITH_CONTROLLER if ctrl else 0)
+            for b in range(B):
+                check_against_oracle(h, x0[b], u[b], b, ctrl=ctrl)
+            h.close()
+
+
+@pytest.mark.parametrize("mode", ["00", "11"])
+def test_network_store_loops(monkeypatch, mode):
+    """Both forms of the network store loop (generic nibble select, and the fast
+    bit-extract form used at N % 1024 == 0) write the oracle's rows, plain and with the
+    controller (GYMFLOCK_STORE_FAST=<plain><ctrl>)."""
+    monkeypatch.setenv("GYMFLOCK_STORE_FAST", mode)
+    n, B = 1024, 2
+    x0 = synthetic_batch(B, n, seed0=77)
+    u = np.random.RandomState(78).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    for ctrl in (False, True):
+        h = nat.FlockHandle(n, B)
+        h.set_state(x0)
+        h.step(u, nat.FE_WITH_CONTROLLER if ctrl else 0)
+        for b in range(B):
+            check_against_oracle(h, x0[b], u[b], b, ctrl=ctrl)
+        h.close()
+
+
 @pytest.mark.parametrize("n", [100, 1030])
 def test_packed_network_vs_oracle(n):
     """FE_PACKED_NETWORK: adjacency bits and degrees (the packed output mode) match the
