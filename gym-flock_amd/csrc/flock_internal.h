@@ -11,6 +11,7 @@ constexpr int kTileDefault = 512;   // default tile (measured best, see step_til
 constexpr int kResidentRows = 32;   // rows per block of the env-resident kernel
 constexpr int kResidentMax = 1024;  // largest N whose env fits the resident kernel's LDS
 constexpr int kSplitMax = 2048;     // largest N of the split-phase kernel (float32 env in LDS)
+constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many full-scan rows per workgroup
                                     // go wave-cooperative, more go one row per thread

@@ -199,6 +199,12 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// float32 position of a staged float64 state (reads px, py only)
+__device__ __forceinline__ float2 pos32(const St& s) {
+  const double2 p = *reinterpret_cast<const double2*>(&s);
+  return make_float2(static_cast<float>(p.x), static_cast<float>(p.y));
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -391,8 +397,15 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 // ---------------------------------------------------------------------------------
 // The fused step: DYN = apply dynamics (step) or not (compute_helpers on the current
 // state: reset / standalone controller), UF64 = action dtype, CTRL = also controller().
-#ifndef GF_STEP_MIN_WAVES
-#define GF_STEP_MIN_WAVES 1
+// Waves per SIMD the register allocation must allow: 7 for the plain step (71 VGPRs,
+// no spills; its LDS is floored to hold it at 6 workgroups per CU, see
+// kStepLdsPlainFloor), 6 with the controller (79 VGPRs, 23.2 KiB of LDS: 6 per CU);
+// variants are not capped (their extra state would spill).
+#ifndef GF_STEP_WAVES_PLAIN
+#define GF_STEP_WAVES_PLAIN 7
+#endif
+#ifndef GF_STEP_WAVES_CTRL
+#define GF_STEP_WAVES_CTRL 6
 #endif
 // Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
 // wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
@@ -411,14 +424,14 @@ __device__ unsigned long long gf_stamp_buf[8192 * 16];
 // VAR: the flocking variants' switches (StepArgs.variant); without it the FlockingRelative
 // path carries none of their instructions.
 template <bool DYN, bool UF64, bool CTRL, bool VAR>
-__global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel(StepArgs a) {
+__global__ __launch_bounds__(kThreads, VAR ? 1 : (CTRL ? GF_STEP_WAVES_CTRL : GF_STEP_WAVES_PLAIN))
+void flock_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
   const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
   const int Wt = T >> 6;         // words per row of one tile
   St* tile = reinterpret_cast<St*>(smem);                      // float64 state, T
-  float2* tile32 = reinterpret_cast<float2*>(tile + T);        // float32 positions, T
-  St* rows = reinterpret_cast<St*>(tile32 + T);                // this block's rows, R
+  St* rows = tile + T;                                         // this block's rows, R
   uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
   uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
   double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)R * Wt : 0));
@@ -450,12 +463,13 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   const bool frow = fr < nrows;
   double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
   double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
-  St me{0, 0, 0, 0};
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
 
   const int i_row = i0 + fr;  // global row of this thread's feature slice
-  // one neighbour pair (row fr, tile column c): features and controller gradient
-  auto pair_terms = [&](int j0, int c, bool isadj, bool isnear) {
+  // one neighbour pair (row fr = me, tile column c): features and controller gradient.
+  // The row's state is read from LDS per feature pass, so it holds no registers
+  // through pass 1.
+  auto pair_terms = [&](const St& me, int j0, int c, bool isadj, bool isnear) {
     const St o = tile[c];
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
@@ -487,6 +501,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   // cursor bookkeeping cost more than it saved: 266 vs 215 us, DESIGN.md.)
   auto feature_pass = [&](int j0, int nch) {
     if (!frow || (a.diag & 2)) return;
+    const St me = rows[fr];
     const int wpt = (nch + S - 1) / S;
     const int wb = fs * wpt, we = min(nch, wb + wpt);
     for (int w = wb; w < we; ++w) {
@@ -496,7 +511,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       while (m) {
         const int k = __builtin_ctzll(m);
         m &= m - 1;
-        pair_terms(j0, (w << 6) + k, (am >> k) & 1ull, CTRL && ((nm >> k) & 1ull));
+        pair_terms(me, j0, (w << 6) + k, (am >> k) & 1ull, CTRL && ((nm >> k) & 1ull));
       }
     }
   };
@@ -511,13 +526,11 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       const St s = load_state<DYN, UF64, VAR>(a, env0 + j0 + t);
       tile[t] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
-      tile32[t] = make_float2(fx, fy);
       pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
       svx += s.vx;
       svy += s.vy;
     }
     if (j0 == 0) {
-      if (frow) me = rows[fr];
       if (lane < nrows) {
         const St ri = rows[lane];
         rx32 = static_cast<float>(ri.px);
@@ -549,9 +562,10 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
       const bool has_b = ca + 1 < nch;
       const int jta = (ca << 6) + lane, jtb = jta + 64;
       const bool va = jta < tc, vb = jtb < tc;
+      // float32 positions from the tile's float64 states (no float32 copy is staged);
       // columns past the tile sit far away: never adjacent, never in the band
-      const float2 qa = va ? tile32[jta] : make_float2(1.0e18f, 1.0e18f);
-      const float2 qb = vb ? tile32[jtb] : make_float2(1.0e18f, 1.0e18f);
+      const float2 qa = va ? pos32(tile[jta]) : make_float2(1.0e18f, 1.0e18f);
+      const float2 qb = vb ? pos32(tile[jtb]) : make_float2(1.0e18f, 1.0e18f);
       const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
       unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
       uint64_t band = 0;
@@ -658,6 +672,7 @@ __global__ __launch_bounds__(kThreads, GF_STEP_MIN_WAVES) void flock_step_kernel
   feature_pass(jl, nchl);
   GF_STAMP(9);
 
+  const St me = frow ? rows[fr] : St{0, 0, 0, 0};
   step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
                                       frow && fs == 0, S, tid);
   GF_STAMP(10);
@@ -1363,10 +1378,10 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
 
 // ----------------------------------------------------------------------------- host
 // Geometry measured on MI355X (scripts/ablate.py, N=1024 x 256 envs): 32-row blocks
-// with 512-agent LDS tiles (25.2 KiB of LDS, 77 VGPRs) keep 6 workgroups per CU
-// resident, which is what hides the per-block load/compute latency under the network
-// stores: 190 us at 6 per CU, 193 at 5, 211 at 4 (scripts/occprobe.hip measures what
-// fits: <= 26 KiB -> 6, 27-31 KiB -> 5, 32 KiB -> 4).
+// with 512-agent LDS tiles keep 6 workgroups per CU resident, which is what hides the
+// per-block load/compute latency under the network stores: 190 us at 6 per CU, 193 at
+// 5, 211 at 4, 206 at 7 (scripts/occprobe.hip measures what fits: <= 20 KiB -> 8,
+// 24-26 KiB -> 6, 27-31 KiB -> 5, 32 KiB -> 4).
 int step_rows_per_block(int N) {
   const int words = (N + 63) / 64;
   int R = 32;
@@ -1382,7 +1397,7 @@ int step_tile(int N) {
 
 size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
-  size_t s = (size_t)T * (sizeof(St) + 8) + (size_t)R * sizeof(St);
+  size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 + 15) / 16) * 16;
   return s;
@@ -1442,6 +1457,9 @@ template <bool DYN, bool UF64, bool CTRL, bool VAR>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   if (a.split && a.N <= kSplitMax) return launch_step_split<DYN, UF64, CTRL, VAR>(a, s);
   size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
+  // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
+  // would allow
+  if (!CTRL && !VAR && a.lds_pad == 0 && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR>),
