@@ -53,6 +53,33 @@ def pair_geometry(x):
     return dx, dy, dvx, dvy, r2
 
 
+def pair_geometry_rows(x, rows):
+    """pair_geometry() for the rows `rows` only (each against every agent), the same
+    operations in the same order, so large N can be checked on sampled rows without the
+    (N,N) temporaries."""
+    rows = np.asarray(rows)
+    px, py, vx, vy = x[:, 0], x[:, 1], x[:, 2], x[:, 3]
+    dx = px[rows, None] - px[None, :]
+    dy = py[rows, None] - py[None, :]
+    dvx = vx[rows, None] - vx[None, :]
+    dvy = vy[rows, None] - vy[None, :]
+    r2 = dx * dx + dy * dy
+    r2[np.arange(len(rows)), rows] = np.inf
+    return dx, dy, dvx, dvy, r2
+
+
+def step_rows(x, u, rows, comm_radius=0.9, dt=0.01, action_scalar=10.0, with_controller=False):
+    """step() restricted to the rows `rows` of the per-agent outputs (helpers() and
+    controller() take the row geometry unchanged); x and the reward are the whole env's."""
+    x1 = integrate(x, u, dt, action_scalar)
+    geom = pair_geometry_rows(x1, rows)
+    sv, net, adj, deg = helpers(x1, comm_radius, True, geom)
+    out = dict(x=x1, state_values=sv, network=net, adj=adj, deg=deg, reward=reward(x1))
+    if with_controller:
+        out["ctrl"] = controller(x1, comm_radius, action_scalar, True, geom)
+    return out
+
+
 def helpers(x, comm_radius=0.9, mean_pooling=True, geom=None):
     """compute_helpers(), flocking_relative.py:111-134.
 

@@ -305,6 +305,33 @@ def test_env_resident_kernel_parity(monkeypatch):
         h.close()
 
 
+def test_config5_size_sampled_rows():
+    """N=8192 (BASELINE.json configs[4]'s agent count; 16-row blocks, 16 LDS tiles per
+    row sweep): the whole state and reward, and 40 sampled rows of the network,
+    state_values and controller (first/last rows, tile and block edges, random rows)
+    against the oracle restricted to those rows."""
+    n, B = 8192, 2
+    x0 = synthetic_batch(B, n, seed0=8192)
+    u = np.random.RandomState(81).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    rs = np.random.RandomState(82)
+    rows = np.unique(np.concatenate([[0, 1, 15, 16, 511, 512, 4095, 4096, 8190, 8191],
+                                     rs.choice(n, 30, replace=False)]))
+    h = nat.FlockHandle(n, B)
+    h.set_state(x0)
+    h.step(u, nat.FE_WITH_CONTROLLER)
+    x1, sv, rew, ctrl = h.get_state(), h.state_values(), h.rewards(), h.controls()
+    for b in range(B):
+        ref = orc.step_rows(x0[b], u[b], rows, with_controller=True)
+        np.testing.assert_array_equal(x1[b], ref["x"])
+        np.testing.assert_allclose(rew[b], ref["reward"], rtol=1e-12)
+        for k, r in enumerate(rows):
+            net = h.network_rows(b, int(r), 1)[0]
+            np.testing.assert_array_equal(net, ref["network"][k].astype(np.float32))
+        close_sv(sv[b][rows], ref["state_values"])
+        np.testing.assert_allclose(ctrl[b][rows], ref["ctrl"], rtol=1e-9, atol=1e-12)
+    h.close()
+
+
 def test_split_kernel_parity(monkeypatch):
     """The opt-in split-phase step kernel (GYMFLOCK_SPLIT=1: float32 env positions, pass 1
     over every column, stores, then float64 tiles for the features) matches the oracle,
