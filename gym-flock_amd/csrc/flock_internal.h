@@ -43,7 +43,7 @@ struct StepArgs {
                           // unwritten: timing only), 16 skip tile loads (timing only),
                           // 64 / 128 generic / fast network store loop (A/B), 256 no
                           // per-row outputs, 512 no reward, 1024 constant network rows
-                          // (timing only)
+                          // (timing only), 8192 plain XCD remap for the plain step (A/B)
   // Flocking variants (flocking_leader/obstacle/stoch.py). variant == 0 keeps the
   // FlockingRelative path untouched; otherwise the fields below apply (tiled kernel).
   int variant;
