@@ -383,7 +383,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "flock_step_kernel<DYN,f32 u>", "kernel_ms": kernel_ms,
-                         "launches_timed": launches, "algorithmic_bytes_per_launch": bytes_launch},
+                         "steps_timed": launches, "algorithmic_bytes_per_step": bytes_launch,
+                         "launches_per_step": 2 if B >= 2 else 1,
+                         "timing": "device time per step over the timed region (HIP events on the "
+                                   "handle's stream after it joins the second): each step is two "
+                                   "concurrent half-batch launches of the kernel on two streams, "
+                                   "so kernel_ms and the bytes are per step (both launches)"},
         }
         line.update(extra)
         if world == 1 and not args.no_cpu_baseline:

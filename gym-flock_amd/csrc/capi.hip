@@ -49,6 +49,18 @@ struct fe_handle {
   fe_config cfg{};
   hipStream_t stream = nullptr;
   hipStream_t comm_stream = nullptr;
+  // Split steps: the step's env batch goes out as two launches, envs [0, B0) on
+  // `stream` and [B0, B) on `stream2`, so one launch's ramp and tail overlap the other's
+  // body (175.8 vs 196.0 us per config-2 step). The halves only depend on
+  // their own previous step; `stream` waits for `stream2` (join) before any other work.
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_s2 = nullptr;           // stream2 -> stream join
+  hipEvent_t ev_main = nullptr;         // stream -> stream2 ordering
+  int nsplit = 2;                       // launches per step (fe_set_streams, GYMFLOCK_STREAMS)
+  bool s2_pending = false;              // stream2 holds work `stream` has not waited for
+  bool main_dirty = true;               // `stream` holds work stream2 has not waited for
+  hipEvent_t tw[2] = {nullptr, nullptr};  // split-step timing window (fe_kernel_timing)
+  int64_t tw_steps = 0;
   double* x[2] = {nullptr, nullptr};
   int cur = 0;
   void* u = nullptr;                    // (B,N,2) up to float64
@@ -102,7 +114,28 @@ struct fe_handle {
 
 namespace {
 
-int use_dev(const fe_handle* h) {
+// `stream` waits for the second half-batch stream (enqueue only, no host sync).
+int join_s2(fe_handle* h) {
+  if (h->s2_pending) {
+    GF_HIP(hipEventRecord(h->ev_s2, h->stream2));
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ev_s2, 0));
+    h->s2_pending = false;
+  }
+  return GF_OK;
+}
+
+// Every API call except the step launches: the device, and `stream` ordered after all
+// of the handle's outstanding work; what it enqueues is ordered before the next
+// second-half launch (main_dirty).
+int use_dev(fe_handle* h) {
+  GF_HIP(hipSetDevice(h->cfg.device));
+  if (int rc = join_s2(h)) return rc;
+  h->main_dirty = true;
+  return GF_OK;
+}
+
+// The step path: only the device (the halves order themselves, see launch_step_split).
+int use_dev_step(fe_handle* h) {
   GF_HIP(hipSetDevice(h->cfg.device));
   return GF_OK;
 }
@@ -122,6 +155,7 @@ void release(fe_handle* h) {
   if (!h) return;
   hipSetDevice(h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
@@ -134,7 +168,10 @@ void release(fe_handle* h) {
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
   for (hipEvent_t e : h->ag_ev)
     if (e) hipEventDestroy(e);
+  for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1]})
+    if (e) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
+  if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->comm_stream) hipStreamDestroy(h->comm_stream);
   delete h;
 }
@@ -153,6 +190,7 @@ int next_reward_slot(fe_handle* h) {
   const int blk = h->rslot / kGatherBlock;
   if (h->rslot % kGatherBlock == 0 && h->ag_pending[blk]) {  // re-entering a gathered block
     GF_HIP(hipStreamWaitEvent(h->stream, h->ag_ev[blk], 0));
+    if (h->stream2) GF_HIP(hipStreamWaitEvent(h->stream2, h->ag_ev[blk], 0));
     h->ag_pending[blk] = false;
   }
   return GF_OK;
@@ -230,6 +268,38 @@ gf::StepArgs base_args(fe_handle* h) {
 int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
   gf::StepArgs a = a_in;
   a.store_fast = h->store_fast[ctrl ? 1 : 0];
+  if (h->nsplit > 1 && a.B >= 2 && h->stream2) {
+    // two launches: envs [0, B0) on `stream`, [B0, B) on `stream2`, each after its own
+    // half of the previous step; stream2 also waits for whatever `stream` was given
+    // since (host action copies, state uploads, consumers of the last outputs)
+    if (h->main_dirty) {
+      GF_HIP(hipEventRecord(h->ev_main, h->stream));
+      GF_HIP(hipStreamWaitEvent(h->stream2, h->ev_main, 0));
+      h->main_dirty = false;
+    }
+    const int B = a.B, B0 = (B + 1) / 2, N = a.N;
+    const size_t Wn = (N + 63) / 64, e0 = (size_t)B0 * N;
+    gf::StepArgs a1 = a;
+    a.B = B0;
+    a1.B = B - B0;
+    a1.x_in = a.x_in + e0 * 4;
+    if (a.x_out) a1.x_out = a.x_out + e0 * 4;
+    if (a.u) a1.u = static_cast<const char*>(a.u) + e0 * 2 * (uf64 ? 8 : 4);
+    if (a.state_values) a1.state_values = a.state_values + e0 * 6;
+    if (a.network) a1.network = a.network + e0 * N;
+    if (a.ctrl_out) a1.ctrl_out = a.ctrl_out + e0 * 2;
+    if (a.reward) a1.reward = a.reward + B0;
+    if (a.dt_env) a1.dt_env = a.dt_env + B0;
+    if (a.adj_bits) a1.adj_bits = a.adj_bits + e0 * Wn;
+    if (a.degree_out) a1.degree_out = a.degree_out + e0;
+    hipError_t e = gf::launch_step(a, dyn, uf64, ctrl, h->stream);
+    if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
+    if (e != hipSuccess) return fail_hip("flock_step_kernel launch", e);
+    h->s2_pending = true;
+    if (h->timing) h->tw_steps++;
+    return GF_OK;
+  }
+  if (int rc = join_s2(h)) return rc;  // a single launch covers both halves
   // a sampled launch is bracketed by two events (which also keep it from overlapping
   // its neighbours, so sampling every launch costs the stream ~7 us per step)
   const bool sample = h->timing && (h->timing_count++ % h->timing_stride) == 0;
@@ -255,6 +325,8 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
 // kNN of the current state; uses_adj: the last launch wrote this state's adjacency
 // (packed outputs), which lets agents with >= k neighbours rank only those.
 int launch_knn_cur(fe_handle* h, int mode) {
+  if (int rc = join_s2(h)) return rc;  // reads both halves' state and bits
+  h->main_dirty = true;
   gf::KnnArgs k{};
   k.x = h->x[h->cur];
   k.adj_bits = mode == 1 ? h->adj_bits : nullptr;
@@ -369,10 +441,15 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     release(h);
     return rc;
   }
-  if ((e = hipEventCreateWithFlags(&h->h2d_ev, hipEventDisableTiming)) != hipSuccess) {
+  if ((e = hipEventCreateWithFlags(&h->h2d_ev, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreate(&h->tw[0])) != hipSuccess || (e = hipEventCreate(&h->tw[1])) != hipSuccess) {
     release(h);
     return fail_hip("event create", e);
   }
+  if (const char* e = getenv("GYMFLOCK_STREAMS")) h->nsplit = atoi(e) == 1 ? 1 : 2;
   if ((e = hipMemsetAsync(h->reward_ring, 0, sizeof(double) * kRewardSlots * B, h->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
     release(h);
@@ -461,7 +538,7 @@ int fe_get_state_env(fe_handle* h, int env, double* x) {
 int fe_compute_helpers(fe_handle* h, int flags) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->has_state) return fail(GF_ESTATE, "state not set");
-  if (int rc = use_dev(h)) return rc;
+  if (int rc = use_dev_step(h)) return rc;
   const bool ctrl = flags & FE_WITH_CONTROLLER;
   if (int rc = next_reward_slot(h)) return rc;
   gf::StepArgs a = base_args(h);
@@ -486,7 +563,7 @@ int fe_compute_helpers(fe_handle* h, int flags) {
 int fe_step(fe_handle* h, const void* u, int flags) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->has_state) return fail(GF_ESTATE, "state not set (call fe_set_state first)");
-  if (int rc = use_dev(h)) return rc;
+  if (int rc = use_dev_step(h)) return rc;
   const bool ctrl = flags & FE_WITH_CONTROLLER;
   bool uf64 = flags & FE_U_F64;
   const void* up = nullptr;
@@ -503,8 +580,11 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   } else if (flags & FE_U_DEVICE) {
     up = u;
   } else {
+    // the previous step's second half may still read h->u: copy after it
+    if (int rc = join_s2(h)) return rc;
     GF_HIP(hipMemcpyAsync(h->u, u, h->BN * 2 * (uf64 ? 8 : 4), hipMemcpyHostToDevice, h->stream));
     GF_HIP(hipEventRecord(h->h2d_ev, h->stream));
+    h->main_dirty = true;
     up = h->u;
     h->u_resident_f64 = -1;  // the buffer now holds this call's actions
   }
@@ -715,6 +795,18 @@ int fe_sync(fe_handle* h) {
   return GF_OK;
 }
 
+int fe_set_streams(fe_handle* h, int n) {
+  if (!h || (n != 1 && n != 2)) return fail(GF_EINVAL, "n must be 1 or 2");
+  if (int rc = use_dev(h)) return rc;
+  h->nsplit = n;
+  return GF_OK;
+}
+
+int fe_join(fe_handle* h) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  return use_dev(h);
+}
+
 int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (int rc = use_dev(h)) return rc;
@@ -724,6 +816,24 @@ int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches
     h->timing = true;
     h->timing_stride = enable;
     h->timing_count = 0;
+    // split steps: one window over all of them (both halves run concurrently, so a
+    // launch's own duration is not the step's); stream2 starts after the mark
+    h->tw_steps = 0;
+    GF_HIP(hipEventRecord(h->tw[0], h->stream));
+    return GF_OK;
+  }
+  if (h->tw_steps > 0) {  // split steps: device time of the window per step
+    GF_HIP(hipEventRecord(h->tw[1], h->stream));  // after use_dev's join: both halves
+    GF_HIP(hipEventSynchronize(h->tw[1]));
+    float ms = 0;
+    GF_HIP(hipEventElapsedTime(&ms, h->tw[0], h->tw[1]));
+    if (avg_ms) *avg_ms = ms / h->tw_steps;
+    if (launches) *launches = h->tw_steps;
+    if (enable == 0) h->timing = false;
+    else {
+      h->tw_steps = 0;
+      GF_HIP(hipEventRecord(h->tw[0], h->stream));
+    }
     return GF_OK;
   }
   GF_HIP(hipStreamSynchronize(h->stream));

@@ -96,6 +96,8 @@ SIGNATURES = {
     "fe_get_knn": [_P, _I, _P, _P],
     "fe_device_buffers": [_P, ctypes.POINTER(FeBuffers)],
     "fe_sync": [_P],
+    "fe_set_streams": [_P, _I],
+    "fe_join": [_P],
     "fe_comm_unique_id": [_P],
     "fe_comm_init": [_P, _I, _I, _P],
     "fe_allgather_rewards": [_P],
@@ -159,6 +161,8 @@ def load(path=None):
         mode |= os.RTLD_DEEPBIND
     lib = ctypes.CDLL(p, mode=mode)
     for name, args in SIGNATURES.items():
+        if not hasattr(lib, name) and os.environ.get("GYMFLOCK_LIB"):
+            continue  # an older library selected for an A/B run lacks newer entry points
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPE.get(name, ctypes.c_int)
@@ -345,8 +349,18 @@ class FlockHandle:
         check(self.lib.fe_sync(self.h))
 
     # -- timing (bench)
+    def set_streams(self, n):
+        """Launches per step: 2 (default) splits the env batch over two HIP streams so
+        consecutive launches overlap; 1 keeps every step on the handle's stream."""
+        check(self.lib.fe_set_streams(self.h, int(n)))
+
+    def join(self):
+        """Order the handle's stream after all outstanding work (no host wait)."""
+        check(self.lib.fe_join(self.h))
+
     def timing_start(self, every=1):
-        """Time every `every`-th step launch with HIP events (fe_kernel_timing)."""
+        """Time every `every`-th step launch with HIP events (fe_kernel_timing); with
+        split steps, the device time per step of the whole window instead."""
         check(self.lib.fe_kernel_timing(self.h, int(every), None, None))
 
     def timing_stop(self):

@@ -15,8 +15,10 @@
  *  - Arrays are row-major, C-contiguous. Shapes use B = n_envs, N = n_agents.
  *  - Host pointers are borrowed for the duration of the call. The library owns
  *    all device memory; fe_device_buffers() exposes it for zero-copy consumers.
- *  - One handle per host thread. All work of a handle is ordered on its own HIP
- *    stream; getters synchronise that stream before copying out.
+ *  - One handle per host thread. A step's two half-batch launches run on the
+ *    handle's stream and a second one (fe_set_streams); every other call orders the
+ *    handle's stream after both first, and getters synchronise it before copying out.
+ *    Zero-copy consumers of fe_buffers.stream call fe_join() after fe_step.
  *  - Agent state is float64 (B,N,4) = [px, py, vx, vy] because the reference
  *    integrates in float64 (flocking_relative.py:157); observations are float32.
  */
@@ -286,8 +288,19 @@ int fe_abi_version(void);
 /* Average device time (ms) of the step kernel, measured with HIP events on the
  * handle's stream (bench roofline). enable >= 1 starts timing every enable-th launch
  * (events keep a sampled launch from overlapping its neighbours); 0 reads and stops;
- * -1 reads and keeps timing. */
+ * -1 reads and keeps timing. With split steps (fe_set_streams, 2 by default) the
+ * result is the device time of the whole window since enable divided by the steps in
+ * it, and `launches` counts steps (each two concurrent half-batch launches). */
 int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches);
+/* Launches per step: 2 (default; GYMFLOCK_STREAMS=1 at create for 1) sends envs
+ * [0, ceil(B/2)) to the handle's stream and the rest to a second stream; each half
+ * depends only on its own previous step, so one launch's ramp and tail overlap the
+ * other's body. Every other call first orders the handle's stream after both halves,
+ * so getters and fe_sync see whole steps. */
+int fe_set_streams(fe_handle* h, int n);
+/* Order the handle's stream after all of its outstanding work (enqueue only, no host
+ * wait): for zero-copy consumers that enqueue on fe_buffers.stream after fe_step. */
+int fe_join(fe_handle* h);
 /* The same for cov_step_kernel on a Coverage handle. */
 int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launches);
 /* Diagnostics for roofline work: what = 0/1 times `reps` launches of a float4
