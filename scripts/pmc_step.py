@@ -13,6 +13,9 @@ N = int(os.environ.get("N", 1024))
 B = int(os.environ.get("B", 256))
 STEPS = int(os.environ.get("STEPS", 5))
 h = nat.FlockHandle(N, B)
+# one launch per step (fe_set_streams(1)) so each counter row is a whole step's bytes;
+# the split launches of the default write the same bytes in two halves
+h.set_streams(1)
 h.set_state(synthetic_batch(B, N))
 h.set_actions(np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
 h.diag_switches(int(os.environ.get("DIAG", 0)))
