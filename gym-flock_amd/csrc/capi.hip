@@ -59,6 +59,9 @@ struct fe_handle {
   int nsplit = 2;                       // launches per step (fe_set_streams, GYMFLOCK_STREAMS)
   bool s2_pending = false;              // stream2 holds work `stream` has not waited for
   bool main_dirty = true;               // `stream` holds work stream2 has not waited for
+  bool other_work = true;               // non-step work was enqueued since the last step:
+                                        // the next step goes out as one launch (a split
+                                        // step would only wait on it across streams)
   hipEvent_t tw[2] = {nullptr, nullptr};  // split-step timing window (fe_kernel_timing)
   int64_t tw_steps = 0;
   double* x[2] = {nullptr, nullptr};
@@ -131,6 +134,7 @@ int use_dev(fe_handle* h) {
   GF_HIP(hipSetDevice(h->cfg.device));
   if (int rc = join_s2(h)) return rc;
   h->main_dirty = true;
+  h->other_work = true;
   return GF_OK;
 }
 
@@ -268,7 +272,9 @@ gf::StepArgs base_args(fe_handle* h) {
 int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
   gf::StepArgs a = a_in;
   a.store_fast = h->store_fast[ctrl ? 1 : 0];
-  if (h->nsplit > 1 && a.B >= 2 && h->stream2) {
+  const bool split = h->nsplit > 1 && a.B >= 2 && h->stream2 && !h->other_work;
+  h->other_work = false;
+  if (split) {
     // two launches: envs [0, B0) on `stream`, [B0, B) on `stream2`, each after its own
     // half of the previous step; stream2 also waits for whatever `stream` was given
     // since (host action copies, state uploads, consumers of the last outputs)
@@ -300,6 +306,8 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     return GF_OK;
   }
   if (int rc = join_s2(h)) return rc;  // a single launch covers both halves
+  h->main_dirty = true;
+  if (h->timing && h->nsplit > 1) h->tw_steps++;  // the window counts every step
   // a sampled launch is bracketed by two events (which also keep it from overlapping
   // its neighbours, so sampling every launch costs the stream ~7 us per step)
   const bool sample = h->timing && (h->timing_count++ % h->timing_stride) == 0;
@@ -584,7 +592,7 @@ int fe_step(fe_handle* h, const void* u, int flags) {
     if (int rc = join_s2(h)) return rc;
     GF_HIP(hipMemcpyAsync(h->u, u, h->BN * 2 * (uf64 ? 8 : 4), hipMemcpyHostToDevice, h->stream));
     GF_HIP(hipEventRecord(h->h2d_ev, h->stream));
-    h->main_dirty = true;
+    h->main_dirty = h->other_work = true;
     up = h->u;
     h->u_resident_f64 = -1;  // the buffer now holds this call's actions
   }

@@ -41,6 +41,16 @@ int calloc_dev(T** p, size_t n) {
 struct cov_handle {
   cov_config cfg{};
   hipStream_t stream = nullptr;
+  // Split steps as in fe_handle: envs [0, ceil(B/2)) step on `stream`, the rest on
+  // `stream2`; each half depends only on its own previous step, every other call first
+  // makes `stream` wait for `stream2`.
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_s2 = nullptr, ev_main = nullptr;
+  int nsplit = 2;
+  bool s2_pending = false, main_dirty = true;
+  bool other_work = true;  // non-step work since the last step: next step is one launch
+  hipEvent_t tw[2] = {nullptr, nullptr};
+  int64_t tw_steps = 0;
   gf::CovArgs a{};
   int32_t* ntg = nullptr;
   double* tgt = nullptr;
@@ -78,8 +88,22 @@ struct cov_handle {
 
 namespace {
 
-int use(const cov_handle* h) {
+int join_s2(cov_handle* h) {
+  if (h->s2_pending) {
+    CV_HIP(hipEventRecord(h->ev_s2, h->stream2));
+    CV_HIP(hipStreamWaitEvent(h->stream, h->ev_s2, 0));
+    h->s2_pending = false;
+  }
+  return GF_OK;
+}
+
+// Every call but cov_step: the device, `stream` after all outstanding work, and what
+// it enqueues ordered before the next second-half step.
+int use(cov_handle* h) {
   CV_HIP(hipSetDevice(h->cfg.device));
+  if (int rc = join_s2(h)) return rc;
+  h->main_dirty = true;
+  h->other_work = true;
   return GF_OK;
 }
 
@@ -87,6 +111,7 @@ void cov_release(cov_handle* h) {
   if (!h) return;
   hipSetDevice(h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->stream2) hipStreamSynchronize(h->stream2);
   gf::CovArgs& a = h->a;
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
@@ -96,7 +121,10 @@ void cov_release(cov_handle* h) {
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
+  for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1]})
+    if (e) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
+  if (h->stream2) hipStreamDestroy(h->stream2);
   delete h;
 }
 
@@ -262,10 +290,15 @@ int cov_create(const cov_config* cfg, cov_handle** out) {
   a.res = cfg->res;
   a.motion_radius = cfg->motion_radius;
   int rc = GF_OK;
-  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&h->tw[0]) != hipSuccess || hipEventCreate(&h->tw[1]) != hipSuccess) {
     cov_release(h);
     return cfail(GF_EHIP, "stream create failed");
   }
+  if (const char* e = getenv("GYMFLOCK_STREAMS")) h->nsplit = atoi(e) == 1 ? 1 : 2;
   if ((rc = calloc_dev(&h->ntg, B)) || (rc = calloc_dev(&h->tgt, B * Tm * 2)) || (rc = calloc_dev(&a.nbr, B * Tm * 4)) ||
       (rc = calloc_dev(&a.cnt, B * Tm)) || (rc = calloc_dev(&a.n_motion, B)) || (rc = calloc_dev(&a.xr, B * R * 2)) ||
       (rc = calloc_dev(&a.cur, B * R)) || (rc = calloc_dev(&a.visited, B * Tm)) || (rc = calloc_dev(&a.nvisited, B)) ||
@@ -353,7 +386,7 @@ int cov_set_actions(cov_handle* h, const int32_t* actions) {
 int cov_step(cov_handle* h, const int32_t* actions, int flags) {
   if (!h) return cfail(GF_EINVAL, "null handle");
   if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
-  if (int rc = use(h)) return rc;
+  CV_HIP(hipSetDevice(h->cfg.device));
   gf::CovArgs a = h->a;
   if (flags & COV_ACTIONS_DEVICE) {
     if (!actions) return cfail(GF_EINVAL, "null action pointer");
@@ -365,9 +398,34 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     const size_t n = (size_t)h->cfg.n_envs * h->cfg.n_robots;
     for (size_t k = 0; k < n; ++k)
       if (actions[k] < 0 || actions[k] >= 4) return cfail(GF_EINVAL, "action outside [0, 4) (coverage.py:189 index)");
+    if (int rc = join_s2(h)) return rc;  // the previous second half may still read h->actions
     CV_HIP(hipMemcpyAsync(h->actions, actions, n * 4, hipMemcpyHostToDevice, h->stream));
+    h->main_dirty = h->other_work = true;
     a.actions = h->actions;
   }
+  const bool split = h->nsplit > 1 && a.B >= 2 && !h->other_work;
+  h->other_work = false;
+  if (split) {
+    if (h->main_dirty) {
+      CV_HIP(hipEventRecord(h->ev_main, h->stream));
+      CV_HIP(hipStreamWaitEvent(h->stream2, h->ev_main, 0));
+      h->main_dirty = false;
+    }
+    gf::CovArgs a1 = a;
+    a.B = (a.B + 1) / 2;
+    a1.env0 = a.B;
+    a1.B = h->a.B - a.B;
+    hipError_t e = gf::launch_cov_step(a, h->stream);
+    if (e == hipSuccess) e = gf::launch_cov_step(a1, h->stream2);
+    if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
+    h->s2_pending = true;
+    if (h->timing) h->tw_steps++;
+    if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT))) CV_HIP(hipStreamSynchronize(h->stream));
+    return GF_OK;
+  }
+  if (int rc = join_s2(h)) return rc;
+  h->main_dirty = true;
+  if (h->timing && h->nsplit > 1) h->tw_steps++;  // the window counts every step
   const bool sample = h->timing && (h->timing_count++ % h->timing_stride) == 0;
   if (sample) {
     if (h->ev_used + 2 > h->ev.size()) {
@@ -398,6 +456,22 @@ int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launch
     h->timing = true;
     h->timing_stride = enable;
     h->timing_count = 0;
+    h->tw_steps = 0;  // split steps: one window, device time per step
+    CV_HIP(hipEventRecord(h->tw[0], h->stream));
+    return GF_OK;
+  }
+  if (h->tw_steps > 0) {
+    CV_HIP(hipEventRecord(h->tw[1], h->stream));
+    CV_HIP(hipEventSynchronize(h->tw[1]));
+    float ms = 0;
+    CV_HIP(hipEventElapsedTime(&ms, h->tw[0], h->tw[1]));
+    if (avg_ms) *avg_ms = ms / h->tw_steps;
+    if (launches) *launches = h->tw_steps;
+    if (enable == 0) h->timing = false;
+    else {
+      h->tw_steps = 0;
+      CV_HIP(hipEventRecord(h->tw[0], h->stream));
+    }
     return GF_OK;
   }
   double tot = 0;

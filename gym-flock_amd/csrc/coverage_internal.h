@@ -9,6 +9,7 @@ namespace gf {
 // (robots + targets), i.e. at most Tmax = M - R targets per env.
 struct CovArgs {
   int B, R, M, Tmax, episode_length;
+  int env0;               // cov_step_kernel: first env of this launch (split steps)
   double res, motion_radius;
   const double* tgt;      // (B,Tmax,2) target positions
   const int32_t* ntg;     // (B) targets per env

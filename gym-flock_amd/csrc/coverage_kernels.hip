@@ -131,7 +131,7 @@ __device__ __forceinline__ int action_node(const int32_t* nbr, const int32_t* cn
 // After an external placement, a new graph or a reset, everything is recomputed.
 __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x;
+  const int b = a.env0 + blockIdx.x;
   const int R = a.R, M = a.M, Tm = a.Tmax, E = 4 * M;
   const int T = a.ntg[b];
   int* cur_s = reinterpret_cast<int*>(smem);          // R: node before the move
