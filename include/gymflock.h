@@ -221,6 +221,9 @@ int cov_get_rewards(cov_handle* h, double* reward, uint8_t* done);   /* (B), (B)
 int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes); /* closest_targets :427 */
 int cov_get_visited(cov_handle* h, int env, uint8_t* visited);
 int cov_get_n_motion(cov_handle* h, int32_t* n_motion);
+/* Back-to-back cov_step calls go out as two half-batch launches on two streams (as
+ * fe_set_streams; GYMFLOCK_STREAMS=1 at create for one); every other call, cov_sync
+ * included, first orders the handle's stream after both. */
 int cov_sync(cov_handle* h);
 /* Greedy expert, controller(greedy=True) :800-872. On first use after cov_set_targets
  * it builds each env's time matrix (construct_time_matrix :621-653) on the device;
@@ -296,7 +299,8 @@ int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches
  * [0, ceil(B/2)) to the handle's stream and the rest to a second stream; each half
  * depends only on its own previous step, so one launch's ramp and tail overlap the
  * other's body. Every other call first orders the handle's stream after both halves,
- * so getters and fe_sync see whole steps. */
+ * so getters and fe_sync see whole steps. A step follows as one launch when other
+ * work was enqueued on the handle since the previous step. */
 int fe_set_streams(fe_handle* h, int n);
 /* Order the handle's stream after all of its outstanding work (enqueue only, no host
  * wait): for zero-copy consumers that enqueue on fe_buffers.stream after fe_step. */
