@@ -202,3 +202,32 @@ def test_crowded_grid_claims_vs_oracle(R):
         np.testing.assert_array_equal(h.robots(0)[1], o.closest())
         assert h.rewards()[0][0] == rr
     h.close()
+
+
+def test_split_steps_match_single_stream(monkeypatch):
+    """Back-to-back resident steps go out as two half-batch launches on two streams;
+    the observations, rewards and robots equal the one-launch-per-step run."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, R, M = 5, 12, 600
+    np.random.seed(7)
+    targets = generate_targets()
+    runs = []
+    for streams in ("2", "1"):
+        monkeypatch.setenv("GYMFLOCK_STREAMS", streams)
+        h = nat.CoverageHandle(R, B, M)
+        h.set_targets(targets)
+        T = len(targets)
+        rs = np.random.RandomState(11)
+        start = np.stack([rs.choice(T, R, replace=False) for _ in range(B)]).astype(np.int32)
+        h.reset(start, np.zeros((B, M - R), np.uint8))
+        got = []
+        for k in range(3):
+            h.set_actions(rs.randint(0, 4, size=(B, R)))
+            for _ in range(4):
+                h.step(resident=True)
+            got += [h.rewards()[0]] + [h.obs(b)[key] for b in range(B) for key in ("nodes", "edges", "senders")]
+            got += [h.robots(b)[1] for b in range(B)]
+        runs.append(got)
+        h.close()
+    for a, b in zip(*runs):
+        np.testing.assert_array_equal(a, b)

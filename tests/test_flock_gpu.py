@@ -332,6 +332,37 @@ def test_config5_size_sampled_rows():
     h.close()
 
 
+def test_split_steps_match_single_stream():
+    """Two half-batch launches per step on two streams (the default) give the same bits
+    as one launch per step, over resident, host and closed-loop steps mixed with
+    getters, kNN and packed outputs (the join / ordering rules of fe_set_streams)."""
+    n, B = 300, 5
+    x0 = synthetic_batch(B, n, seed0=3000)
+    rs = np.random.RandomState(3001)
+    us = [rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32) for _ in range(6)]
+    outs = []
+    for streams in (2, 1):
+        h = nat.FlockHandle(n, B, n_neighbors=7)
+        h.set_streams(streams)
+        h.set_state(x0)
+        h.set_actions(us[0])
+        got = []
+        for _ in range(4):  # back-to-back resident steps (split when streams == 2)
+            h.step(None, nat.FE_U_RESIDENT)
+        got += [h.get_state(), h.network(), h.rewards()]
+        h.step(us[1], nat.FE_WITH_CONTROLLER | nat.FE_WITH_KNN)  # host actions, kNN
+        got += [h.knn()[0], h.state_values(), h.controls()]
+        for _ in range(3):  # closed loop on the device
+            h.step(None, nat.FE_U_EXPERT | nat.FE_WITH_CONTROLLER)
+        got += [h.controls()]
+        h.step(us[2], nat.FE_PACKED_NETWORK)
+        got += [h.get_state(), h.network_packed()[0], h.rewards()]
+        outs.append(got)
+        h.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_split_kernel_parity(monkeypatch):
     """The opt-in split-phase step kernel (GYMFLOCK_SPLIT=1: float32 env positions, pass 1
     over every column, stores, then float64 tiles for the features) matches the oracle,
