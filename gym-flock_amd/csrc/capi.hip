@@ -86,6 +86,8 @@ struct fe_handle {
   // kernel timing (bench roofline)
   int diag = 0;                         // ablation switches for every step launch
   int lds_pad = 0;                      // occupancy tuning (GYMFLOCK_LDS_PAD)
+  int prefetch = 0;                     // tile loads one tile ahead (GYMFLOCK_PREFETCH)
+  int lds_floor = (int)gf::kStepLdsPlainFloor;  // plain-step occupancy cap (GYMFLOCK_LDS_FLOOR)
   int split = 0;                        // split-phase step kernel (opt-in GYMFLOCK_SPLIT=1; slower)
   int T_split = 512;                    // its phase-B tile (GYMFLOCK_SPLIT_TILE)
   int store_fast[2] = {0, 1};           // fast network store loop, plain step / with controller
@@ -246,6 +248,8 @@ gf::StepArgs base_args(fe_handle* h) {
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
   a.lds_pad = h->lds_pad;
+  a.lds_floor = h->lds_floor;
+  a.prefetch = h->prefetch;
   a.split = h->split && h->cfg.n_agents <= gf::kSplitMax;
   if (a.split) a.T = h->T_split;
   a.u_scale = h->cfg.action_scalar;
@@ -407,6 +411,7 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     gf::step_resident_geometry(cfg->n_agents, cfg->n_envs, target, &h->spe, &h->rps);
   }
   if (const char* e = getenv("GYMFLOCK_LDS_PAD")) h->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
+  if (const char* e = getenv("GYMFLOCK_LDS_FLOOR")) h->lds_floor = atoi(e) >= 0 ? atoi(e) : 0;
   if (const char* e = getenv("GYMFLOCK_SPLIT")) h->split = atoi(e) != 0;
   {
     const int full = ((cfg->n_agents + 63) / 64) * 64;
@@ -429,6 +434,10 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     }
   }
 
+  // tile loads issued a tile ahead: 1604 -> 1527 us at N=8192 (16 tiles); no gain at 2-8
+  // tiles, where its registers cost occupancy instead
+  h->prefetch = (cfg->n_agents + h->T - 1) / h->T >= 16 ? 1 : 0;
+  if (const char* e = getenv("GYMFLOCK_PREFETCH")) h->prefetch = atoi(e) == 2 ? 2 : atoi(e) != 0;
   h->bpe = (cfg->n_agents + h->R - 1) / h->R;
   if ((size_t)h->bpe * B > 0x7fffffff) {
     delete h;

@@ -36,7 +36,9 @@ struct StepArgs {
   int resident;           // 1: env-resident kernel (N <= kResidentMax)
   int spe, rps;           // resident kernel: slices per env, rows per slice
   int lds_pad;            // extra dynamic LDS bytes (occupancy control; tuning knob)
+  int lds_floor;          // plain step: dynamic LDS raised to at least this (occupancy cap)
   int split;              // 1: split-phase kernel (N <= kSplitMax, see flock_step_split_kernel)
+  int prefetch;           // tiled step issues each tile's loads one tile ahead (T <= 512)
   int store_fast;         // network rows by the fast bit-extract loop (N % 1024 == 0)
   int diag;               // ablation switches (0 in production): 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left

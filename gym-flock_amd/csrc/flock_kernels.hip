@@ -24,6 +24,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <type_traits>
+
 namespace gf {
 
 namespace {
@@ -131,23 +133,39 @@ __device__ St load_state_variant(const StepArgs& a, size_t g, double2 p, double2
   return s;
 }
 
-template <bool DYN, bool UF64, bool VAR = false>
-__device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
+// The global loads behind one agent's post-update state, and the update itself: split
+// so the tiled step can issue a tile's loads one tile ahead (PF) and apply the update
+// when it stages the tile.
+template <bool UF64>
+struct RawState {
+  double2 p, v;
+  typename std::conditional<UF64, double2, float2>::type u;
+};
+
+template <bool DYN, bool UF64>
+__device__ __forceinline__ RawState<UF64> load_raw(const StepArgs& a, size_t g) {
+  using U = typename std::conditional<UF64, double2, float2>::type;
   const double2* xp = reinterpret_cast<const double2*>(a.x_in) + 2 * g;
-  const double2 p = xp[0], v = xp[1];
+  RawState<UF64> r;
+  r.p = xp[0];
+  r.v = xp[1];
+  if constexpr (DYN) r.u = reinterpret_cast<const U*>(a.u)[g];
+  return r;
+}
+
+template <bool DYN, bool UF64>
+__device__ __forceinline__ St state_from_raw(const StepArgs& a, const RawState<UF64>& r) {
+  const double2 p = r.p, v = r.v;
   St s{p.x, p.y, v.x, v.y};
   if constexpr (DYN) {
-    if constexpr (VAR) return load_state_variant<UF64>(a, g, p, v);
     if constexpr (UF64) {
-      const double2 u = reinterpret_cast<const double2*>(a.u)[g];
-      const double ux = u.x * a.action_scalar, uy = u.y * a.action_scalar;
+      const double ux = r.u.x * a.action_scalar, uy = r.u.y * a.action_scalar;
       s.px = (p.x + v.x * a.dt) + ((ux * a.dt) * a.dt) * 0.5;
       s.py = (p.y + v.y * a.dt) + ((uy * a.dt) * a.dt) * 0.5;
       s.vx = v.x + ux * a.dt;
       s.vy = v.y + uy * a.dt;
     } else {
-      const float2 u = reinterpret_cast<const float2*>(a.u)[g];
-      const float ux = u.x * a.as_f, uy = u.y * a.as_f;
+      const float ux = r.u.x * a.as_f, uy = r.u.y * a.as_f;
       const float apx = ((ux * a.dt_f) * a.dt_f) * 0.5f;
       const float apy = ((uy * a.dt_f) * a.dt_f) * 0.5f;
       s.px = (p.x + v.x * a.dt) + static_cast<double>(apx);
@@ -157,6 +175,16 @@ __device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
     }
   }
   return s;
+}
+
+template <bool DYN, bool UF64, bool VAR = false>
+__device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
+  if constexpr (DYN && VAR) {
+    const double2* xp = reinterpret_cast<const double2*>(a.x_in) + 2 * g;
+    return load_state_variant<UF64>(a, g, xp[0], xp[1]);
+  } else {
+    return state_from_raw<DYN, UF64>(a, load_raw<DYN, UF64>(a, g));
+  }
 }
 
 // Sorted insertion of (r2, j) into a K-list; ties go to the lower index (stable).
@@ -418,6 +446,9 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 #ifndef GF_STEP_WAVES_PLAIN
 #define GF_STEP_WAVES_PLAIN 7
 #endif
+#ifndef GF_STEP_WAVES_PF
+#define GF_STEP_WAVES_PF 4
+#endif
 #ifndef GF_STEP_WAVES_CTRL
 #define GF_STEP_WAVES_CTRL 6
 #endif
@@ -437,8 +468,10 @@ __device__ unsigned long long gf_stamp_buf[8192 * 16];
 
 // VAR: the flocking variants' switches (StepArgs.variant); without it the FlockingRelative
 // path carries none of their instructions.
-template <bool DYN, bool UF64, bool CTRL, bool VAR>
-__global__ __launch_bounds__(kThreads, VAR ? 1 : (CTRL ? GF_STEP_WAVES_CTRL : GF_STEP_WAVES_PLAIN))
+// PF (1 or 2): each tile's global loads are issued PF tiles ahead (raw x/u in registers,
+// T <= 2 * kThreads), for envs of many tiles; its register budget is that of 4 waves.
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0>
+__global__ __launch_bounds__(kThreads, VAR ? 1 : (PF ? GF_STEP_WAVES_PF : (CTRL ? GF_STEP_WAVES_CTRL : GF_STEP_WAVES_PLAIN)))
 void flock_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
@@ -470,6 +503,20 @@ void flock_step_kernel(StepArgs a) {
     gf_stamp_buf[blockIdx.x * 16 + 15] = (static_cast<unsigned long long>(xcc) << 32) | hw;
   }
 #endif
+
+  // PF: the loads of the tiles PF ahead are in flight (pfa: even tiles, pfb: odd ones
+  // when PF == 2), the first ones issued before the rows' loads
+  [[maybe_unused]] RawState<UF64> pfa[2], pfb[2];
+  auto issue = [&](int j, RawState<UF64>(&pf)[2]) {
+    const int tn = min(T, N - j);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + k * kThreads < tn) pf[k] = load_raw<DYN, UF64>(a, env0 + j + tid + k * kThreads);
+  };
+  if constexpr (PF >= 1) issue(0, pfa);
+  if constexpr (PF == 2) {
+    if (T < N) issue(T, pfb);
+  }
 
   // rows owned by this workgroup (post-update state)
   for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
@@ -533,19 +580,27 @@ void flock_step_kernel(StepArgs a) {
     }
   };
 
-  for (int j0 = 0; j0 < N; j0 += T) {
+  auto tile_body = [&](const int j0, RawState<UF64>(&pf)[2]) {
     const int tc = min(T, N - j0);
     __syncthreads();  // previous tile fully consumed; rows[] visible on first pass
     [[maybe_unused]] const int ti = j0 / T;
     if (ti == 0) GF_STAMP(1);
     float pt = 0.f;
-    for (int t = (a.diag & 16) ? tc : tid; t < tc; t += kThreads) {
-      const St s = load_state<DYN, UF64, VAR>(a, env0 + j0 + t);
+    auto stage = [&](int t, const St& s) {
       tile[t] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
       pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
       svx += s.vx;
       svy += s.vy;
+    };
+    if constexpr (PF >= 1) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (tid + k * kThreads < tc) stage(tid + k * kThreads, state_from_raw<DYN, UF64>(a, pf[k]));
+      if (j0 + PF * T < N) issue(j0 + PF * T, pf);
+    } else {
+      for (int t = (a.diag & 16) ? tc : tid; t < tc; t += kThreads)
+        stage(t, load_state<DYN, UF64, VAR>(a, env0 + j0 + t));
     }
     if (j0 == 0) {
       if (lane < nrows) {
@@ -657,6 +712,14 @@ void flock_step_kernel(StepArgs a) {
       feature_pass(j0, nch);
       if (ti < 1) GF_STAMP(4);
     }
+  };
+  if constexpr (PF == 2) {
+    for (int j0 = 0; j0 < N; j0 += 2 * T) {
+      tile_body(j0, pfa);
+      if (j0 + T < N) tile_body(j0 + T, pfb);
+    }
+  } else {
+    for (int j0 = 0; j0 < N; j0 += T) tile_body(j0, pfa);
   }
   const int jl = ((N - 1) / T) * T;  // first column of the last tile (still in LDS)
   const int nchl = (N - jl + 63) >> 6;
@@ -1207,6 +1270,104 @@ __global__ __launch_bounds__(kThreads) void flock_step_resident_kernel(StepArgs 
 }
 
 // ---------------------------------------------------------------------------------
+// Full-scan kNN row without a sorted insertion per column (the insertions diverge: in a
+// dispersed swarm ~80 % of the columns trigger one in some lane of the wave).
+//   A: float32 r2 to every column, folded into 2K group minima (column j -> group j mod
+//      2K); the K-th smallest group minimum B bounds the row's K-th smallest float32 r2
+//      from above (K distinct columns reach it).
+//   B: every column whose float32 r2 <= B + margin is a candidate (packed u16 indices
+//      in registers). The margin covers the float32 error of both r2 (positions rounded
+//      to float32, coordinates <= P: |r2_f - r2| <= 2^-20.5 P sqrt(r2) + 2^-23 r2 +
+//      2^-44 P^2), so every column of the exact top K is a candidate.
+//   C: the candidates are ranked exactly (float64 r2, ties to the lower index).
+// Returns false (the caller scans with insertions) when the bound is not finite, the
+// coordinates are huge, or the candidates overflow the register list.
+template <int K>
+__device__ __forceinline__ bool knn_bounded_scan(const double2* lpos, const float2* lpf, int N, int i, double pxi,
+                                                 double pyi, float Pf, double (&kr)[K], int (&kj)[K]) {
+  constexpr int G = 2 * K;
+  constexpr int C = K <= 8 ? 32 : 64;  // candidate capacity (C / 2 registers)
+  const float xi = static_cast<float>(pxi), yi = static_cast<float>(pyi);
+  auto r2f = [&](int j) {
+    const float2 q = lpf[j];
+    const float dx = xi - q.x, dy = yi - q.y;
+    return dx * dx + dy * dy;
+  };
+  float m[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) m[g] = __builtin_inff();
+  int j0 = 0;
+  for (; j0 + G <= N; j0 += G) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float r = r2f(j0 + g);
+      m[g] = fminf(m[g], (j0 + g == i) ? __builtin_inff() : r);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (j0 + g < N && j0 + g != i) m[g] = fminf(m[g], r2f(j0 + g));
+  float sk[K];  // the K smallest group minima, branch-free
+#pragma unroll
+  for (int q = 0; q < K; ++q) sk[q] = __builtin_inff();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float v = m[g];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const float lo = fminf(sk[q], v);
+      v = fmaxf(sk[q], v);
+      sk[q] = lo;
+    }
+  }
+  if (!(sk[K - 1] < __builtin_inff()) || !(Pf < 1.0e15f)) return false;
+  const double Bd = sk[K - 1], P = static_cast<double>(Pf) * (1.0 + 0x1p-20);
+  const double lim = Bd + ldexp(P * (sqrt(Bd) + 1.0) + Bd + 1.0, -18) + ldexp(P * P, -39);
+  float thr = static_cast<float>(lim);
+  if (static_cast<double>(thr) < lim) thr = nextafterf(thr, __builtin_inff());
+
+  unsigned cand[C / 2];
+#pragma unroll
+  for (int q = 0; q < C / 2; ++q) cand[q] = 0;
+  int cnt = 0;
+  auto push = [&](int j) {
+    if (cnt < C) {
+#pragma unroll
+      for (int q = C / 2 - 1; q > 0; --q) cand[q] = (cand[q] << 16) | (cand[q - 1] >> 16);
+      cand[0] = (cand[0] << 16) | static_cast<unsigned>(j);
+    }
+    ++cnt;
+  };
+  // 8 columns per round: their loads and compares are independent, and a lane appends
+  // only in the rounds where it has a hit
+  constexpr int U = 8;
+  int jb = 0;
+  for (; jb + U <= N; jb += U) {
+    unsigned hm = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) hm |= static_cast<unsigned>(r2f(jb + u) <= thr && jb + u != i) << u;
+    while (hm) {
+      const int u = __builtin_ctz(hm);
+      hm &= hm - 1;
+      push(jb + u);
+    }
+  }
+  for (int j = jb; j < N; ++j)
+    if (r2f(j) <= thr && j != i) push(j);
+  if (cnt > C) return false;
+  for (int q = 0; q < cnt; ++q) {
+    const int j = static_cast<int>(cand[0] & 0xffffu);
+#pragma unroll
+    for (int p = 0; p + 1 < C / 2; ++p) cand[p] = (cand[p] >> 16) | (cand[p + 1] << 16);
+    cand[C / 2 - 1] >>= 16;
+    const double2 p = lpos[j];
+    const double dx = pxi - p.x, dy = pyi - p.y;
+    knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------
 // Flocking-v0 observation (flocking.py:20-25): the K nearest agents by r2 (self
 // excluded by its infinite r2). One thread per agent. When the step left this
 // state's adjacency behind (adj_bits) and the agent has at least K neighbours, its K
@@ -1228,9 +1389,19 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   // positions: the whole env staged in LDS (N <= kKnnLdsMax), else read from L2
   const double2* gpos = reinterpret_cast<const double2*>(xb);
   double2* lpos = reinterpret_cast<double2*>(smem);
+  float2* lpf = reinterpret_cast<float2*>(lpos + N);  // float32 copies (bounded scan)
+  __shared__ float kred[4];
+  float Pf = 0.f;  // max |coordinate| of the env's float32 positions (LDS only)
   if (LDS) {
-    for (int t = threadIdx.x; t < N; t += kThreads) lpos[t] = gpos[2 * (size_t)t];
-    __syncthreads();
+    float pm = 0.f;
+    for (int t = threadIdx.x; t < N; t += kThreads) {
+      const double2 p = gpos[2 * (size_t)t];
+      lpos[t] = p;
+      const float2 q = make_float2(static_cast<float>(p.x), static_cast<float>(p.y));
+      lpf[t] = q;
+      pm = fmaxf(pm, fmaxf(fabsf(q.x), fabsf(q.y)));
+    }
+    Pf = block_max(pm, kred);  // also publishes the staged positions
   }
   auto pos = [&](int j) -> double2 { return LDS ? lpos[j] : gpos[2 * (size_t)j]; };
   double pxi = 0, pyi = 0;
@@ -1250,8 +1421,10 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   if (fast) {  // rank the neighbours only
     const int Wn = (N + 63) >> 6;
     const uint64_t* bits = a.adj_bits + g * Wn;
+    uint64_t nxt = bits[0];  // one word in flight ahead of the one being ranked
     for (int w = 0; w < Wn; ++w) {
-      uint64_t m = bits[w];
+      uint64_t m = nxt;
+      if (w + 1 < Wn) nxt = bits[w + 1];
       while (m) {
         const int j = (w << 6) + __builtin_ctzll(m);
         m &= m - 1;
@@ -1268,16 +1441,17 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   // lanes busy on distinct rows.
   const int nslow = __syncthreads_count(vi && !fast);
   if (nslow > kKnnFewSlow) {
-    for (int j0 = 0; j0 < N; j0 += 64) {
-      if (vi && !fast) {
-        const int tc = min(64, N - j0);
-        for (int t = 0; t < tc; ++t) {
-          const int j = j0 + t;
-          const double2 p = pos(j);
-          const double dx = pxi - p.x, dy = pyi - p.y;
-          knn_insert<K>(kr, kj, (j == i) ? __builtin_inf() : dx * dx + dy * dy, j);
-        }
+    auto full_scan = [&]() {
+      for (int j = 0; j < N; ++j) {
+        const double2 p = pos(j);
+        const double dx = pxi - p.x, dy = pyi - p.y;
+        knn_insert<K>(kr, kj, (j == i) ? __builtin_inf() : dx * dx + dy * dy, j);
       }
+    };
+    if (LDS) {
+      if (vi && !fast && !knn_bounded_scan<K>(lpos, lpf, N, i, pxi, pyi, Pf, kr, kj)) full_scan();
+    } else if (vi && !fast) {
+      full_scan();
     }
   } else {
     uint64_t todo = __ballot(vi && !fast);
@@ -1470,22 +1644,22 @@ static hipError_t launch_step_split(const StepArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool DYN, bool UF64, bool CTRL, bool VAR>
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   if (a.split && a.N <= kSplitMax) return launch_step_split<DYN, UF64, CTRL, VAR>(a, s);
   size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
   // would allow
-  if (!CTRL && !VAR && a.lds_pad == 0 && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
+  if (!CTRL && !VAR && a.lds_pad == 0 && lds < (size_t)a.lds_floor) lds = a.lds_floor;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int grid = a.B * a.bpe;
-  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR>), dim3(grid), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR, PF>), dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1493,6 +1667,9 @@ template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if (a.variant) return launch_step_tiled<DYN, UF64, CTRL, true>(a, s);
   if (a.resident && !a.adj_bits && !a.degree_out) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
+  if (a.prefetch && a.T <= 2 * kThreads && a.N > a.T && !a.split)
+    return a.prefetch == 2 ? launch_step_tiled<DYN, UF64, CTRL, false, 2>(a, s)
+                           : launch_step_tiled<DYN, UF64, CTRL, false, 1>(a, s);
   return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
 }
 
@@ -1507,13 +1684,20 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
   const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
   const bool lds = a.N <= kKnnLdsMax;
-  const size_t bytes = lds ? (size_t)a.N * 16 : 0;  // the env's positions
+  const size_t bytes = lds ? (size_t)a.N * 24 : 0;  // the env's positions, float64 + float32
   switch (a.K) {
 #define GF_KNN_CASE(k)                                                                            \
   case k:                                                                                         \
-    if (lds)                                                                                      \
+    if (lds) {                                                                                    \
+      static bool attr_##k = false;                                                               \
+      if (!attr_##k) {                                                                            \
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_knn_kernel<k, true>), \
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kKnnLdsMax * 24); \
+        if (e != hipSuccess) return e;                                                            \
+        attr_##k = true;                                                                          \
+      }                                                                                           \
       hipLaunchKernelGGL((flock_knn_kernel<k, true>), dim3(grid), dim3(kThreads), bytes, s, a);  \
-    else                                                                                          \
+    } else                                                                                        \
       hipLaunchKernelGGL((flock_knn_kernel<k, false>), dim3(grid), dim3(kThreads), 0, s, a);     \
     break;
     GF_KNN_CASE(1) GF_KNN_CASE(2) GF_KNN_CASE(3) GF_KNN_CASE(4) GF_KNN_CASE(5) GF_KNN_CASE(6)

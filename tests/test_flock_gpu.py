@@ -472,3 +472,50 @@ def test_degenerate_states_match_oracle():
         ok = ~np.isnan(ref["state_values"])
         np.testing.assert_allclose(sv[ok], ref["state_values"][ok], rtol=1e-5, atol=1e-9)
         h.close()
+
+
+def _knn_cases():
+    rs = np.random.RandomState(21)
+    cases = {}
+    n = 1024
+    x = np.zeros((n, 4))
+    x[:, :2] = rs.uniform(-60, 60, size=(n, 2))  # dispersed: almost every agent below k neighbours
+    cases["dispersed"] = x
+    g = np.stack(np.meshgrid(np.arange(32), np.arange(32)), -1).reshape(-1, 2) * 2.0
+    x = np.zeros((n, 4))
+    x[:, :2] = g[rs.permutation(n)]  # lattice: exact r2 ties everywhere, no neighbours
+    cases["lattice"] = x
+    x = cases["lattice"].copy()
+    x[:, :2] += rs.uniform(-1, 1, size=(n, 2)) * 1e-12  # ties broken below float32 resolution
+    cases["lattice_jitter"] = x
+    x = np.zeros((1000, 4))
+    x[:, :2] = rs.uniform(-40, 40, size=(1000, 2))
+    x[10:20, :2] = x[0, :2]  # coincident agents (r2 = 0 ties); N not a multiple of 2k
+    cases["coincident_ragged"] = x
+    x = cases["dispersed"].copy()
+    x[:, :2] += 3.0e6  # large coordinates: the float32 margin is wide (candidate overflow path)
+    cases["offset"] = x
+    return cases
+
+
+@pytest.mark.parametrize("k", [1, 7, 16])
+@pytest.mark.parametrize("case", ["dispersed", "lattice", "lattice_jitter", "coincident_ragged", "offset"])
+def test_knn_full_scan_rows_vs_oracle(case, k):
+    """Flocking-v0 observation for states where (nearly) every agent has fewer than k
+    neighbours, so each row is a full scan (bounded two-pass scan: float32 group-minimum
+    bound, candidate list, exact float64 ranking): indices bit-exact vs the oracle's
+    stable argsort, ties to the lower index."""
+    x0 = _knn_cases()[case]
+    n = x0.shape[0]
+    xb = np.stack([x0, x0[::-1].copy()])  # second env: reversed agent order (other tie winners)
+    h = nat.FlockHandle(n, 2, n_neighbors=k)
+    h.set_state(xb)
+    h.step(np.zeros((2, n, 2), np.float32), nat.FE_WITH_KNN)
+    for b in range(2):
+        x1 = h.get_state(b)
+        np.testing.assert_array_equal(x1, xb[b])
+        idx, obs = h.knn(b)
+        ridx, robs = orc.knn_observation(x1, k)
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_array_equal(obs, robs.astype(np.float32))
+    h.close()
