@@ -348,6 +348,7 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.N = h->cfg.n_agents;
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
+  k.diag = h->diag;
   hipError_t e = gf::launch_knn(k, h->stream);
   if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
   h->has_knn = true;

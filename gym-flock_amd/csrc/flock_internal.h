@@ -68,6 +68,7 @@ struct KnnArgs {
   int N, B, K;
   const uint64_t* adj_bits;  // (B,N,Wn) adjacency of x from the step, or nullptr
   const int32_t* degree;     // (B,N) with adj_bits
+  int diag;                  // ablation: 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path
 };
 
 struct StatsArgs {

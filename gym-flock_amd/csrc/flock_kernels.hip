@@ -206,6 +206,28 @@ __device__ __forceinline__ void knn_insert(double (&kr)[K], int (&kj)[K], double
   }
 }
 
+// knn_insert for columns that arrive in ascending j with finite r2: a tie keeps the
+// listed (lower) index first, so only the new entry is compared against the list.
+template <int K>
+__device__ __forceinline__ void knn_insert_asc(double (&kr)[K], int (&kj)[K], double r2, int j) {
+  if (r2 < kr[K - 1]) {
+    bool prev = false;
+    double pr = 0.0;
+    int pj = 0;
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+      const bool sw = r2 < kr[m];
+      const double om = kr[m];
+      const int oj = kj[m];
+      kr[m] = sw ? (prev ? pr : r2) : om;
+      kj[m] = sw ? (prev ? pj : j) : oj;
+      prev = sw;
+      pr = om;
+      pj = oj;
+    }
+  }
+}
+
 __device__ __forceinline__ double clip10(double v) {  // np.clip(v, -10, 10); NaN stays NaN
   return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v);
 }
@@ -1283,30 +1305,40 @@ __global__ __launch_bounds__(kThreads) void flock_step_resident_kernel(StepArgs 
 // Returns false (the caller scans with insertions) when the bound is not finite, the
 // coordinates are huge, or the candidates overflow the register list.
 template <int K>
-__device__ __forceinline__ bool knn_bounded_scan(const double2* lpos, const float2* lpf, int N, int i, double pxi,
-                                                 double pyi, float Pf, double (&kr)[K], int (&kj)[K]) {
+__device__ __forceinline__ bool knn_bounded_scan(const double2* lpos, const float2* lpf, int N, int i, int r0,
+                                                 double pxi, double pyi, float Pf, double (&kr)[K], int (&kj)[K]) {
   constexpr int G = 2 * K;
   constexpr int C = K <= 8 ? 32 : 64;  // candidate capacity (C / 2 registers)
-  const float xi = static_cast<float>(pxi), yi = static_cast<float>(pyi);
-  auto r2f = [&](int j) {
-    const float2 q = lpf[j];
-    const float dx = xi - q.x, dy = yi - q.y;
-    return dx * dx + dy * dy;
+  const f2v me = {static_cast<float>(pxi), static_cast<float>(pyi)};
+  const f2v* lp = reinterpret_cast<const f2v*>(lpf);
+  auto r2f = [&](int j) {  // packed: one subtract and one multiply for x and y
+    const f2v d = me - lp[j];
+    const f2v d2 = d * d;
+    return d2.x + d2.y;
   };
+  // The columns split into three ranges: the wave's own 64 rows [r0, r1) (each lane's
+  // self is among them: checked) and the rest (no check). r0 is wave-uniform.
+  const int r1 = min(N, r0 + 64);
   float m[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) m[g] = __builtin_inff();
-  int j0 = 0;
-  for (; j0 + G <= N; j0 += G) {
+  // groups: any partition into G disjoint column sets gives a valid bound
+  auto groups = [&](int s, int e, auto self) {
+    int j = s;
+    for (; j + G <= e; j += G) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float r = r2f(j0 + g);
-      m[g] = fminf(m[g], (j0 + g == i) ? __builtin_inff() : r);
+      for (int g = 0; g < G; ++g) {
+        const float r = r2f(j + g);
+        m[g] = fminf(m[g], (decltype(self)::value && j + g == i) ? __builtin_inff() : r);
+      }
     }
-  }
 #pragma unroll
-  for (int g = 0; g < G; ++g)
-    if (j0 + g < N && j0 + g != i) m[g] = fminf(m[g], r2f(j0 + g));
+    for (int g = 0; g < G; ++g)
+      if (j + g < e && !(decltype(self)::value && j + g == i)) m[g] = fminf(m[g], r2f(j + g));
+  };
+  groups(0, r0, std::false_type{});
+  groups(r0, r1, std::true_type{});
+  groups(r1, N, std::false_type{});
   float sk[K];  // the K smallest group minima, branch-free
 #pragma unroll
   for (int q = 0; q < K; ++q) sk[q] = __builtin_inff();
@@ -1340,20 +1372,26 @@ __device__ __forceinline__ bool knn_bounded_scan(const double2* lpos, const floa
   };
   // 8 columns per round: their loads and compares are independent, and a lane appends
   // only in the rounds where it has a hit
-  constexpr int U = 8;
-  int jb = 0;
-  for (; jb + U <= N; jb += U) {
-    unsigned hm = 0;
+  auto cands = [&](int s, int e, auto self) {
+    constexpr int U = 8;
+    int jb = s;
+    for (; jb + U <= e; jb += U) {
+      unsigned hm = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) hm |= static_cast<unsigned>(r2f(jb + u) <= thr && jb + u != i) << u;
-    while (hm) {
-      const int u = __builtin_ctz(hm);
-      hm &= hm - 1;
-      push(jb + u);
+      for (int u = 0; u < U; ++u)
+        hm |= static_cast<unsigned>(r2f(jb + u) <= thr && !(decltype(self)::value && jb + u == i)) << u;
+      while (hm) {
+        const int u = __builtin_ctz(hm);
+        hm &= hm - 1;
+        push(jb + u);
+      }
     }
-  }
-  for (int j = jb; j < N; ++j)
-    if (r2f(j) <= thr && j != i) push(j);
+    for (int j = jb; j < e; ++j)
+      if (r2f(j) <= thr && !(decltype(self)::value && j == i)) push(j);
+  };
+  cands(0, r0, std::false_type{});
+  cands(r0, r1, std::true_type{});
+  cands(r1, N, std::false_type{});
   if (cnt > C) return false;
   for (int q = 0; q < cnt; ++q) {
     const int j = static_cast<int>(cand[0] & 0xffffu);
@@ -1417,7 +1455,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
     kj[m] = INT_MAX;
   }
   const size_t g = (size_t)b * N + i;
-  const bool fast = vi && a.adj_bits && a.degree[g] >= K;
+  const bool fast = vi && a.adj_bits && a.degree[g] >= K && !(a.diag & 0x8000);
   if (fast) {  // rank the neighbours only
     const int Wn = (N + 63) >> 6;
     const uint64_t* bits = a.adj_bits + g * Wn;
@@ -1430,8 +1468,17 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
         m &= m - 1;
         const double2 p = pos(j);
         const double dx = pxi - p.x, dy = pyi - p.y;
-        knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
+        if (a.diag & 0x4000) {  // ablation: no ranking (outputs: the last neighbour K times)
+          kr[0] += dx * dx + dy * dy;
+          kj[0] = j;
+        } else {
+          knn_insert_asc<K>(kr, kj, dx * dx + dy * dy, j);
+        }
       }
+    }
+    if (a.diag & 0x4000) {
+#pragma unroll
+      for (int m = 1; m < K; ++m) kj[m] = kj[0];
     }
   }
   // Agents the neighbour ranking cannot serve: when a workgroup holds only a few, its
@@ -1449,7 +1496,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
       }
     };
     if (LDS) {
-      if (vi && !fast && !knn_bounded_scan<K>(lpos, lpf, N, i, pxi, pyi, Pf, kr, kj)) full_scan();
+      if (vi && !fast && !knn_bounded_scan<K>(lpos, lpf, N, i, __builtin_amdgcn_readfirstlane(i - lane), pxi, pyi, Pf, kr, kj)) full_scan();
     } else if (vi && !fast) {
       full_scan();
     }

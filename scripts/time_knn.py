@@ -14,6 +14,8 @@ from gym_flock.init_states import synthetic_batch  # noqa: E402
 
 N, B, K = int(os.environ.get("N", 1024)), int(os.environ.get("B", 256)), 30
 h = nat.FlockHandle(N, B, n_neighbors=7)
+if os.environ.get("DIAG"):  # ablation switches (fe_diag), e.g. DIAG=0x4000
+    h.diag_switches(int(os.environ["DIAG"], 0))
 x0 = synthetic_batch(B, N)
 h.set_actions(np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
 h.set_state(x0)
