@@ -239,6 +239,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-controller-line", action="store_true")
     ap.add_argument("--no-packed-line", action="store_true")
+    ap.add_argument("--no-knn-line", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-rank path (gloo rendezvous + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
@@ -356,6 +357,36 @@ def main():
             "achieved_GBs": pk_bytes / (pk_ms * 1e-3) / 1e9 if pk_ms > 0 else None,
             "note": "adjacency as bits (N*ceil(N/64)*8 B) + int32 degree per env instead of the dense "
                     "float32 network; the pair work, not HBM, bounds this mode"}
+
+    # Flocking-v0 (§8f rank 1): the same step plus the 7-nearest-neighbour observation
+    # (flocking.py:20-25), dense network kept; a second handle with n_neighbors=7
+    if not args.no_knn_line:
+        envk = VecFlockingRelative(B, N, device=local_rank, env_offset=rank * B, n_neighbors=7)
+        envk.reset(seed=0)
+        envk.set_actions(u)
+        for _ in range(min(W, 5)):
+            envk.step(resident=True, knn=True)
+        envk.sync()
+        if dist is not None:
+            dist.barrier()
+        t6 = time.perf_counter()
+        for _ in range(K):
+            envk.step(resident=True, knn=True)
+        envk.sync()
+        t7 = time.perf_counter()
+        if dist is not None:
+            dist.barrier()
+        ek = t7 - t6
+        if dist is not None:
+            import torch
+            t = torch.tensor([ek], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ek = float(t.item())
+        extra["flocking_v0_knn7"] = {
+            "value": world * B * N * K / ek, "unit": "agent-steps/s", "ms_per_step": 1e3 * ek / K,
+            "note": "Flocking-v0 step: FlockingRelative step + 7-NN observation (idx + obs), from the "
+                    "synthetic init under the same random actions; two launches per step"}
+        envk.close()
 
     if rank == 0:
         value = world * B * N * K / elapsed
