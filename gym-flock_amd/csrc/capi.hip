@@ -56,7 +56,7 @@ struct fe_handle {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_s2 = nullptr;           // stream2 -> stream join
   hipEvent_t ev_main = nullptr;         // stream -> stream2 ordering
-  int nsplit = 2;                       // launches per step (fe_set_streams, GYMFLOCK_STREAMS)
+  int nsplit = 2;                       // launches per step (fe_set_streams)
   bool s2_pending = false;              // stream2 holds work `stream` has not waited for
   bool main_dirty = true;               // `stream` holds work stream2 has not waited for
   bool other_work = true;               // non-step work was enqueued since the last step:
@@ -81,18 +81,12 @@ struct fe_handle {
   int u_resident_f64 = -1;              // dtype of the resident actions (-1: none)
   bool has_state = false, has_ctrl = false, has_obs = false, has_knn = false;
   int R = 0, T = 0, bpe = 0;
-  int resident = 0, spe = 1, rps = 0;  // env-resident kernel geometry
   size_t BN = 0;
-  // kernel timing (bench roofline)
-  int diag = 0;                         // ablation switches for every step launch
-  int lds_pad = 0;                      // occupancy tuning (GYMFLOCK_LDS_PAD)
+  int diag = 0;                         // ablation switches (diagnostic build only, fe_diag)
   int R_ctrl = 0;                       // rows per block of the step + controller kernel
-  int prefetch = 0;                     // tile loads one tile ahead (GYMFLOCK_PREFETCH)
-  int lds_floor = (int)gf::kStepLdsPlainFloor;  // plain-step occupancy cap (GYMFLOCK_LDS_FLOOR)
-  int split = 0;                        // split-phase step kernel (opt-in GYMFLOCK_SPLIT=1; slower)
-  int T_split = 512;                    // its phase-B tile (GYMFLOCK_SPLIT_TILE)
-  int store_fast[2] = {0, 1};           // fast network store loop, plain step / with controller
-                                        // (GYMFLOCK_STORE_FAST=<plain><ctrl>, e.g. "01")
+  int prefetch = 0;                     // tile loads one tile ahead (N >= 16 tiles)
+  int store_fast[2] = {0, 1};           // fast network store loop: plain step / with controller
+  // kernel timing (bench roofline)
   bool timing = false;
   int timing_stride = 1;                // sample every timing_stride-th launch
   int64_t timing_count = 0;
@@ -242,23 +236,15 @@ gf::StepArgs base_args(fe_handle* h) {
   a.R = h->R;
   a.T = h->T;
   a.bpe = h->bpe;
-  a.resident = h->resident;
-  a.spe = h->spe;
-  a.rps = h->rps;
   a.mean_pooling = h->cfg.mean_pooling;
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
-  a.lds_pad = h->lds_pad;
-  a.lds_floor = h->lds_floor;
   a.prefetch = h->prefetch;
-  a.split = h->split && h->cfg.n_agents <= gf::kSplitMax;
-  if (a.split) a.T = h->T_split;
   a.u_scale = h->cfg.action_scalar;
   a.us_f = a.as_f;
   a.x_scale = 1.0;
   if (h->has_variant || h->dt_per_env) {
     a.variant = 1;
-    a.resident = 0;  // variants run on the tiled kernel
     if (h->has_variant) {
       a.n_frozen = h->var.n_frozen;
       a.n_vel_zero = h->var.n_vel_zero;
@@ -276,7 +262,7 @@ gf::StepArgs base_args(fe_handle* h) {
 
 int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
   gf::StepArgs a = a_in;
-  if (ctrl && !a.variant && !a.resident && !a.split && h->R_ctrl != a.R) {
+  if (ctrl && !a.variant && h->R_ctrl != a.R) {
     a.R = h->R_ctrl;
     a.bpe = (a.N + a.R - 1) / a.R;
   }
@@ -397,61 +383,12 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   h->BN = B * N;
   h->R = gf::step_rows_per_block(cfg->n_agents);
   h->T = gf::step_tile(cfg->n_agents);
-  // tuning overrides (power-of-two rows 4..64; tile a multiple of 64, <= 1024)
-  if (const char* e = getenv("GYMFLOCK_ROWS")) {
-    const int r = atoi(e);
-    if (r >= 4 && r <= 64 && (r & (r - 1)) == 0) h->R = r;
-  }
-  // env-resident kernel (opt-in, GYMFLOCK_RESIDENT=1, N <= 1024): measured 226-234 us vs
-  // 213-217 us for the tiled kernel at 256 x 1024, so off by default.
-  // GYMFLOCK_RESIDENT_WGS sets its target workgroup count (default 3 per CU).
-  h->resident = 0;
-  if (const char* e = getenv("GYMFLOCK_RESIDENT")) h->resident = atoi(e) != 0 && cfg->n_agents <= gf::kResidentMax;
-  {
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
-      cus = prop.multiProcessorCount;
-    int target = 3 * cus;
-    if (const char* e = getenv("GYMFLOCK_RESIDENT_WGS")) target = atoi(e) > 0 ? atoi(e) : target;
-    gf::step_resident_geometry(cfg->n_agents, cfg->n_envs, target, &h->spe, &h->rps);
-  }
-  if (const char* e = getenv("GYMFLOCK_LDS_PAD")) h->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
-  if (const char* e = getenv("GYMFLOCK_LDS_FLOOR")) h->lds_floor = atoi(e) >= 0 ? atoi(e) : 0;
-  if (const char* e = getenv("GYMFLOCK_SPLIT")) h->split = atoi(e) != 0;
-  {
-    const int full = ((cfg->n_agents + 63) / 64) * 64;
-    int t = 512;
-    if (const char* e = getenv("GYMFLOCK_SPLIT_TILE")) {
-      const int v = atoi(e);
-      if (v >= 64 && v <= gf::kTileMax && v % 64 == 0) t = v;
-    }
-    h->T_split = t < full ? t : full;
-  }
-  if (const char* e = getenv("GYMFLOCK_STORE_FAST")) {
-    if (e[0] == '0' || e[0] == '1') h->store_fast[0] = e[0] - '0';
-    if (e[0] && (e[1] == '0' || e[1] == '1')) h->store_fast[1] = e[1] - '0';
-  }
-  if (const char* e = getenv("GYMFLOCK_TILE")) {
-    const int t = atoi(e);
-    if (t >= 64 && t <= gf::kTileMax && t % 64 == 0) {
-      const int full = ((cfg->n_agents + 63) / 64) * 64;
-      h->T = t < full ? t : full;
-    }
-  }
-
   // tile loads issued a tile ahead: 1604 -> 1527 us at N=8192 (16 tiles); no gain at 2-8
   // tiles, where its registers cost occupancy instead
   h->prefetch = (cfg->n_agents + h->T - 1) / h->T >= 16 ? 1 : 0;
-  if (const char* e = getenv("GYMFLOCK_PREFETCH")) h->prefetch = atoi(e) == 2 ? 2 : atoi(e) != 0;
   // step + controller: 64-row blocks at 513..1024 agents (194.7 vs 200.1 us at config 2;
   // the plain step stays at 32: 198 vs 184)
-  h->R_ctrl = (getenv("GYMFLOCK_ROWS") == nullptr && h->R == 32 && cfg->n_agents > 512 && cfg->n_agents <= 1024)
-                  ? 64 : h->R;
-  if (const char* e = getenv("GYMFLOCK_ROWS_CTRL")) {
-    const int r = atoi(e);
-    if (r >= 4 && r <= 64 && (r & (r - 1)) == 0) h->R_ctrl = r;
-  }
+  h->R_ctrl = (h->R == 32 && cfg->n_agents > 512 && cfg->n_agents <= 1024) ? 64 : h->R;
   h->bpe = (cfg->n_agents + h->R - 1) / h->R;
   if ((size_t)h->bpe * B > 0x7fffffff) {
     delete h;
@@ -480,7 +417,6 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     release(h);
     return fail_hip("event create", e);
   }
-  if (const char* e = getenv("GYMFLOCK_STREAMS")) h->nsplit = atoi(e) == 1 ? 1 : 2;
   if ((e = hipMemsetAsync(h->reward_ring, 0, sizeof(double) * kRewardSlots * B, h->stream)) != hipSuccess ||
       (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
     release(h);
@@ -609,7 +545,10 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   } else if (!u) {
     return fail(GF_EINVAL, "null action pointer");
   } else if (flags & FE_U_DEVICE) {
+    // the caller may have written the actions on the handle's stream (fe_buffers.stream):
+    // the second half's stream waits for it (an event, no host sync)
     up = u;
+    h->main_dirty = true;
   } else {
     // the previous step's second half may still read h->u: copy after it
     if (int rc = join_s2(h)) return rc;
@@ -805,6 +744,9 @@ int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs) {
 
 int fe_device_buffers(fe_handle* h, fe_buffers* out) {
   if (!h || !out) return fail(GF_EINVAL, "null argument");
+  // a reader on out->stream sees whole steps (both halves), and the next split step's
+  // second half waits for what the caller enqueues there
+  if (int rc = use_dev(h)) return rc;
   out->x = h->x[h->cur];
   out->state_values = h->sv;
   out->network = h->net;
@@ -823,6 +765,8 @@ int fe_sync(fe_handle* h) {
   if (int rc = use_dev(h)) return rc;
   GF_HIP(hipStreamSynchronize(h->stream));
   if (h->comm_stream) GF_HIP(hipStreamSynchronize(h->comm_stream));
+  // both streams are idle now: the next step may split at once (nothing to wait on)
+  h->main_dirty = h->other_work = false;
   return GF_OK;
 }
 
@@ -840,7 +784,11 @@ int fe_join(fe_handle* h) {
 
 int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches) {
   if (!h) return fail(GF_EINVAL, "null handle");
+  const bool ow = h->other_work;
   if (int rc = use_dev(h)) return rc;
+  // the window's event marks are not work a step waits on: the first step of a window
+  // splits like the rest (main_dirty stays set, so stream2 starts after the mark)
+  h->other_work = ow;
   if (enable >= 1) {  // start: time every enable-th step launch
     GF_HIP(hipStreamSynchronize(h->stream));
     h->ev_used = 0;
@@ -885,8 +833,12 @@ int fe_diag(fe_handle* h, int what, int reps, double* avg_ms) {
   if (!h || reps < 1) return fail(GF_EINVAL, "bad argument");
   if (int rc = use_dev(h)) return rc;
   if (what >= 0x10000) {  // set ablation switches (low 16 bits) for subsequent step launches
+#ifdef GF_DIAG
     h->diag = what & 0xffff;
     return GF_OK;
+#else
+    return fail(GF_EINVAL, "ablation switches need the diagnostic build (make -C gym-flock_amd/csrc diag)");
+#endif
   }
   hipEvent_t e0, e1;
   GF_HIP(hipEventCreate(&e0));

@@ -298,7 +298,6 @@ int cov_create(const cov_config* cfg, cov_handle** out) {
     cov_release(h);
     return cfail(GF_EHIP, "stream create failed");
   }
-  if (const char* e = getenv("GYMFLOCK_STREAMS")) h->nsplit = atoi(e) == 1 ? 1 : 2;
   if ((rc = calloc_dev(&h->ntg, B)) || (rc = calloc_dev(&h->tgt, B * Tm * 2)) || (rc = calloc_dev(&a.nbr, B * Tm * 4)) ||
       (rc = calloc_dev(&a.cnt, B * Tm)) || (rc = calloc_dev(&a.n_motion, B)) || (rc = calloc_dev(&a.xr, B * R * 2)) ||
       (rc = calloc_dev(&a.cur, B * R)) || (rc = calloc_dev(&a.visited, B * Tm)) || (rc = calloc_dev(&a.nvisited, B)) ||
@@ -458,6 +457,7 @@ int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launch
     h->timing_count = 0;
     h->tw_steps = 0;  // split steps: one window, device time per step
     CV_HIP(hipEventRecord(h->tw[0], h->stream));
+    h->other_work = false;  // both streams idle: the first timed step splits like the rest
     return GF_OK;
   }
   if (h->tw_steps > 0) {
@@ -698,10 +698,18 @@ int cov_get_graphs_tuple(cov_handle* h, int32_t* n_node, float* nodes, int32_t* 
   return check_err(h);
 }
 
+int cov_set_streams(cov_handle* h, int n) {
+  if (!h || (n != 1 && n != 2)) return cfail(GF_EINVAL, "n must be 1 or 2");
+  if (int rc = use(h)) return rc;
+  h->nsplit = n;
+  return GF_OK;
+}
+
 int cov_sync(cov_handle* h) {
   if (!h) return cfail(GF_EINVAL, "null handle");
   if (int rc = use(h)) return rc;
   CV_HIP(hipStreamSynchronize(h->stream));
+  h->main_dirty = h->other_work = false;  // both streams idle: the next step may split
   return check_err(h);
 }
 

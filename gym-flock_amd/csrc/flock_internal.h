@@ -5,12 +5,18 @@
 
 namespace gf {
 
+// Ablation switches (StepArgs / KnnArgs .diag, timing experiments that give wrong
+// outputs) exist only in the diagnostic build (make diag: -DGF_DIAG); the product build
+// compiles every such branch out.
+#ifdef GF_DIAG
+#define GF_ABLATE(args, bits) (((args).diag & (bits)) != 0)
+#else
+#define GF_ABLATE(args, bits) false
+#endif
+
 constexpr int kThreads = 256;   // 4 wave64s per workgroup
 constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float64 state)
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
-constexpr int kResidentRows = 32;   // rows per block of the env-resident kernel
-constexpr int kResidentMax = 1024;  // largest N whose env fits the resident kernel's LDS
-constexpr int kSplitMax = 2048;     // largest N of the split-phase kernel (float32 env in LDS)
 constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many full-scan rows per workgroup
@@ -33,14 +39,10 @@ struct StepArgs {
   int T;                  // agents per LDS tile (multiple of 64)
   int bpe;                // workgroups per env = ceil(N / R)
   int mean_pooling, centralized;
-  int resident;           // 1: env-resident kernel (N <= kResidentMax)
-  int spe, rps;           // resident kernel: slices per env, rows per slice
-  int lds_pad;            // extra dynamic LDS bytes (occupancy control; tuning knob)
-  int lds_floor;          // plain step: dynamic LDS raised to at least this (occupancy cap)
-  int split;              // 1: split-phase kernel (N <= kSplitMax, see flock_step_split_kernel)
   int prefetch;           // tiled step issues each tile's loads one tile ahead (T <= 512)
   int store_fast;         // network rows by the fast bit-extract loop (N % 1024 == 0)
-  int diag;               // ablation switches (0 in production): 2 skip feature pass,
+  int diag;               // ablation switches, read only by the diagnostic build (GF_ABLATE):
+                          // 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
                           // unwritten: timing only), 16 skip tile loads (timing only),
                           // 64 / 128 generic / fast network store loop (A/B), 256 no
@@ -84,9 +86,6 @@ struct StatsArgs {
 int step_rows_per_block(int N);
 int step_tile(int N);
 size_t step_lds_bytes(int N, int R, int T, bool ctrl);
-size_t split_lds_bytes(int N, int R, int T, bool ctrl);
-size_t step_resident_lds_bytes(int N, bool ctrl);
-void step_resident_geometry(int N, int B, int target_wgs, int* spe, int* rps);
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);

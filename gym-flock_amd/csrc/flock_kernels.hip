@@ -24,6 +24,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <atomic>
+
 #include <type_traits>
 
 namespace gf {
@@ -288,13 +290,6 @@ __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m,
   w1 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m >> 32), l, static_cast<int>(w1)));
 }
 
-// Split-phase kernel LDS: one region that holds the env's float32 positions in phase A
-// and a float64 tile of T agents in phase B, then the adjacency (and controller) bits.
-__host__ __device__ inline size_t split_region_bytes(int N, int T) {
-  const size_t p = (size_t)N * 8, t = (size_t)T * sizeof(St);
-  return ((p > t ? p : t) + 15) & ~static_cast<size_t>(15);
-}
-
 // Dense network rows adj/deg of one row block (flocking_relative.py:120-122), 16-byte
 // stores (1 KiB per wave instruction); the block's rows are one contiguous range
 // starting at global row grow0.
@@ -309,7 +304,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
   // its nibble sits at a fixed bit offset of 32-bit words 8 apart; four words are read
   // ahead and each float becomes sign-extended bit & bits(1/deg) (2 VALU per float).
   // The host picks it per kernel (StepArgs.store_fast; diag 64 / 128 force it off / on).
-  const bool fast = (N & 1023) == 0 && !(a.diag & (4 | 64)) && (a.store_fast || (a.diag & 128));
+  const bool fast = (N & 1023) == 0 && !GF_ABLATE(a, (4 | 64)) && (a.store_fast || GF_ABLATE(a, 128));
   const unsigned* bits32 = reinterpret_cast<const unsigned*>(adj);
   const int hl = lane & 15;
   const int wsel = 2 * (lane >> 4) + (hl >> 3);  // 32-bit word of column block m = 0
@@ -320,7 +315,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
     const float iv = inv[r];
     const uint64_t* bits = adj + (size_t)r * Wn;
     float* rowp = a.network + (grow0 + r) * (size_t)N;
-    if (a.diag & 1024) {  // timing only: constant rows, no bit reads
+    if (GF_ABLATE(a, 1024)) {  // timing only: constant rows, no bit reads
       f4v* r4 = reinterpret_cast<f4v*>(rowp);
       for (int q = lane; q < (N >> 2); q += 64) r4[q] = f4v{iv, 0.f, iv, 0.f};
       continue;
@@ -350,7 +345,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
         const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
         const f4v v = {(nib & 1u) ? iv : 0.0f, (nib & 2u) ? iv : 0.0f, (nib & 4u) ? iv : 0.0f,
                        (nib & 8u) ? iv : 0.0f};
-        if (a.diag & 4)
+        if (GF_ABLATE(a, 4))
           __builtin_nontemporal_store(v, &r4[q]);
         else
           r4[q] = v;
@@ -389,7 +384,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
   const double Svx = block_sum(svx, red);
   const double Svy = block_sum(svy, red);
 
-  if (writer && !(a.diag & 256)) {  // diag 256: skip the per-row outputs (timing only)
+  if (writer && !GF_ABLATE(a, 256)) {  // diag 256: skip the per-row outputs (timing only)
     const size_t g = env0 + i_row;
     if (a.state_values) {
       float* sv = a.state_values + g * 6;
@@ -435,7 +430,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 
   // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
   // first row block; single-tile envs read the velocities from the LDS tile
-  if (a.reward && i0 == 0 && !(a.diag & 512)) {  // diag 512: skip the reward (timing only)
+  if (a.reward && i0 == 0 && !GF_ABLATE(a, 512)) {  // diag 512: skip the reward (timing only)
     const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
     double qx = 0, qy = 0;
     if (N <= T) {
@@ -509,7 +504,7 @@ void flock_step_kernel(StepArgs a) {
 
   // the plain step deals the reward blocks out first (195 vs 200 us at config 2; with
   // the controller it measured 1 us slower); diag 8192 forces the plain remap (A/B)
-  const int L = (!CTRL && !(a.diag & 8192)) ? xcd_remap_reward_first(blockIdx.x, gridDim.x, a.bpe)
+  const int L = (!CTRL && !GF_ABLATE(a, 8192)) ? xcd_remap_reward_first(blockIdx.x, gridDim.x, a.bpe)
                                             : xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / a.bpe;
   const int i0 = (L - b * a.bpe) * R;
@@ -586,7 +581,7 @@ void flock_step_kernel(StepArgs a) {
   // (Dealing a row's bits round robin over its S threads balances the slices but its
   // cursor bookkeeping cost more than it saved: 266 vs 215 us, DESIGN.md.)
   auto feature_pass = [&](int j0, int nch) {
-    if (!frow || (a.diag & 2)) return;
+    if (!frow || GF_ABLATE(a, 2)) return;
     const St me = rows[fr];
     const int wpt = (nch + S - 1) / S;
     const int wb = fs * wpt, we = min(nch, wb + wpt);
@@ -621,7 +616,7 @@ void flock_step_kernel(StepArgs a) {
         if (tid + k * kThreads < tc) stage(tid + k * kThreads, state_from_raw<DYN, UF64>(a, pf[k]));
       if (j0 + PF * T < N) issue(j0 + PF * T, pf);
     } else {
-      for (int t = (a.diag & 16) ? tc : tid; t < tc; t += kThreads)
+      for (int t = GF_ABLATE(a, 16) ? tc : tid; t < tc; t += kThreads)
         stage(t, load_state<DYN, UF64, VAR>(a, env0 + j0 + t));
     }
     if (j0 == 0) {
@@ -651,7 +646,7 @@ void flock_step_kernel(StepArgs a) {
     }
     ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
     bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
-    for (int cp = (a.diag & 8) ? npair : wid; cp < npair; cp += 4) {
+    for (int cp = GF_ABLATE(a, 8) ? npair : wid; cp < npair; cp += 4) {
       const int ca = cp << 1;
       const bool has_b = ca + 1 < nch;
       const int jta = (ca << 6) + lane, jtb = jta + 64;
@@ -782,513 +777,6 @@ void flock_step_kernel(StepArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   GF_STAMP(11);
 #endif
-}
-
-// ---------------------------------------------------------------------------------
-// Split-phase form of the same step (N <= kSplitMax): everything the network rows need
-// comes first and everything else after their stores are issued.
-//   A: the env's float32 positions (one load round trip, the rows included), pass 1
-//      over every column, degrees, the network stores;
-//   B: float64 tiles of the env over the same LDS (the positions are dead by then), the
-//      feature / controller pass, the per-row outputs and the reward.
-// A workgroup thus reaches its stores after one load and one bit pass instead of three
-// dependent loads and two bit passes with a feature pass between them; its phase-B loads
-// queue behind its own stores, which is time its stores drain anyway. Same numerics as
-// flock_step_kernel (float32 prefilter + float64 band decisions, float64 features in
-// ascending column order per slice).
-template <bool DYN, bool UF64, bool CTRL, bool VAR>
-__global__ __launch_bounds__(kThreads) void flock_step_split_kernel(StepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = a.N, R = a.R, T = a.T;
-  const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
-  const size_t region = split_region_bytes(N, T);
-  float2* pos32 = reinterpret_cast<float2*>(smem);              // A: float32 positions, N
-  St* tile = reinterpret_cast<St*>(smem);                       // B: float64 state, T
-  uint64_t* adj = reinterpret_cast<uint64_t*>(smem + region);   // R x Wn adjacency bits
-  uint64_t* nearb = adj + (size_t)R * Wn;                       // R x Wn controller bits
-  double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)R * Wn : 0));
-  float* redf = reinterpret_cast<float*>(red + 4);
-  float* inv = reinterpret_cast<float*>(red + 8);
-
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = L / a.bpe;
-  const int i0 = (L - b * a.bpe) * R;
-  const int nrows = min(R, N - i0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const size_t env0 = (size_t)b * N;
-  GF_STAMP(0);
-#ifdef GF_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < 8192) {
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-    gf_stamp_buf[blockIdx.x * 16 + 15] = (static_cast<unsigned long long>(xcc) << 32) | hw;
-  }
-#endif
-
-  // ---- phase A: positions of the whole env, float32 (post-update state)
-  float pt = 0.f;
-  for (int t = (a.diag & 16) ? N : tid; t < N; t += kThreads) {
-    const St s = load_state<DYN, UF64, VAR>(a, env0 + t);
-    const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
-    pos32[t] = make_float2(fx, fy);
-    pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
-  }
-  const float Pt = block_max(pt, redf);  // also the barrier that publishes pos32
-  GF_STAMP(2);
-  float rx32 = 0.f, ry32 = 0.f;  // lane r: row r's float32 position
-  if (lane < nrows) {
-    const float2 p = pos32[i0 + lane];
-    rx32 = p.x;
-    ry32 = p.y;
-  }
-  const float Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
-
-  // pass 1 over every column of the env (flock_step_kernel's pass 1 with j0 = 0)
-  const int npair = (Wn + 1) >> 1;
-  const float pu = uniform_f(Pr) + uniform_f(Pt);
-  Band ba{-__builtin_inff(), __builtin_inff()}, bn = ba;  // huge/non-finite: all exact
-  if (pu < 1.0e5f) {
-    const double delta = ldexp(static_cast<double>(pu) * (1.0 + 1e-6) + 4.0, -20);
-    ba = make_band(a.cr2, delta);
-    bn = make_band(a.cr, delta);
-  }
-  ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
-  bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
-  for (int cp = (a.diag & 8) ? npair : wid; cp < npair; cp += 4) {
-    const int ca = cp << 1;
-    const bool has_b = ca + 1 < Wn;
-    const int jta = (ca << 6) + lane, jtb = jta + 64;
-    const bool va = jta < N, vb = jtb < N;
-    // columns past the env sit far away: never adjacent, never in the band
-    const float2 qa = va ? pos32[jta] : make_float2(1.0e18f, 1.0e18f);
-    const float2 qb = vb ? pos32[jtb] : make_float2(1.0e18f, 1.0e18f);
-    const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
-    unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
-    uint64_t band = 0;
-    for (int r = 0; r < nrows; ++r) {
-      const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-      const f2v dx = xi - qx, dy = yi - qy;
-      const f2v d2 = dx * dx + dy * dy;
-      const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
-      const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
-      band |= (Aa ^ Ma) | (Ab ^ Mb);
-      put_lane(wa0, wa1, Aa, r);
-      put_lane(wb0, wb1, Ab, r);
-      if constexpr (CTRL) {
-        const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
-        const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
-        band |= (Na ^ NMa) | (Nb ^ NMb);
-        put_lane(na0, na1, Na, r);
-        put_lane(nb0, nb1, Nb, r);
-      }
-    }
-    if (band) {  // rare: some pair is within the float32 error band of a threshold;
-                 // the float64 states come from global memory (L2) here
-      const St oa = va ? load_state<DYN, UF64, VAR>(a, env0 + jta) : St{1.0e300, 1.0e300, 0, 0};
-      const St ob = vb ? load_state<DYN, UF64, VAR>(a, env0 + jtb) : St{1.0e300, 1.0e300, 0, 0};
-      for (int r = 0; r < nrows; ++r) {
-        const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-        const f2v dx = xi - qx, dy = yi - qy;
-        const f2v d2 = dx * dx + dy * dy;
-        const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
-        const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
-        uint64_t Na = 0, Nb = 0, NMa = 0, NMb = 0;
-        if constexpr (CTRL) {
-          Na = __ballot(d2.x <= bn.lo);
-          Nb = __ballot(d2.y <= bn.lo);
-          NMa = __ballot(!(d2.x > bn.hi));
-          NMb = __ballot(!(d2.y > bn.hi));
-        }
-        if ((Aa ^ Ma) | (Ab ^ Mb) | (Na ^ NMa) | (Nb ^ NMb)) {
-          const St ri = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
-          const double dxa = ri.px - oa.px, dya = ri.py - oa.py;
-          const double dxb = ri.px - ob.px, dyb = ri.py - ob.py;
-          const double r2a = dxa * dxa + dya * dya, r2b = dxb * dxb + dyb * dyb;
-          put_lane(wa0, wa1, Aa | (__ballot(r2a < a.cr2) & (Aa ^ Ma)), r);
-          put_lane(wb0, wb1, Ab | (__ballot(r2b < a.cr2) & (Ab ^ Mb)), r);
-          if constexpr (CTRL) {
-            put_lane(na0, na1, Na | (__ballot(r2a <= a.cr) & (Na ^ NMa)), r);
-            put_lane(nb0, nb1, Nb | (__ballot(r2b <= a.cr) & (Nb ^ NMb)), r);
-          }
-        }
-      }
-    }
-    if (lane < nrows) {
-      // the diagonal (self, r2 = 0 here; inf in the reference) is never a neighbour
-      const int dl = i0 + lane - (ca << 6);
-      const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
-      const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
-      uint64_t* arow = adj + (size_t)lane * Wn + ca;
-      arow[0] = ((static_cast<uint64_t>(wa1) << 32) | wa0) & ka;
-      if (has_b) arow[1] = ((static_cast<uint64_t>(wb1) << 32) | wb0) & kb;
-      if constexpr (CTRL) {
-        uint64_t* nrow = nearb + (size_t)lane * Wn + ca;
-        nrow[0] = ((static_cast<uint64_t>(na1) << 32) | na0) & ka;
-        if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
-      }
-    }
-  }
-  __syncthreads();
-  GF_STAMP(6);
-
-  // feature-pass thread mapping: S word-slices per row
-  const int S = kThreads / R;
-  const int fr = tid / S, fs = tid - fr * S;
-  const bool frow = fr < nrows;
-  // degree of each row -> 1/deg for the mean-pooled network (:120-122)
-  {
-    int deg = 0;
-    if (frow) {
-      const int wpt = (Wn + S - 1) / S;
-      const int wb = fs * wpt, we = min(Wn, wb + wpt);
-      for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
-    }
-    for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
-    if (frow && fs == 0) {
-      inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
-      if (a.degree_out) a.degree_out[env0 + i0 + fr] = deg;
-    }
-  }
-  if (a.adj_bits) {
-    uint64_t* dst = a.adj_bits + (env0 + i0) * (size_t)Wn;
-    for (int k = tid; k < nrows * Wn; k += kThreads) dst[k] = adj[k];
-  }
-  __syncthreads();
-  GF_STAMP(7);
-  if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
-  GF_STAMP(8);
-
-  // ---- phase B: float64 tiles over the region, features / gradients of set bits
-  double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
-  double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
-  const int i_row = i0 + fr;
-  const St me = frow ? load_state<DYN, UF64, VAR>(a, env0 + i_row) : St{0, 0, 0, 0};
-  for (int j0 = 0; j0 < N; j0 += T) {
-    const int tc = min(T, N - j0);
-    __syncthreads();  // pos32 / the previous tile fully consumed
-    for (int t = tid; t < tc; t += kThreads) {
-      const St s = load_state<DYN, UF64, VAR>(a, env0 + j0 + t);
-      tile[t] = s;
-      svx += s.vx;
-      svy += s.vy;
-    }
-    __syncthreads();
-    if (!frow || (a.diag & 2)) continue;
-    const int nch = (tc + 63) >> 6;
-    const int wpt = (nch + S - 1) / S;
-    const int wb = fs * wpt, we = min(nch, wb + wpt);
-    for (int w = wb; w < we; ++w) {
-      const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
-      const uint64_t nm = CTRL ? nearb[(size_t)fr * Wn + (j0 >> 6) + w] : 0ull;
-      uint64_t m = am | nm;
-      while (m) {
-        const int k = __builtin_ctzll(m);
-        m &= m - 1;
-        const int c = (w << 6) + k;
-        const bool isadj = (am >> k) & 1ull;
-        const St o = tile[c];
-        const double dx = me.px - o.px, dy = me.py - o.py;
-        const double r2 = dx * dx + dy * dy;
-        // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
-        // reference's two divisions; far inside the float32 outputs' tolerance)
-        const double ir = 1.0 / r2, irr = ir * ir;
-        const double q1x = dx * irr, q2x = dx * ir;
-        const double q1y = dy * irr, q2y = dy * ir;
-        if (isadj) {
-          // obstacle variant: no velocity difference for pairs touching agents < nvz
-          const bool vz = VAR && (i_row < a.n_vel_zero || j0 + c < a.n_vel_zero);
-          f0 += vz ? 0.0 : me.vx - o.vx;
-          f1 += q1x;
-          f2 += q2x;
-          f3 += vz ? 0.0 : me.vy - o.vy;
-          f4 += q1y;
-          f5 += q2y;
-        }
-        if constexpr (CTRL) {
-          if (((nm >> k) & 1ull) && (a.centralized || isadj)) {
-            gx += (-2.0 * q1x) + (2.0 * q2x);
-            gy += (-2.0 * q1y) + (2.0 * q2y);
-          }
-        }
-      }
-    }
-  }
-  GF_STAMP(9);
-  step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
-                                      frow && fs == 0, S, tid);
-  GF_STAMP(10);
-#if defined(GF_STAMPS) && GF_STAMPS >= 2
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  GF_STAMP(11);
-#endif
-}
-
-// ---------------------------------------------------------------------------------
-// Env-resident form of the same step (N <= kResidentMax): a workgroup loads its env's
-// agents into LDS once, then walks a slice of 32-row blocks. Nothing inside the block
-// loop reads global memory, so the network stores of block k drain while block k+1
-// computes (no vmcnt wait ever sits behind them), and the env's state is read and
-// integrated once per slice instead of once per 32 rows. Same numerics and outputs as
-// flock_step_kernel (pass 1 float32 prefilter + float64 band, float64 features).
-template <bool DYN, bool UF64, bool CTRL>
-__global__ __launch_bounds__(kThreads) void flock_step_resident_kernel(StepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int RB = kResidentRows;
-  constexpr int S = kThreads / RB;  // word-slices per row in the feature pass
-  const int N = a.N;
-  const int Np = (N + 63) & ~63;
-  const int Wn = Np >> 6;
-  St* tile = reinterpret_cast<St*>(smem);                    // Np float64 states
-  float2* tile32 = reinterpret_cast<float2*>(tile + Np);     // Np float32 positions
-  uint64_t* adj = reinterpret_cast<uint64_t*>(tile32 + Np);  // RB x Wn
-  uint64_t* nearb = adj + (size_t)RB * Wn;                   // RB x Wn (CTRL)
-  double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)RB * Wn : 0));
-  float* redf = reinterpret_cast<float*>(red + 4);
-  float* inv = reinterpret_cast<float*>(red + 8);  // RB
-
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = L / a.spe, sl = L - b * a.spe;
-  const int r0 = sl * a.rps, r1 = min(N, r0 + a.rps);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const size_t env0 = (size_t)b * N;
-
-  // prologue: the env's post-update state, once per workgroup
-  double svx = 0, svy = 0;
-  float pt = 0.f;
-  for (int t = tid; t < N; t += kThreads) {
-    const St s = load_state<DYN, UF64>(a, env0 + t);
-    tile[t] = s;
-    const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
-    tile32[t] = make_float2(fx, fy);
-    pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
-    svx += s.vx;
-    svy += s.vy;
-  }
-  const float Pt = uniform_f(block_max(pt, redf));
-  const double Svx = block_sum(svx, red);
-  const double Svy = block_sum(svy, red);
-  if (a.reward && sl == 0) {  // instant_cost (:145-147), two-pass like np.var
-    const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
-    double qx = 0, qy = 0;
-    for (int t = tid; t < N; t += kThreads) {
-      const double ex = tile[t].vx - mx, ey = tile[t].vy - my;
-      qx += ex * ex;
-      qy += ey * ey;
-    }
-    const double Qx = block_sum(qx, red);
-    const double Qy = block_sum(qy, red);
-    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
-  }
-  const float pu = Pt + Pt;  // rows are agents of the same env
-  Band ba{-__builtin_inff(), __builtin_inff()}, bn = ba;
-  if (pu < 1.0e5f) {
-    const double delta = ldexp(static_cast<double>(pu) * (1.0 + 1e-6) + 4.0, -20);
-    ba = make_band(a.cr2, delta);
-    bn = make_band(a.cr, delta);
-  }
-  ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
-  bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
-  const int npair = (Wn + 1) >> 1;
-  const int fr = tid / S, fs = tid - fr * S;
-  const bool vec4 = (N & 3) == 0;
-
-  for (int i0 = r0; i0 < r1; i0 += RB) {
-    const int nrows = min(RB, r1 - i0);
-    float rx32 = 0.f, ry32 = 0.f;
-    if (lane < nrows) {
-      const float2 p = tile32[i0 + lane];
-      rx32 = p.x;
-      ry32 = p.y;
-    }
-    // pass 1 over every column of the env (see flock_step_kernel)
-    for (int cp = (a.diag & 8) ? npair : wid; cp < npair; cp += 4) {
-      const int ca = cp << 1;
-      const bool has_b = ca + 1 < Wn;
-      const int jta = (ca << 6) + lane, jtb = jta + 64;
-      const bool va = jta < N, vb = jtb < N;
-      const float2 qa = va ? tile32[jta] : make_float2(1.0e18f, 1.0e18f);
-      const float2 qb = vb ? tile32[jtb] : make_float2(1.0e18f, 1.0e18f);
-      const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
-      unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
-      uint64_t band = 0;
-      for (int r = 0; r < nrows; ++r) {
-        const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-        const f2v dx = xi - qx, dy = yi - qy;
-        const f2v d2 = dx * dx + dy * dy;
-        const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
-        const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
-        band |= (Aa ^ Ma) | (Ab ^ Mb);
-        put_lane(wa0, wa1, Aa, r);
-        put_lane(wb0, wb1, Ab, r);
-        if constexpr (CTRL) {
-          const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
-          const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
-          band |= (Na ^ NMa) | (Nb ^ NMb);
-          put_lane(na0, na1, Na, r);
-          put_lane(nb0, nb1, Nb, r);
-        }
-      }
-      if (band) {  // rare: decide the band pairs exactly in float64
-        const St oa = va ? tile[jta] : St{1.0e300, 1.0e300, 0, 0};
-        const St ob = vb ? tile[jtb] : St{1.0e300, 1.0e300, 0, 0};
-        for (int r = 0; r < nrows; ++r) {
-          const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-          const f2v dx = xi - qx, dy = yi - qy;
-          const f2v d2 = dx * dx + dy * dy;
-          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
-          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
-          uint64_t Na = 0, Nb = 0, NMa = 0, NMb = 0;
-          if constexpr (CTRL) {
-            Na = __ballot(d2.x <= bn.lo);
-            Nb = __ballot(d2.y <= bn.lo);
-            NMa = __ballot(!(d2.x > bn.hi));
-            NMb = __ballot(!(d2.y > bn.hi));
-          }
-          if ((Aa ^ Ma) | (Ab ^ Mb) | (Na ^ NMa) | (Nb ^ NMb)) {
-            const St ri = tile[i0 + r];
-            const double dxa = ri.px - oa.px, dya = ri.py - oa.py;
-            const double dxb = ri.px - ob.px, dyb = ri.py - ob.py;
-            const double r2a = dxa * dxa + dya * dya, r2b = dxb * dxb + dyb * dyb;
-            put_lane(wa0, wa1, Aa | (__ballot(r2a < a.cr2) & (Aa ^ Ma)), r);
-            put_lane(wb0, wb1, Ab | (__ballot(r2b < a.cr2) & (Ab ^ Mb)), r);
-            if constexpr (CTRL) {
-              put_lane(na0, na1, Na | (__ballot(r2a <= a.cr) & (Na ^ NMa)), r);
-              put_lane(nb0, nb1, Nb | (__ballot(r2b <= a.cr) & (Nb ^ NMb)), r);
-            }
-          }
-        }
-      }
-      if (lane < nrows) {
-        const int dl = i0 + lane - (ca << 6);  // the diagonal is never a neighbour
-        const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
-        const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
-        uint64_t* arow = adj + (size_t)lane * Wn + ca;
-        arow[0] = ((static_cast<uint64_t>(wa1) << 32) | wa0) & ka;
-        if (has_b) arow[1] = ((static_cast<uint64_t>(wb1) << 32) | wb0) & kb;
-        if constexpr (CTRL) {
-          uint64_t* nrow = nearb + (size_t)lane * Wn + ca;
-          nrow[0] = ((static_cast<uint64_t>(na1) << 32) | na0) & ka;
-          if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
-        }
-      }
-    }
-    __syncthreads();
-
-    // degrees -> 1/deg
-    const bool frow = fr < nrows;
-    const int wpt = (Wn + S - 1) / S;
-    const int wb = fs * wpt, we = min(Wn, wb + wpt);
-    {
-      int deg = 0;
-      if (frow)
-        for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
-      for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
-      if (frow && fs == 0)
-        inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
-    }
-    __syncthreads();
-
-    // network rows of this block (one contiguous nrows*N*4-byte range)
-    if (a.network) {
-      for (int r = wid; r < nrows; r += 4) {
-        const float iv = inv[r];
-        const uint64_t* bits = adj + (size_t)r * Wn;
-        float* rowp = a.network + (env0 + i0 + r) * (size_t)N;
-        if (vec4) {
-          f4v* r4 = reinterpret_cast<f4v*>(rowp);
-          const int nq = N >> 2;
-          for (int q = lane; q < nq; q += 64) {
-            const unsigned nib = static_cast<unsigned>(bits[q >> 4] >> ((q & 15) << 2)) & 0xFu;
-            const f4v v = {(nib & 1u) ? iv : 0.0f, (nib & 2u) ? iv : 0.0f, (nib & 4u) ? iv : 0.0f,
-                           (nib & 8u) ? iv : 0.0f};
-            if (a.diag & 4)
-              __builtin_nontemporal_store(v, &r4[q]);
-            else
-              r4[q] = v;
-          }
-        } else {
-          for (int c = lane; c < N; c += 64) rowp[c] = ((bits[c >> 6] >> (c & 63)) & 1ull) ? iv : 0.0f;
-        }
-      }
-    }
-
-    // features / gradients of this block's rows (set bits only), then per-row outputs
-    double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
-    const St me = frow ? tile[i0 + fr] : St{0, 0, 0, 0};
-    if (frow && !(a.diag & 2)) {
-      for (int w = wb; w < we; ++w) {
-        const uint64_t am = adj[(size_t)fr * Wn + w];
-        const uint64_t nm = CTRL ? nearb[(size_t)fr * Wn + w] : 0ull;
-        uint64_t m = am | nm;
-        while (m) {
-          const int k = __builtin_ctzll(m);
-          m &= m - 1;
-          const St o = tile[(w << 6) + k];
-          const double dx = me.px - o.px, dy = me.py - o.py;
-          const double r2 = dx * dx + dy * dy;
-          const double rr = r2 * r2;
-          const double q1x = dx / rr, q2x = dx / r2;
-          const double q1y = dy / rr, q2y = dy / r2;
-          const bool isadj = (am >> k) & 1ull;
-          if (isadj) {
-            f0 += me.vx - o.vx;
-            f1 += q1x;
-            f2 += q2x;
-            f3 += me.vy - o.vy;
-            f4 += q1y;
-            f5 += q2y;
-          }
-          if constexpr (CTRL) {
-            const bool isnear = (nm >> k) & 1ull;
-            if (isnear && (a.centralized || isadj)) {
-              gx += (-2.0 * q1x) + (2.0 * q2x);
-              gy += (-2.0 * q1y) + (2.0 * q2y);
-            }
-          }
-        }
-      }
-    }
-    for (int o = 1; o < S; o <<= 1) {
-      f0 += __shfl_xor(f0, o);
-      f1 += __shfl_xor(f1, o);
-      f2 += __shfl_xor(f2, o);
-      f3 += __shfl_xor(f3, o);
-      f4 += __shfl_xor(f4, o);
-      f5 += __shfl_xor(f5, o);
-      if constexpr (CTRL) {
-        gx += __shfl_xor(gx, o);
-        gy += __shfl_xor(gy, o);
-      }
-    }
-    if (frow && fs == 0) {
-      const size_t g = env0 + i0 + fr;
-      if (a.state_values) {
-        float* sv = a.state_values + g * 6;
-        sv[0] = static_cast<float>(f0);
-        sv[1] = static_cast<float>(f1);
-        sv[2] = static_cast<float>(f2);
-        sv[3] = static_cast<float>(f3);
-        sv[4] = static_cast<float>(f4);
-        sv[5] = static_cast<float>(f5);
-      }
-      if constexpr (DYN) {
-        double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
-        xo[0] = double2{me.px, me.py};
-        xo[1] = double2{me.vx, me.vy};
-      }
-      if constexpr (CTRL) {
-        const double p2 = a.centralized ? static_cast<double>(N) * me.vx - Svx : f0;
-        const double p3 = a.centralized ? static_cast<double>(N) * me.vy - Svy : f3;
-        double2 u;
-        u.x = clip10(-gx - p2) / a.action_scalar;
-        u.y = clip10(-p3 - gy) / a.action_scalar;
-        reinterpret_cast<double2*>(a.ctrl_out)[g] = u;
-      }
-    }
-    __syncthreads();  // bits and 1/deg are rewritten by the next block
-  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1455,7 +943,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
     kj[m] = INT_MAX;
   }
   const size_t g = (size_t)b * N + i;
-  const bool fast = vi && a.adj_bits && a.degree[g] >= K && !(a.diag & 0x8000);
+  const bool fast = vi && a.adj_bits && a.degree[g] >= K && !GF_ABLATE(a, 0x8000);
   if (fast) {  // rank the neighbours only
     const int Wn = (N + 63) >> 6;
     const uint64_t* bits = a.adj_bits + g * Wn;
@@ -1468,7 +956,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
         m &= m - 1;
         const double2 p = pos(j);
         const double dx = pxi - p.x, dy = pyi - p.y;
-        if (a.diag & 0x4000) {  // ablation: no ranking (outputs: the last neighbour K times)
+        if (GF_ABLATE(a, 0x4000)) {  // ablation: no ranking (outputs: the last neighbour K times)
           kr[0] += dx * dx + dy * dy;
           kj[0] = j;
         } else {
@@ -1476,7 +964,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
         }
       }
     }
-    if (a.diag & 0x4000) {
+    if (GF_ABLATE(a, 0x4000)) {
 #pragma unroll
       for (int m = 1; m < K; ++m) kj[m] = kj[0];
     }
@@ -1641,70 +1129,29 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
   return s;
 }
 
-size_t split_lds_bytes(int N, int R, int T, bool ctrl) {
-  const size_t Wn = (N + 63) / 64;
-  return split_region_bytes(N, T) + (size_t)R * Wn * 8 * (ctrl ? 2 : 1) + 8 * sizeof(double) +
-         (((size_t)R * 4 + 15) / 16) * 16;
-}
-
-size_t step_resident_lds_bytes(int N, bool ctrl) {
-  const size_t Np = (N + 63) / 64 * 64, Wn = Np / 64;
-  return Np * (sizeof(St) + 8) + (size_t)kResidentRows * Wn * 8 * (ctrl ? 2 : 1) + 8 * sizeof(double) +
-         kResidentRows * 4;
-}
-
-void step_resident_geometry(int N, int B, int target_wgs, int* spe, int* rps) {
-  const int blocks = (N + kResidentRows - 1) / kResidentRows;
-  int s = (target_wgs + B - 1) / B;
-  s = s < 1 ? 1 : (s > blocks ? blocks : s);
-  const int per = ((N + s - 1) / s + kResidentRows - 1) / kResidentRows * kResidentRows;
-  *rps = per;
-  *spe = (N + per - 1) / per;
-}
-
-template <bool DYN, bool UF64, bool CTRL>
-static hipError_t launch_step_resident_t(const StepArgs& a, hipStream_t s) {
-  const size_t lds = step_resident_lds_bytes(a.N, CTRL) + (size_t)a.lds_pad;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_resident_kernel<DYN, UF64, CTRL>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((flock_step_resident_kernel<DYN, UF64, CTRL>), dim3(a.B * a.spe), dim3(kThreads), lds, s, a);
-  return hipGetLastError();
-}
-
-template <bool DYN, bool UF64, bool CTRL, bool VAR>
-static hipError_t launch_step_split(const StepArgs& a, hipStream_t s) {
-  const size_t lds = split_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_split_kernel<DYN, UF64, CTRL, VAR>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int grid = a.B * a.bpe;
-  hipLaunchKernelGGL((flock_step_split_kernel<DYN, UF64, CTRL, VAR>), dim3(grid), dim3(kThreads), lds, s, a);
-  return hipGetLastError();
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): `done`
+// holds one bit per device ordinal (a second handle on another device sets its own;
+// concurrent first calls both set it, which is harmless).
+hipError_t max_lds_once(const void* f, std::atomic<uint64_t>& done, int bytes) {
+  int dev = 0;
+  if (const hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+  const uint64_t bit = dev < 64 ? (1ull << dev) : 0ull;
+  if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_acq_rel);
+  return e;
 }
 
 template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
-  if (a.split && a.N <= kSplitMax) return launch_step_split<DYN, UF64, CTRL, VAR>(a, s);
-  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL) + (size_t)a.lds_pad;
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL);
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
   // would allow
-  if (!CTRL && !VAR && a.lds_pad == 0 && lds < (size_t)a.lds_floor) lds = a.lds_floor;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  if (!CTRL && !VAR && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
+  static std::atomic<uint64_t> attr{0};
+  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF>),
+                                        attr, 160 * 1024); e != hipSuccess)
+    return e;
   const int grid = a.B * a.bpe;
   hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR, PF>), dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
@@ -1713,10 +1160,7 @@ static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if (a.variant) return launch_step_tiled<DYN, UF64, CTRL, true>(a, s);
-  if (a.resident && !a.adj_bits && !a.degree_out) return launch_step_resident_t<DYN, UF64, CTRL>(a, s);
-  if (a.prefetch && a.T <= 2 * kThreads && a.N > a.T && !a.split)
-    return a.prefetch == 2 ? launch_step_tiled<DYN, UF64, CTRL, false, 2>(a, s)
-                           : launch_step_tiled<DYN, UF64, CTRL, false, 1>(a, s);
+  if (a.prefetch && a.T <= 2 * kThreads && a.N > a.T) return launch_step_tiled<DYN, UF64, CTRL, false, 1>(a, s);
   return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
 }
 
@@ -1733,19 +1177,17 @@ hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
   const bool lds = a.N <= kKnnLdsMax;
   const size_t bytes = lds ? (size_t)a.N * 24 : 0;  // the env's positions, float64 + float32
   switch (a.K) {
-#define GF_KNN_CASE(k)                                                                            \
-  case k:                                                                                         \
-    if (lds) {                                                                                    \
-      static bool attr_##k = false;                                                               \
-      if (!attr_##k) {                                                                            \
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&flock_knn_kernel<k, true>), \
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kKnnLdsMax * 24); \
-        if (e != hipSuccess) return e;                                                            \
-        attr_##k = true;                                                                          \
-      }                                                                                           \
-      hipLaunchKernelGGL((flock_knn_kernel<k, true>), dim3(grid), dim3(kThreads), bytes, s, a);  \
-    } else                                                                                        \
-      hipLaunchKernelGGL((flock_knn_kernel<k, false>), dim3(grid), dim3(kThreads), 0, s, a);     \
+#define GF_KNN_CASE(k)                                                                                  \
+  case k:                                                                                               \
+    if (lds) {                                                                                          \
+      static std::atomic<uint64_t> attr_##k{0};                                                         \
+      if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_knn_kernel<k, true>), \
+                                            attr_##k, kKnnLdsMax * 24);                                 \
+          e != hipSuccess)                                                                              \
+        return e;                                                                                       \
+      hipLaunchKernelGGL((flock_knn_kernel<k, true>), dim3(grid), dim3(kThreads), bytes, s, a);        \
+    } else                                                                                              \
+      hipLaunchKernelGGL((flock_knn_kernel<k, false>), dim3(grid), dim3(kThreads), 0, s, a);           \
     break;
     GF_KNN_CASE(1) GF_KNN_CASE(2) GF_KNN_CASE(3) GF_KNN_CASE(4) GF_KNN_CASE(5) GF_KNN_CASE(6)
     GF_KNN_CASE(7) GF_KNN_CASE(8) GF_KNN_CASE(10) GF_KNN_CASE(12) GF_KNN_CASE(16)

@@ -119,6 +119,7 @@ SIGNATURES = {
     "cov_get_visited": [_P, _I, _P],
     "cov_get_n_motion": [_P, _P],
     "cov_sync": [_P],
+    "cov_set_streams": [_P, _I],
     "cov_controller_greedy": [_P, _P, _P, _P],
     "cov_get_time_matrix": [_P, _I, _P, _P],
     "cov_get_flat_obs": [_P, _P, _I],
@@ -494,6 +495,11 @@ class CoverageHandle:
 
     def sync(self):
         check(self.lib.cov_sync(self.h))
+
+    def set_streams(self, n):
+        """Launches per step: 2 (default) splits the env batch over two HIP streams; 1
+        keeps every step on the handle's stream (cov_set_streams)."""
+        check(self.lib.cov_set_streams(self.h, int(n)))
 
     def controller_greedy(self, fetch=True):
         """Greedy expert actions (B,R) int32 and the (B,R) bool mask of robots the

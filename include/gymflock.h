@@ -222,9 +222,10 @@ int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes); /* close
 int cov_get_visited(cov_handle* h, int env, uint8_t* visited);
 int cov_get_n_motion(cov_handle* h, int32_t* n_motion);
 /* Back-to-back cov_step calls go out as two half-batch launches on two streams (as
- * fe_set_streams; GYMFLOCK_STREAMS=1 at create for one); every other call, cov_sync
+ * fe_set_streams; cov_set_streams(h, 1) for one); every other call, cov_sync
  * included, first orders the handle's stream after both. */
 int cov_sync(cov_handle* h);
+int cov_set_streams(cov_handle* h, int n);
 /* Greedy expert, controller(greedy=True) :800-872. On first use after cov_set_targets
  * it builds each env's time matrix (construct_time_matrix :621-653) on the device;
  * then every robot heads for its nearest unvisited target via the predecessor matrix.
@@ -295,7 +296,7 @@ int fe_abi_version(void);
  * result is the device time of the whole window since enable divided by the steps in
  * it, and `launches` counts steps (each two concurrent half-batch launches). */
 int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches);
-/* Launches per step: 2 (default; GYMFLOCK_STREAMS=1 at create for 1) sends envs
+/* Launches per step: 2 (default) sends envs
  * [0, ceil(B/2)) to the handle's stream and the rest to a second stream; each half
  * depends only on its own previous step, so one launch's ramp and tail overlap the
  * other's body. Every other call first orders the handle's stream after both halves,
@@ -308,9 +309,10 @@ int fe_join(fe_handle* h);
 /* The same for cov_step_kernel on a Coverage handle. */
 int cov_kernel_timing(cov_handle* h, int enable, double* avg_ms, int64_t* launches);
 /* Diagnostics for roofline work: what = 0/1 times `reps` launches of a float4
- * plain/non-temporal fill of the network buffer (the write-bandwidth ceiling);
+ * plain/non-temporal fill of the network buffer (the write-bandwidth ceiling).
  * what = 0x10000 | bits (16 bits) sets ablation switches on later step launches
- * (0x10000 clears). */
+ * (0x10000 clears) in the diagnostic build only (make diag, -DGF_DIAG); the product
+ * library returns GF_EINVAL for it and never reads an environment variable. */
 int fe_diag(fe_handle* h, int what, int reps, double* avg_ms);
 
 #ifdef __cplusplus

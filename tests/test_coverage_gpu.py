@@ -204,7 +204,7 @@ def test_crowded_grid_claims_vs_oracle(R):
     h.close()
 
 
-def test_split_steps_match_single_stream(monkeypatch):
+def test_split_steps_match_single_stream():
     """Back-to-back resident steps go out as two half-batch launches on two streams;
     the observations, rewards and robots equal the one-launch-per-step run."""
     from gym_flock.envs.spatial.maps import generate_targets
@@ -212,9 +212,9 @@ def test_split_steps_match_single_stream(monkeypatch):
     np.random.seed(7)
     targets = generate_targets()
     runs = []
-    for streams in ("2", "1"):
-        monkeypatch.setenv("GYMFLOCK_STREAMS", streams)
+    for streams in (2, 1):
         h = nat.CoverageHandle(R, B, M)
+        h.set_streams(streams)
         h.set_targets(targets)
         T = len(targets)
         rs = np.random.RandomState(11)

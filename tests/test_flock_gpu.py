@@ -290,21 +290,6 @@ def test_rccl_reward_gather_single_rank():
     v.close()
 
 
-def test_env_resident_kernel_parity(monkeypatch):
-    """The opt-in env-resident step kernel (GYMFLOCK_RESIDENT=1) gives the same bits as
-    the tiled kernel and the oracle."""
-    monkeypatch.setenv("GYMFLOCK_RESIDENT", "1")
-    for n, B in ((100, 3), (1024, 2)):
-        x0 = synthetic_batch(B, n, seed0=7 * n)
-        u = np.random.RandomState(n).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
-        h = nat.FlockHandle(n, B)
-        h.set_state(x0)
-        h.step(u, nat.FE_WITH_CONTROLLER)
-        for b in range(B):
-            check_against_oracle(h, x0[b], u[b], b)
-        h.close()
-
-
 def test_config5_size_sampled_rows():
     """N=8192 (BASELINE.json configs[4]'s agent count; 16-row blocks, 16 LDS tiles per
     row sweep): the whole state and reward, and 40 sampled rows of the network,
@@ -363,29 +348,10 @@ def test_split_steps_match_single_stream():
         np.testing.assert_array_equal(a, b)
 
 
-def test_split_kernel_parity(monkeypatch):
-    """The opt-in split-phase step kernel (GYMFLOCK_SPLIT=1: float32 env positions, pass 1
-    over every column, stores, then float64 tiles for the features) matches the oracle,
-    with and without the controller, on ragged and tile-spanning sizes."""
-    monkeypatch.setenv("GYMFLOCK_SPLIT", "1")
-    for n, B in ((100, 3), (1024, 2), (1030, 2), (2048, 1)):
-        x0 = synthetic_batch(B, n, seed0=11 * n)
-        u = np.random.RandomState(n + 1).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
-        for ctrl in (False, True):
-            h = nat.FlockHandle(n, B)
-            h.set_state(x0)
-            h.step(u, nat.FE_WITH_CONTROLLER if ctrl else 0)
-            for b in range(B):
-                check_against_oracle(h, x0[b], u[b], b, ctrl=ctrl)
-            h.close()
-
-
-@pytest.mark.parametrize("mode", ["00", "11"])
-def test_network_store_loops(monkeypatch, mode):
-    """Both forms of the network store loop (generic nibble select, and the fast
-    bit-extract form used at N % 1024 == 0) write the oracle's rows, plain and with the
-    controller (GYMFLOCK_STORE_FAST=<plain><ctrl>)."""
-    monkeypatch.setenv("GYMFLOCK_STORE_FAST", mode)
+def test_network_store_loops():
+    """Both forms of the network store loop write the oracle's rows: at N % 1024 == 0 the
+    plain step uses the generic nibble select and the step + controller the fast
+    bit-extract form (capi.hip store_fast)."""
     n, B = 1024, 2
     x0 = synthetic_batch(B, n, seed0=77)
     u = np.random.RandomState(78).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
