@@ -106,10 +106,25 @@ struct fe_handle {
   fe_variant var{};
   double* dt_env = nullptr;             // (B) per-env dt
   bool dt_per_env = false;
-  // packed output mode (FE_PACKED_NETWORK)
-  uint64_t* adj_bits = nullptr;         // (B,N,Wn)
-  int32_t* pdeg = nullptr;              // (B,N)
+  // packed output mode (FE_PACKED_NETWORK) and the kNN step's adjacency: two buffers,
+  // so a step can write one while the kNN of the previous step reads the other
+  uint64_t* adj_bits[2] = {nullptr, nullptr};  // (B,N,Wn)
+  int32_t* pdeg[2] = {nullptr, nullptr};       // (B,N)
+  int bits_cur = 0;                     // buffer of the latest bits / degrees
   bool has_packed = false;
+  // Flocking-v0 pipelining: the kNN of step t runs on kstream, after both halves of
+  // step t and beside step t+1. A step that writes the state buffer x[i] (or a bits
+  // buffer) an unfinished kNN reads waits for that kNN's event first; every other API
+  // call joins kstream into `stream` (use_dev).
+  hipStream_t kstream = nullptr;
+  hipEvent_t ev_kin[2] = {nullptr, nullptr};  // stream / stream2 -> kstream
+  hipEvent_t ev_kjoin = nullptr;              // kstream -> stream
+  bool k_pending = false;                     // kstream holds work `stream` has not waited for
+  struct KnnReader {
+    hipEvent_t ev = nullptr;
+    bool live = false;
+    unsigned bmask = 0;                       // bits buffers it reads
+  } kread[2];                                 // by the state buffer x[i] the kNN reads
 };
 
 namespace {
@@ -124,12 +139,40 @@ int join_s2(fe_handle* h) {
   return GF_OK;
 }
 
+// `stream` waits for the kNN stream (enqueue only). Later work on `stream` (and, through
+// main_dirty, on stream2) is then ordered after every kNN launched so far.
+int join_k(fe_handle* h) {
+  if (h->k_pending) {
+    GF_HIP(hipEventRecord(h->ev_kjoin, h->kstream));
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ev_kjoin, 0));
+    h->k_pending = false;
+    for (auto& r : h->kread) r.live = false, r.bmask = 0;
+  }
+  return GF_OK;
+}
+
+// Before a step writes x[xw] (xw < 0: no state write) and bits buffer bw (bw < 0: none):
+// both step streams wait for the unfinished kNN launches that read them.
+int wait_knn_readers(fe_handle* h, int xw, int bw) {
+  for (int i = 0; i < 2; ++i) {
+    auto& r = h->kread[i];
+    if (r.live && (i == xw || (bw >= 0 && ((r.bmask >> bw) & 1u)))) {
+      GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
+      GF_HIP(hipStreamWaitEvent(h->stream2, r.ev, 0));
+      r.live = false;
+      r.bmask = 0;
+    }
+  }
+  return GF_OK;
+}
+
 // Every API call except the step launches: the device, and `stream` ordered after all
 // of the handle's outstanding work; what it enqueues is ordered before the next
 // second-half launch (main_dirty).
 int use_dev(fe_handle* h) {
   GF_HIP(hipSetDevice(h->cfg.device));
   if (int rc = join_s2(h)) return rc;
+  if (int rc = join_k(h)) return rc;
   h->main_dirty = true;
   h->other_work = true;
   return GF_OK;
@@ -158,10 +201,11 @@ void release(fe_handle* h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
+  if (h->kstream) hipStreamSynchronize(h->kstream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
                   h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
-                  h->adj_bits, h->pdeg};
+                  h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -169,8 +213,10 @@ void release(fe_handle* h) {
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
   for (hipEvent_t e : h->ag_ev)
     if (e) hipEventDestroy(e);
-  for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1]})
+  for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
+                       h->kread[0].ev, h->kread[1].ev})
     if (e) hipEventDestroy(e);
+  if (h->kstream) hipStreamDestroy(h->kstream);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->comm_stream) hipStreamDestroy(h->comm_stream);
@@ -198,14 +244,19 @@ int next_reward_slot(fe_handle* h) {
 }
 
 // Packed-output buffers on first use: adjacency bits (FE_PACKED_NETWORK, or the kNN
-// step) and their degrees.
-int packed_outputs(fe_handle* h, bool bits, bool deg, gf::StepArgs& a) {
-  if (bits && !h->adj_bits)
-    if (int rc = dalloc(&h->adj_bits, h->BN * ((h->cfg.n_agents + 63) / 64))) return rc;
-  if ((bits || deg) && !h->pdeg)
-    if (int rc = dalloc(&h->pdeg, h->BN)) return rc;
-  if (bits) a.adj_bits = h->adj_bits;
-  if (bits || deg) a.degree_out = h->pdeg;
+// step) and their degrees. A launch writes the buffer pair the latest bits are not in;
+// *bw is its index (-1: no bits written).
+int packed_outputs(fe_handle* h, bool bits, gf::StepArgs& a, int* bw) {
+  *bw = -1;
+  if (!bits) return GF_OK;
+  const int k = h->bits_cur ^ 1;
+  if (!h->adj_bits[k])
+    if (int rc = dalloc(&h->adj_bits[k], h->BN * ((h->cfg.n_agents + 63) / 64))) return rc;
+  if (!h->pdeg[k])
+    if (int rc = dalloc(&h->pdeg[k], h->BN)) return rc;
+  a.adj_bits = h->adj_bits[k];
+  a.degree_out = h->pdeg[k];
+  *bw = k;
   return GF_OK;
 }
 
@@ -215,10 +266,15 @@ int knn_mode(const fe_handle* h, int flags) {
   return ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0) ? 1 : 0;
 }
 
-int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a) {
+// Output buffers of a launch that writes x[xw] (xw < 0: none): picks the bits buffer and
+// orders the step streams after the kNN launches still reading what it overwrites.
+int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a, int xw) {
   const int km = knn_mode(h, flags);
   const bool packed = flags & FE_PACKED_NETWORK;
-  if (int rc = packed_outputs(h, packed || km == 1, false, a)) return rc;
+  int bw = -1;
+  if (int rc = packed_outputs(h, packed || km == 1, a, &bw)) return rc;
+  if (int rc = wait_knn_readers(h, xw, bw)) return rc;
+  if (bw >= 0) h->bits_cur = bw;  // the launch that follows fills it
   if (packed) h->has_packed = true;
   return GF_OK;
 }
@@ -328,20 +384,30 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
 // kNN of the current state; uses_adj: the last launch wrote this state's adjacency
 // (packed outputs), which lets agents with >= k neighbours rank only those.
 int launch_knn_cur(fe_handle* h, int mode) {
-  if (int rc = join_s2(h)) return rc;  // reads both halves' state and bits
-  h->main_dirty = true;
+  // on kstream after everything on both step streams (both halves' state and bits)
+  GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
+  GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[0], 0));
+  if (h->s2_pending) {
+    GF_HIP(hipEventRecord(h->ev_kin[1], h->stream2));
+    GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[1], 0));
+  }
   gf::KnnArgs k{};
   k.x = h->x[h->cur];
-  k.adj_bits = mode == 1 ? h->adj_bits : nullptr;
-  k.degree = mode == 1 ? h->pdeg : nullptr;
+  k.adj_bits = mode == 1 ? h->adj_bits[h->bits_cur] : nullptr;
+  k.degree = mode == 1 ? h->pdeg[h->bits_cur] : nullptr;
   k.idx = h->knn_idx;
   k.obs = h->knn_obs;
   k.N = h->cfg.n_agents;
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
   k.diag = h->diag;
-  hipError_t e = gf::launch_knn(k, h->stream);
+  hipError_t e = gf::launch_knn(k, h->kstream);
   if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
+  auto& r = h->kread[h->cur];
+  GF_HIP(hipEventRecord(r.ev, h->kstream));
+  r.live = true;
+  if (mode == 1) r.bmask |= 1u << h->bits_cur;
+  h->k_pending = true;
   h->has_knn = true;
   return GF_OK;
 }
@@ -413,7 +479,13 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreate(&h->tw[0])) != hipSuccess || (e = hipEventCreate(&h->tw[1])) != hipSuccess) {
+      (e = hipEventCreate(&h->tw[0])) != hipSuccess || (e = hipEventCreate(&h->tw[1])) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_kin[0], hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_kin[1], hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_kjoin, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->kread[0].ev, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->kread[1].ev, hipEventDisableTiming)) != hipSuccess) {
     release(h);
     return fail_hip("event create", e);
   }
@@ -515,7 +587,7 @@ int fe_compute_helpers(fe_handle* h, int flags) {
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
   const int km = knn_mode(h, flags);
-  if (int rc = prepare_outputs(h, flags, a)) return rc;
+  if (int rc = prepare_outputs(h, flags, a, -1)) return rc;
   if (int rc = timed_launch(h, a, false, false, ctrl)) return rc;
   if (ctrl) {
     h->ccur ^= 1;
@@ -568,7 +640,7 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
   const int km = knn_mode(h, flags);
-  if (int rc = prepare_outputs(h, flags, a)) return rc;
+  if (int rc = prepare_outputs(h, flags, a, h->cur ^ 1)) return rc;
   if (int rc = timed_launch(h, a, true, uf64, ctrl)) return rc;
   h->cur ^= 1;
   if (ctrl) h->ccur ^= 1;
@@ -698,11 +770,12 @@ int fe_get_network_packed(fe_handle* h, int env, uint64_t* bits, int32_t* degree
   const size_t N = h->cfg.n_agents, Wn = (N + 63) / 64;
   if (bits) {
     const size_t n = N * Wn;
-    if (int rc = env < 0 ? d2h(h, bits, h->adj_bits, h->BN * Wn * 8) : d2h(h, bits, h->adj_bits + env * n, n * 8))
-      return rc;
+    const uint64_t* src = h->adj_bits[h->bits_cur];
+    if (int rc = env < 0 ? d2h(h, bits, src, h->BN * Wn * 8) : d2h(h, bits, src + env * n, n * 8)) return rc;
   }
   if (degree) {
-    if (int rc = env < 0 ? d2h(h, degree, h->pdeg, h->BN * 4) : d2h(h, degree, h->pdeg + env * N, N * 4)) return rc;
+    const int32_t* src = h->pdeg[h->bits_cur];
+    if (int rc = env < 0 ? d2h(h, degree, src, h->BN * 4) : d2h(h, degree, src + env * N, N * 4)) return rc;
   }
   return GF_OK;
 }
@@ -732,6 +805,7 @@ int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs) {
   if (!h->has_knn) {
     if (!h->has_state) return fail(GF_ESTATE, "state not set");
     if (int rc = launch_knn_cur(h, 0)) return rc;  // no adjacency of this state at hand
+    if (int rc = join_k(h)) return rc;               // the copies below read its outputs
   }
   const size_t K = h->cfg.n_neighbors, N = h->cfg.n_agents;
   const size_t off = env < 0 ? 0 : env * N;
@@ -755,8 +829,8 @@ int fe_device_buffers(fe_handle* h, fe_buffers* out) {
   out->knn_idx = h->knn_idx;
   out->knn_obs = h->knn_obs;
   out->stream = h->stream;
-  out->adj_bits = h->adj_bits;
-  out->degree = h->pdeg;
+  out->adj_bits = h->adj_bits[h->bits_cur];
+  out->degree = h->pdeg[h->bits_cur];
   return GF_OK;
 }
 

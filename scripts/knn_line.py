@@ -1,0 +1,41 @@
+"""Flocking-v0 line alone (config 2 + 7-NN observation), for rocprofv3 kernel traces.
+
+  rocprofv3 --kernel-trace --stats -d gpurun_out/knnprof -o run -- python scripts/knn_line.py
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gym-flock_amd"))
+sys.path.insert(0, ROOT)
+
+from gym_flock.vec import VecFlockingRelative  # noqa: E402
+
+
+def main():
+    N, B = 1024, 256
+    steps = int(os.environ.get("KSTEPS", "50"))
+    knn = os.environ.get("KNN", "1") == "1"
+    env = VecFlockingRelative(B, N, n_neighbors=7)
+    x0 = env.reset(seed=0)
+    env.set_actions(np.random.RandomState(1234).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        for _ in range(8):
+            env.step(resident=True, knn=knn)
+        env.sync()
+    env.reset(x=x0)
+    env.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        env.step(resident=True, knn=knn)
+    env.sync()
+    print("knn=%d %.1f us/step" % (knn, 1e6 * (time.perf_counter() - t0) / steps))
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

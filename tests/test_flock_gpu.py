@@ -485,3 +485,32 @@ def test_knn_full_scan_rows_vs_oracle(case, k):
         np.testing.assert_array_equal(idx, ridx)
         np.testing.assert_array_equal(obs, robs.astype(np.float32))
     h.close()
+
+
+def test_knn_pipelined_back_to_back():
+    """Flocking-v0 steps issued back to back: each step's kNN runs on its own stream
+    beside the next step, with double-buffered adjacency bits. The state chain stays
+    bit-exact, and the kNN outputs read after 1, 2, 3 ... pipelined steps (and after a
+    packed-output step in between) equal the oracle's on that step's state."""
+    n, B = 300, 6
+    x0 = synthetic_batch(B, n, seed0=4242)
+    rs = np.random.RandomState(4243)
+    u = rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7)
+    h.set_state(x0)
+    h.set_actions(u)
+    x = x0.copy()
+    for burst in (1, 2, 3, 5):
+        for s in range(burst):
+            flags = nat.FE_U_RESIDENT | nat.FE_WITH_KNN
+            if burst == 3 and s == 1:  # a packed-output step writes the other bits buffer
+                flags |= nat.FE_PACKED_NETWORK
+            h.step(None, flags)
+            x = np.stack([orc.step(x[b], u[b], with_controller=False)["x"] for b in range(B)])
+        np.testing.assert_array_equal(h.get_state(), x)
+        idx, obs = h.knn()
+        for b in range(B):
+            ridx, robs = orc.knn_observation(x[b])
+            np.testing.assert_array_equal(idx[b], ridx)
+            np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
+    h.close()
