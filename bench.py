@@ -10,10 +10,18 @@ random-init swarms, float32 actions U(-1,1) resident in HBM.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+At one GPU the same JSON line also carries the other single-GPU configs of
+BASELINE.json as sub-objects: "coverage_config4" (Coverage-v0, R=200, 512 envs) and
+"n8192_config5" (N=8192 x 32 envs), each with ms_per_step, roofline and cpu_baseline;
+plus the step + fused controller, the packed-adjacency output and the Flocking-v0
+(k-nearest observation) forms of config 2.
+
 Multi-GPU: the env batch is sharded (256 envs per rank, weak scaling, no exchange on
-the step path); per-env rewards are all-gathered with RCCL on a side stream after
-each step (the metrics path). torch.distributed (gloo, CPU) is used only for the
-rendezvous, barriers and the max-over-ranks time; it never touches the GPU.
+the step path); per-env rewards are all-gathered with RCCL on a side stream every 8
+steps (the metrics path), and every rank checks the whole gathered vector. The worker
+never imports torch: torchrun only launches it, and the ranks meet over a plain TCP
+host channel (gym_flock.hostgroup) for the RCCL unique id, barriers and the max over
+ranks of the timed region.
 """
 import argparse
 import json
@@ -28,9 +36,8 @@ sys.path.insert(0, os.path.join(ROOT, "gym-flock_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-# HIP events bracket every TIMING_EVERY-th step launch in the timed region (roofline
-# kernel time); an event pair keeps that launch from overlapping its neighbours, so
-# timing every launch would add ~7 us to every step's wall time
+# with one launch per step, HIP events bracket every TIMING_EVERY-th launch; with split
+# steps (the default) one event pair brackets the whole timed region
 TIMING_EVERY = 8
 # (N, envs per GPU, GPUs) -> which BASELINE.json config the run is
 CONFIG_TAG = {(1024, 256, 1): " (BASELINE.json configs[1])", (1024, 256, 8): " (BASELINE.json configs[2])",
@@ -39,6 +46,17 @@ CONFIG_TAG = {(1024, 256, 1): " (BASELINE.json configs[1])", (1024, 256, 8): " (
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def clock_warmup(step, sync, ms):
@@ -65,53 +83,51 @@ def clock_warmup(step, sync, ms):
 
 
 def step_bytes(n):
-    """Algorithmic HBM bytes of one env-step: read x (float64,
-    32N) + u (float32, 8N); write x (32N), state_values (float32, 24N), network
-    (float32, 4N^2) and the reward (8)."""
+    """Algorithmic HBM bytes of one env-step: read x (float64, 32N) +
+    u (float32, 8N); write x (32N), state_values (float32, 24N), network (float32,
+    4N^2) and the reward (8)."""
     return 4 * n * n + 96 * n + 8
 
 
-def cpu_baseline(n_agents, seconds):
-    """The oracle's NumPy step (one core) on env 0 of the same synthetic workload."""
-    from oracle import flocking as orc
-    from gym_flock.init_states import synthetic_state
+def load_traffic(n_agents, n_envs):
+    """Per-step HBM bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE,
+    gfx950 correction) for this workload, committed under profiles/; None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get("%dx%d" % (n_agents, n_envs))
+        return None if e is None else float(e["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
 
-    x = synthetic_state(n_agents, 0)
-    rs = np.random.RandomState(1234)
-    u = rs.uniform(-1, 1, size=(n_agents, 2)).astype(np.float32)
+
+# ------------------------------------------------------------------ CPU baselines
+def cpu_ref_rate(n_agents, seconds, seed=0, max_steps=100000):
+    """oracle/cpu_ref.py: the reference's own NumPy array-op sequence for step()
+    (checked bitwise and within 15 % of the reference's time by scripts/check_cpu_ref.py)
+    on one env of the same synthetic workload, one thread."""
+    from oracle.cpu_ref import CpuFlock
+    from gym_flock.init_states import synthetic_state
+    env = CpuFlock(synthetic_state(n_agents, seed))
+    u = np.random.RandomState(1234 + seed).uniform(-1, 1, size=(n_agents, 2)).astype(np.float32)
     steps, t0 = 0, time.perf_counter()
     while True:
-        out = orc.step(x, u)
-        x = out["x"]
+        env.step(u)
         steps += 1
         el = time.perf_counter() - t0
-        if (el >= seconds and steps >= 3) or steps >= 100000:
-            break
-    return {"value": n_agents * steps / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": "oracle/flocking.py step() (NumPy, float64, 1 thread) on 1 env of N=%d for "
-                      "%d steps (%.1f s); same synthetic init and float32 actions as the GPU run"
-                      % (n_agents, steps, el)}
+        if (el >= seconds and steps >= 1) or steps >= max_steps:
+            return n_agents * steps / el, steps, el
 
 
 def cpu_worker(n_agents, seconds, seed):
     """--cpu-worker: one process of the all-cores baseline (no GPU is touched)."""
-    from oracle import flocking as orc
-    from gym_flock.init_states import synthetic_state
-
-    x = synthetic_state(n_agents, seed)
-    u = np.random.RandomState(1234 + seed).uniform(-1, 1, size=(n_agents, 2)).astype(np.float32)
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        x = orc.step(x, u)["x"]
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and steps >= 3:
-            break
-    print(json.dumps({"agent_steps_per_s": n_agents * steps / el, "steps": steps, "seconds": el}), flush=True)
+    rate, steps, el = cpu_ref_rate(n_agents, seconds, seed)
+    print(json.dumps({"agent_steps_per_s": rate, "steps": steps, "seconds": el}), flush=True)
 
 
 def cpu_baseline_all_cores(n_agents, seconds, procs):
-    """`procs` independent single-threaded oracle processes at once
+    """`procs` independent single-threaded cpu_ref processes at once
     (child processes, OMP_NUM_THREADS=1), aggregate agent-steps/s."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
@@ -125,17 +141,92 @@ def cpu_baseline_all_cores(n_agents, seconds, procs):
     return sum(rates), len(rates)
 
 
-def load_traffic(n_agents, n_envs):
-    """Per-launch HBM bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE,
-    gfx950 correction) for this workload, committed under profiles/; None if absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        e = d.get("%dx%d" % (n_agents, n_envs))
-        return None if e is None else float(e["bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
-        return None
+def flock_cpu_baseline(n_agents, seconds, procs):
+    rate, steps, el = cpu_ref_rate(n_agents, seconds)
+    out = {"value": rate, "unit": "agent-steps/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+           "per_core": rate,
+           "sample": "oracle/cpu_ref.py step() on 1 env of N=%d for %d steps (%.1f s), 1 thread: the reference's "
+                     "own NumPy array-op sequence (flocking_relative.py:91-147), bitwise equal to it and within 15%% "
+                     "of its time (scripts/check_cpu_ref.py, profiles/r02/cpu_ref_check.json); same synthetic init "
+                     "and float32 actions as the GPU run" % (n_agents, steps, el)}
+    if procs > 1:
+        log("cpu baseline, all cores: %d processes x ~%.0fs..." % (procs, seconds / 2))
+        agg, ok = cpu_baseline_all_cores(n_agents, seconds / 2, procs)
+        out.update(value=agg, cores=ok,
+                   sample=out["sample"] + "; value = %d such processes at once (OMP_NUM_THREADS=1 each, %.0f s), "
+                                          "summed; per_core = one process alone" % (ok, seconds / 2))
+    return out
+
+
+# ------------------------------------------------------------------ timed regions
+class Ranks:
+    """Barrier and max over ranks through the host channel (None: one process)."""
+
+    def __init__(self, group):
+        self.g = group
+
+    def barrier(self, env):
+        env.sync()
+        if self.g is not None:
+            self.g.barrier()
+
+    def max(self, v):
+        return v if self.g is None else self.g.max(v)
+
+
+def timed(env, ranks, k, step):
+    """k steps bracketed by a barrier + device sync on both sides; returns (max-over-
+    ranks wall seconds, device ms per step from the handle's timing window)."""
+    ranks.barrier(env)
+    env.h.timing_start(every=TIMING_EVERY)
+    t0 = time.perf_counter()
+    for s in range(k):
+        step(s)
+    env.sync()
+    el = time.perf_counter() - t0
+    kernel_ms, _ = env.h.timing_stop()
+    ranks.barrier(env)
+    return ranks.max(el), kernel_ms
+
+
+def flock_roofline(n, b, kernel_ms, launches_per_step):
+    bytes_step = b * step_bytes(n)
+    achieved = bytes_step / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n, b),
+            "kernel": "flock_step_kernel<DYN,f32 u>", "region_ms_per_step": kernel_ms,
+            "algorithmic_bytes_per_step": bytes_step, "launches_per_step": launches_per_step,
+            "timing": "device time per step of the whole timed region (HIP events on the handle's stream, the "
+                      "end event after it joins the second): each step is two concurrent half-batch launches "
+                      "of the kernel on two streams, so region_ms_per_step and the bytes are per step"}
+
+
+def bench_config5(args):
+    """BASELINE.json configs[4]: N=8192 x 32 envs (the dense N^2 stress case)."""
+    from gym_flock.vec import VecFlockingRelative
+    N, B, K, W = 8192, 32, max(5, args.steps // 2), max(2, args.warmup)
+    env = VecFlockingRelative(B, N)
+    x0 = env.reset(seed=0)
+    env.set_actions(np.random.RandomState(1234).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
+    warm = clock_warmup(lambda: env.step(resident=True), env.sync, 100.0)
+    env.set_state(x0)
+    for _ in range(W):
+        env.step(resident=True)
+    el, kms = timed(env, Ranks(None), K, lambda s: env.step(resident=True))
+    env.close()
+    out = {"metric": "agent-steps/sec, FlockingRelative N=8192", "value": N * B * K / el, "unit": "agent-steps/s",
+           "steps": K, "warmup": W, "clock_warmup": warm, "ms_per_step": 1e3 * el / K,
+           "config": {"workload": "FlockingRelative-v0 step(), N=8192 agents x 32 envs (BASELINE.json configs[4])"},
+           "roofline": flock_roofline(N, B, kms, 2)}
+    if not args.no_cpu_baseline:
+        log("cpu baseline N=8192 (cpu_ref, 1 step)...")
+        rate, steps, sec = cpu_ref_rate(N, 1.0, max_steps=1)
+        out["cpu_baseline"] = {"value": rate, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+                               "cpu_model": cpu_model(),
+                               "sample": "oracle/cpu_ref.py step() (the reference's array-op sequence, ~12 GB of "
+                                         "(N,N,{4,6}) float64 temporaries) on 1 env of N=8192 for %d step (%.1f s), "
+                                         "1 thread" % (steps, sec)}
+    return out
 
 
 def coverage_cpu_baseline(targets, n_robots, max_nodes, seconds):
@@ -154,56 +245,54 @@ def coverage_cpu_baseline(targets, n_robots, max_nodes, seconds):
         if el >= seconds and steps >= 3:
             break
     return {"value": n_robots * steps / el, "unit": "robot-steps/s", "cores": 1, "kind": "port",
-            "sample": "oracle/coverage.py step() (NumPy, 1 thread) on 1 env, R=%d, T=%d, %d steps (%.1f s)"
-                      % (n_robots, T, steps, el)}
+            "cpu_model": cpu_model(),
+            "sample": "oracle/coverage.py step() (NumPy restatement, 1 thread; NOT the reference's own op sequence: "
+                      "the reference measured 12.36 ms per step at R=200 in the survey container, BASELINE.md §2, "
+                      "slower than this oracle) on 1 env, R=%d, T=%d, %d steps (%.1f s)" % (n_robots, T, steps, el)}
 
 
-def bench_coverage(args):
+def bench_config4(args, with_greedy=False):
     """BASELINE.json configs[3]: Coverage-v0, 200 robots on a ~550-target map, 512 envs,
     max_nodes 1000 (the reference needs nearby_starts=False and max_nodes=1000 at this
     size, SURVEY.md finding 7). All envs share one generated map (global seed 8);
     starts, unvisited sets and actions differ per env; actions stay resident in HBM."""
     from gym_flock.envs.spatial.maps import generate_targets
     from gym_flock.vec import VecCoverage
-    R, B, M, K, W = 200, args.n_envs if args.n_envs != 256 else 512, 1000, args.steps, args.warmup
+    # a Coverage step is ~11 us of latency-bound work: at least 200 steps per window, so
+    # the window's fixed start/end cost (~0.1 ms) does not dominate (20 steps: 15.7 us)
+    R, B, M, K, W = 200, 512, 1000, max(200, args.steps), args.warmup
     np.random.seed(8)
     targets = generate_targets()
     v = VecCoverage(B, R, max_nodes=M, episode_length=10 ** 9)
     v.set_targets(targets)
     v.reset(seed=0)
     v.set_actions(np.random.RandomState(7).randint(0, 4, size=(B, R)))
+    warm = clock_warmup(lambda: v.step(resident=True), v.sync, 100.0)
+    v.reset(seed=0)  # the same starts and unvisited sets as without the warm-up
     for _ in range(W):
         v.step(resident=True)
-    v.sync()
-    v.h.timing_start(every=TIMING_EVERY)
-    t0 = time.perf_counter()
-    for _ in range(K):
-        v.step(resident=True)
-    v.sync()
-    el = time.perf_counter() - t0
-    kernel_ms, launches = v.h.timing_stop()
+    el, kernel_ms = timed(v, Ranks(None), K, lambda s: v.step(resident=True))
     # algorithmic bytes per env-step: the 8R-edge observation tail (sender, receiver,
     # edge: 12 B each) + per robot its action, node, position, visited flag and 4
     # action-target coordinates + the reward/done/step words
     per_env = 8 * R * 12 + R * (16 + 4 + 4 + 4 + 16) + 16
     achieved = B * per_env / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-    line = {"metric": "robot-steps/sec (N_robots x N_envs x steps/s), Coverage-v0 R=200",
-            "value": R * B * K / el, "unit": "robot-steps/s", "n_gpus": 1, "steps": K, "warmup": W,
-            "ms_per_step": 1e3 * el / K, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic (generated map, random starts/unvisited/actions)",
-            "config": {"workload": "Coverage-v0 step(), R=200 robots, T=%d targets, max_nodes %d, %d envs "
-                                   "(BASELINE.json configs[3])" % (len(targets), M, B)},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "cov_step_kernel",
-                         "kernel_ms": kernel_ms, "launches_timed": launches,
-                         "algorithmic_bytes_per_launch": B * per_env,
-                         "note": "latency-limited, not bandwidth-limited: one workgroup per env, two dependent "
-                                 "global round trips and the claim resolution per step (DESIGN.md)"}}
+    out = {"metric": "robot-steps/sec (N_robots x N_envs x steps/s), Coverage-v0 R=200",
+           "value": R * B * K / el, "unit": "robot-steps/s", "steps": K, "warmup": W, "clock_warmup": warm,
+           "ms_per_step": 1e3 * el / K,
+           "config": {"workload": "Coverage-v0 step(), R=200 robots, T=%d targets, max_nodes %d, %d envs "
+                                  "(BASELINE.json configs[3])" % (len(targets), M, B)},
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "cov_step_kernel",
+                        "region_ms_per_step": kernel_ms, "algorithmic_bytes_per_step": B * per_env,
+                        "note": "latency-limited, not bandwidth-limited: one workgroup per env, two dependent "
+                                "global round trips and the claim resolution per step (DESIGN.md)"}}
     if not args.no_cpu_baseline:
-        line["cpu_baseline"] = coverage_cpu_baseline(targets, R, M, min(args.cpu_seconds, 8.0))
-    line["greedy_expert"] = bench_greedy(v, targets, R, M, B, K, args)
-    print(json.dumps(line), flush=True)
+        out["cpu_baseline"] = coverage_cpu_baseline(targets, R, M, min(args.cpu_seconds, 8.0))
+    if with_greedy:
+        out["greedy_expert"] = bench_greedy(v, targets, R, M, B, K, args)
     v.close()
+    return out
 
 
 def bench_greedy(v, targets, R, M, B, K, args):
@@ -259,84 +348,67 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="processes of the all-cores CPU baseline (default: OMP_NUM_THREADS or 16, "
-                         "the box's CPU share; 0 after the flag = single core only)")
+                         "the box's CPU share)")
     ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-controller-line", action="store_true")
     ap.add_argument("--no-packed-line", action="store_true")
     ap.add_argument("--no-knn-line", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the configs[3] (Coverage) and configs[4] (N=8192) sub-objects")
     ap.add_argument("--force-dist", action="store_true",
-                    help="use the multi-rank path (gloo rendezvous + RCCL reward all-gather) even at 1 rank")
+                    help="use the multi-rank path (host channel + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
     if args.cpu_worker is not None:
         return cpu_worker(args.n_agents, args.cpu_worker, args.seed)
     if args.workload == "coverage":
-        return bench_coverage(args)
+        print(json.dumps(dict(bench_config4(args, with_greedy=True), n_gpus=1)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
     multi = world > 1 or args.force_dist
+    group = None
     if multi:
-        import torch.distributed as dist  # CPU (gloo) only: rendezvous, barrier, max
-        dist.init_process_group("gloo")
+        from gym_flock.hostgroup import HostGroup
+        group = HostGroup.from_env()
+    ranks = Ranks(group)
 
-    from gym_flock.shard import RcclRewardGather
+    from gym_flock.shard import RcclRewardGather, check_gathered
     from gym_flock.vec import VecFlockingRelative
 
     N, B, K, W = args.n_agents, args.n_envs, args.steps, args.warmup
     t_setup = time.perf_counter()
     env = VecFlockingRelative(B, N, device=local_rank, env_offset=rank * B)
-    env.reset(seed=0)
+    x_init = env.reset(seed=0)
     u = np.random.RandomState(1234 + rank).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
     env.set_actions(u)
     gather = None
     if multi:
-        uid = [env.h.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        gather = RcclRewardGather(env.h, world, rank, uid[0])
+        uid = group.broadcast_bytes(env.h.comm_unique_id() if rank == 0 else b"")
+        gather = RcclRewardGather(env.h, world, rank, uid)
     log("setup %.1fs: N=%d B=%d per GPU, world=%d" % (time.perf_counter() - t_setup, N, B, world))
 
-    def run(k, with_ctrl=False):
-        for s in range(k):
-            if with_ctrl:
-                env.step(expert=True, controller=True)
-            else:
-                env.step(resident=True)
-            if gather is not None and (s + 1) % args.metrics_every == 0:
-                gather.issue()
+    def plain(s):
+        env.step(resident=True)
+        if gather is not None and (s + 1) % args.metrics_every == 0:
+            gather.issue()
 
-    def barrier():
-        env.sync()
-        if dist is not None:
-            dist.barrier()
-
-    x_init = env.get_state()
     warm = clock_warmup(lambda: env.step(resident=True), env.sync, args.clock_warmup_ms)
     env.set_state(x_init)
-    run(W)
-    barrier()
-    env.h.timing_start(every=TIMING_EVERY)
-    t0 = time.perf_counter()
-    run(K)
-    env.sync()
-    t1 = time.perf_counter()
-    kernel_ms, launches = env.h.timing_stop()
-    barrier()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    for s in range(W):
+        plain(s)
+    elapsed, kernel_ms = timed(env, ranks, K, plain)
 
     extra = {}
     if gather is not None:
-        gather.issue()  # one all-gather after the timed region, checked against the local rewards
+        gather.issue()  # one all-gather after the timed region
         allr = gather.result()  # (steps, world*B), the last row is the latest step
-        mine = env.rewards()
-        extra["gathered_rewards_ok"] = bool(np.array_equal(allr[-1, rank * B:(rank + 1) * B], mine))
+        _, every = check_gathered(group, allr[-1], env.rewards())
+        extra["gathered_rewards_ok"] = every
+        extra["gathered_rewards_check"] = ("every rank compared the whole gathered (world x B) vector of the last "
+                                           "step with the ranks' local rewards sent over the host channel")
 
     # closed-loop step + fused controller (u = previous controller output), same workload
     if not args.no_controller_line:
@@ -345,47 +417,23 @@ def main():
         clock_warmup(lambda: env.step(expert=True, controller=True), env.sync, 50.0)
         env.reset(x=x_init)
         env.controller()
-        run(min(W, 5), with_ctrl=True)
-        barrier()
-        t2 = time.perf_counter()
-        run(K, with_ctrl=True)
-        env.sync()
-        t3 = time.perf_counter()
-        barrier()
-        ec = t3 - t2
-        if dist is not None:
-            import torch
-            t = torch.tensor([ec], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ec = float(t.item())
+        for _ in range(min(W, 5)):
+            env.step(expert=True, controller=True)
+        ec, cms = timed(env, ranks, K, lambda s: env.step(expert=True, controller=True))
         extra["step_with_controller"] = {"value": world * B * N * K / ec, "unit": "agent-steps/s",
-                                         "ms_per_step": 1e3 * ec / K}
+                                         "ms_per_step": 1e3 * ec / K, "region_ms_per_step": cms}
 
     # packed output mode: adjacency bits + degree instead of the dense rows
     if not args.no_packed_line:
         clock_warmup(lambda: env.step(resident=True, network="packed"), env.sync, 50.0)
         env.reset(x=x_init)
         env.step(resident=True, network="packed")
-        barrier()
-        env.h.timing_start(every=TIMING_EVERY)
-        t4 = time.perf_counter()
-        for _ in range(K):
-            env.step(resident=True, network="packed")
-        env.sync()
-        t5 = time.perf_counter()
-        pk_ms, _ = env.h.timing_stop()
-        barrier()
-        ep = t5 - t4
-        if dist is not None:
-            import torch
-            t = torch.tensor([ep], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ep = float(t.item())
+        ep, pk_ms = timed(env, ranks, K, lambda s: env.step(resident=True, network="packed"))
         wn = (N + 63) // 64
         pk_bytes = B * (8 * N * wn + 4 * N + 96 * N + 8)
         extra["packed_network"] = {
             "value": world * B * N * K / ep, "unit": "agent-steps/s", "ms_per_step": 1e3 * ep / K,
-            "kernel_ms": pk_ms, "algorithmic_bytes_per_launch": pk_bytes,
+            "region_ms_per_step": pk_ms, "algorithmic_bytes_per_step": pk_bytes,
             "achieved_GBs": pk_bytes / (pk_ms * 1e-3) / 1e9 if pk_ms > 0 else None,
             "note": "adjacency as bits (N*ceil(N/64)*8 B) + int32 degree per env instead of the dense "
                     "float32 network; the pair work, not HBM, bounds this mode"}
@@ -400,33 +448,17 @@ def main():
         envk.reset(x=x_init)
         for _ in range(min(W, 5)):
             envk.step(resident=True, knn=True)
-        envk.sync()
-        if dist is not None:
-            dist.barrier()
-        t6 = time.perf_counter()
-        for _ in range(K):
-            envk.step(resident=True, knn=True)
-        envk.sync()
-        t7 = time.perf_counter()
-        if dist is not None:
-            dist.barrier()
-        ek = t7 - t6
-        if dist is not None:
-            import torch
-            t = torch.tensor([ek], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            ek = float(t.item())
+        ek, kk_ms = timed(envk, ranks, K, lambda s: envk.step(resident=True, knn=True))
         extra["flocking_v0_knn7"] = {
             "value": world * B * N * K / ek, "unit": "agent-steps/s", "ms_per_step": 1e3 * ek / K,
+            "region_ms_per_step": kk_ms, "ratio_to_plain_step": ek / elapsed,
             "note": "Flocking-v0 step: FlockingRelative step + 7-NN observation (idx + obs), from the "
-                    "synthetic init under the same random actions; two launches per step"}
+                    "synthetic init under the same random actions"}
         envk.close()
+    env.close()
 
     if rank == 0:
         value = world * B * N * K / elapsed
-        bytes_launch = B * step_bytes(N)
-        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-        traffic = load_traffic(N, B)
         line = {
             "metric": "agent-steps/sec (N_agents×N_envs×steps/s), FlockingRelative N=%d" % N,
             "value": value,
@@ -446,32 +478,21 @@ def main():
                        "n_agents": N, "envs_per_gpu": B, "global_envs": world * B,
                        "outputs": "network (N,N) f32 + state_values (N,6) f32 + reward, in HBM",
                        "parallelism": "env-sharded dp%d, RCCL reward all-gather" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "flock_step_kernel<DYN,f32 u>", "kernel_ms": kernel_ms,
-                         "steps_timed": launches, "algorithmic_bytes_per_step": bytes_launch,
-                         "launches_per_step": 2 if B >= 2 else 1,
-                         "timing": "device time per step over the timed region (HIP events on the "
-                                   "handle's stream after it joins the second): each step is two "
-                                   "concurrent half-batch launches of the kernel on two streams, "
-                                   "so kernel_ms and the bytes are per step (both launches)"},
+            "roofline": flock_roofline(N, B, kernel_ms, 2 if B >= 2 else 1),
         }
         line.update(extra)
+        if world == 1 and not args.no_other_configs:
+            log("config 4 (Coverage R=200 x 512)...")
+            line["coverage_config4"] = bench_config4(args)
+            log("config 5 (N=8192 x 32)...")
+            line["n8192_config5"] = bench_config5(args)
         if world == 1 and not args.no_cpu_baseline:
-            log("cpu baseline (oracle, 1 core, ~%.0fs)..." % args.cpu_seconds)
-            one = cpu_baseline(N, args.cpu_seconds)
+            log("cpu baseline (cpu_ref, 1 core, ~%.0fs)..." % args.cpu_seconds)
             procs = args.cpu_procs or min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
-            if procs > 1:
-                log("cpu baseline, all cores: %d processes x ~%.0fs..." % (procs, args.cpu_seconds / 2))
-                agg, ok = cpu_baseline_all_cores(N, args.cpu_seconds / 2, procs)
-                one = dict(one, per_core=one["value"], value=agg, cores=ok,
-                           sample=one["sample"] + "; value = %d such processes at once (OMP_NUM_THREADS=1 "
-                                                  "each, %.0f s), summed" % (ok, args.cpu_seconds / 2))
-            line["cpu_baseline"] = one
+            line["cpu_baseline"] = flock_cpu_baseline(N, args.cpu_seconds, procs)
         print(json.dumps(line), flush=True)
-    env.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if group is not None:
+        group.close()
 
 
 if __name__ == "__main__":

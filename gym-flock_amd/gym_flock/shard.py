@@ -5,13 +5,17 @@ Envs are independent, so the batch is split into contiguous ranges, one per rank
 metrics path: per-env rewards are all-gathered so every rank (or the trainer on
 rank 0) sees the whole batch's rewards in global env order.
 
-Two transports for that all-gather:
+Transports for that all-gather:
   - RcclRewardGather: RCCL over xGMI, issued by libgymflock on a side stream right
     after the step kernel (fe_allgather_rewards) — the GPU path.
-  - GlooRewardGather: torch.distributed (gloo) on host copies — used by the CPU
-    tests and by callers that already hold a gloo group.
-torch is imported lazily and only by the gloo transport: the env itself has no
-PyTorch dependency.
+  - HostRewardGather: the torch-free host channel (hostgroup.HostGroup) on host
+    copies — the CPU tests and CPU-only callers.
+  - GlooRewardGather: torch.distributed (gloo) on host copies — for callers that
+    already hold a gloo group.
+check_gathered() is how every rank verifies the WHOLE gathered vector against the
+ranks' local rewards, exchanged over the host channel. torch is imported lazily and
+only by the gloo transport: the env and the multi-rank bench have no PyTorch
+dependency.
 """
 import numpy as np
 
@@ -43,6 +47,27 @@ class RcclRewardGather:
     def result(self):
         g = self.handle.gathered_rewards()  # (world, steps, B)
         return np.concatenate(list(g), axis=1)
+
+
+class HostRewardGather:
+    """All-gather of per-env rewards over a HostGroup (host copies, any shard sizes)."""
+
+    def __init__(self, group):
+        self.group = group
+
+    def gather(self, local_rewards):
+        parts = self.group.allgather_bytes(np.ascontiguousarray(local_rewards, dtype=np.float64).tobytes())
+        return np.concatenate([np.frombuffer(p, np.float64) for p in parts])
+
+
+def check_gathered(group, gathered, local_rewards):
+    """Every rank checks the whole gathered (world * B,) reward vector against the ranks'
+    local rewards, sent over the host channel and concatenated in rank order. Returns
+    (this rank's check, every rank's check)."""
+    want = HostRewardGather(group).gather(local_rewards)
+    got = np.asarray(gathered, dtype=np.float64).ravel()
+    ok = bool(got.shape == want.shape and np.array_equal(got, want))
+    return ok, all(group.allgather(ok))
 
 
 class GlooRewardGather:
