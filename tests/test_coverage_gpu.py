@@ -231,3 +231,53 @@ def test_split_steps_match_single_stream():
         h.close()
     for a, b in zip(*runs):
         np.testing.assert_array_equal(a, b)
+
+
+def test_full_config4_batch_properties_and_sampled_parity():
+    """BASELINE.json configs[3] at full size: 512 envs x 200 robots, max_nodes 1000, one
+    generated ~550-target map (global seed 8, as bench.py), random actions for 8 steps.
+    Whole batch: every env's robots sit on target nodes (two can share one: a robot
+    blocked after an earlier robot claimed its node stays, coverage.py:187-200, as the
+    oracle shows on the sampled envs), rewards are the newly visited counts (summed
+    rewards = visited growth), and the observation tails name only robots and targets. Sampled envs (first, middle, last): full observations, rewards, robots and
+    visited sets bit-exact against the oracle every step."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, R, M = 512, 200, 1000
+    np.random.seed(8)
+    targets = generate_targets()
+    T = len(targets)
+    v = VecCoverage(B, R, max_nodes=M, episode_length=10 ** 9)
+    v.set_targets(targets)
+    start, visited0 = v.reset(seed=0)
+    # the reset's own observation already marks the start nodes visited (no reward)
+    vis0 = np.stack([v.h.visited(b)[:T].astype(np.int64) for b in range(B)])
+    sample = (0, 257, 511)
+    orcs = {}
+    for b in sample:
+        o = oc.CoverageOracle(targets, R, M)
+        o.reset(start[b], np.nonzero(visited0[b, :T] == 0)[0] + R)
+        orcs[b] = o
+    rs = np.random.RandomState(9)
+    total = np.zeros(B)
+    for t in range(8):
+        acts = rs.randint(0, 4, size=(B, R)).astype(np.int32)
+        v.step(acts)
+        r, d = v.rewards()
+        assert not d.any() and (r >= 0).all()
+        total += r
+        for b in sample:
+            obs, rr, dd = orcs[b].step(acts[b])
+            assert_obs(v.obs(b), {k + "0": val for k, val in obs.items()})
+            assert r[b] == rr and d[b] == dd
+            np.testing.assert_array_equal(v.h.robots(b)[1], orcs[b].closest())
+    for b in range(B):
+        nodes = v.h.robots(b)[1]
+        assert nodes.min() >= R and nodes.max() < R + T
+        vis = v.h.visited(b)[:T].astype(np.int64)
+        assert (vis >= vis0[b]).all() and vis.sum() - vis0[b].sum() == total[b]
+    for b in (1, 300):
+        o = v.obs(b)
+        s, rcv = o["senders"], o["receivers"]
+        live = s >= 0
+        assert (s[live] < R + T).all() and (rcv[live] < R + T).all()
+    v.close()

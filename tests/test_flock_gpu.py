@@ -514,3 +514,34 @@ def test_knn_pipelined_back_to_back():
             np.testing.assert_array_equal(idx[b], ridx)
             np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
     h.close()
+
+
+def test_full_config5_batch_sampled_parity():
+    """BASELINE.json configs[4] at full size: 32 envs x N=8192 (8.6 GB of network), one
+    step with the fused controller. Whole batch: every env's state bit-exact and its
+    reward (rtol 1e-12) against the oracle, and the mean-pooled rows of 6 rows per env
+    summing to 1. Sampled envs (0, 13, 31): 24 rows each (tile and block edges, random
+    rows) of the network bit-exact, state_values and controller against the oracle."""
+    n, B = 8192, 32
+    x0 = synthetic_batch(B, n, seed0=5)
+    u = np.random.RandomState(55).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B)
+    h.set_state(x0)
+    h.step(u, nat.FE_WITH_CONTROLLER)
+    x1, rew, sv, ctrl = h.get_state(), h.rewards(), h.state_values(), h.controls()
+    rs = np.random.RandomState(56)
+    for b in range(B):
+        xo = orc.integrate(x0[b], u[b])
+        np.testing.assert_array_equal(x1[b], xo)
+        np.testing.assert_allclose(rew[b], orc.reward(xo), rtol=1e-12)
+        for r in rs.choice(n, 6, replace=False):
+            row = h.network_rows(b, int(r), 1)[0].astype(np.float64)
+            assert row.sum() == 0 or abs(row.sum() - 1.0) < 1e-5
+    for b in (0, 13, 31):
+        rows = np.unique(np.concatenate([[0, 15, 16, 511, 512, 8191], rs.choice(n, 18, replace=False)]))
+        ref = orc.step_rows(x0[b], u[b], rows, with_controller=True)
+        for k, r in enumerate(rows):
+            np.testing.assert_array_equal(h.network_rows(b, int(r), 1)[0], ref["network"][k].astype(np.float32))
+        close_sv(sv[b][rows], ref["state_values"])
+        np.testing.assert_allclose(ctrl[b][rows], ref["ctrl"], rtol=1e-9, atol=1e-12)
+    h.close()
