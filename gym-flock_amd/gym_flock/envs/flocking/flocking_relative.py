@@ -20,6 +20,8 @@ Differences a caller can observe:
     draws, then falls back to a single draw (the reference would loop forever,
     SURVEY.md finding 5); `reset_mode='synthetic'` skips the rejection.
 """
+import warnings
+
 import numpy as np
 
 from ... import _native as nat
@@ -198,6 +200,12 @@ class FlockingRelativeEnv(Env):
             x = draw_swarm(self.n_agents, self.r_max, self.v_max, self.v_bias)
             if self.reset_mode != "reference" or self._accept(x):
                 break
+        else:
+            # the reference loops until a draw passes (flocking_relative.py:164), which
+            # never ends for N >~ 200; this keeps the last draw instead, and says so
+            warnings.warn("FlockingRelativeEnv.reset(): no draw met the reference's acceptance test "
+                          "(min degree >= 2, min distance >= 0.1) in %d attempts; keeping the last one"
+                          % self.reset_max_attempts, RuntimeWarning, stacklevel=2)
         self.mean_vel = np.mean(x[:, 2:4], axis=0)
         self.init_vel = x[:, 2:4]
         self.x = x
