@@ -73,8 +73,11 @@ struct fe_handle {
   float* net = nullptr;
   double* reward_ring = nullptr;        // kRewardSlots x B
   int rslot = 0;
-  int32_t* knn_idx = nullptr;
-  float* knn_obs = nullptr;
+  // kNN outputs, one pair per state buffer: knn_idx[i] / knn_obs[i] belong to x[i], so
+  // a fused step (which writes those of its output state) never overlaps the rim kNN of
+  // the previous state, and the kread events that guard x[i] guard them too
+  int32_t* knn_idx[2] = {nullptr, nullptr};
+  float* knn_obs[2] = {nullptr, nullptr};
   double* vel_diffs = nullptr;
   double* min_dists = nullptr;
   int32_t* degree = nullptr;
@@ -204,7 +207,7 @@ void release(fe_handle* h) {
   if (h->kstream) hipStreamSynchronize(h->kstream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx, h->knn_obs, h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
+                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
                   h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -260,19 +263,35 @@ int packed_outputs(fe_handle* h, bool bits, gf::StepArgs& a, int* bw) {
   return GF_OK;
 }
 
-// Flocking-v0: the step also writes this state's adjacency bits and degrees, from which
-// the kNN kernel that follows ranks each agent's neighbours.
-int knn_mode(const fe_handle* h, int flags) {
-  return ((flags & FE_WITH_KNN) && h->cfg.n_neighbors > 0) ? 1 : 0;
+// Flocking-v0 k nearest with a step (0: none).
+//  1: the step also writes this state's adjacency bits and degrees, from which the kNN
+//     kernel that follows ranks each agent's neighbours;
+//  2: (fe_step, k = 7, no variant) the step ranks them itself, in its feature pass, and
+//     the kNN kernel that follows (rim mode) only ranks the rows it could not.
+int knn_mode(const fe_handle* h, int flags, bool dyn) {
+  if (!(flags & FE_WITH_KNN) || h->cfg.n_neighbors <= 0) return 0;
+  const bool variant = h->has_variant || h->dt_per_env;
+  if (dyn && gf::step_fused_knn_ok(h->cfg.n_agents, h->R, h->cfg.n_neighbors, variant, h->prefetch != 0)) return 2;
+  return 1;
 }
 
 // Output buffers of a launch that writes x[xw] (xw < 0: none): picks the bits buffer and
 // orders the step streams after the kNN launches still reading what it overwrites.
 int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a, int xw) {
-  const int km = knn_mode(h, flags);
+  const int km = knn_mode(h, flags, xw >= 0);
   const bool packed = flags & FE_PACKED_NETWORK;
   int bw = -1;
   if (int rc = packed_outputs(h, packed || km == 1, a, &bw)) return rc;
+  if (km == 2) {  // fused selection into the kNN buffers of the state it writes
+    const int N = h->cfg.n_agents;
+    int jb = 1;
+    while ((1 << jb) < N) ++jb;
+    a.knn_idx = h->knn_idx[xw];
+    a.knn_obs = h->knn_obs[xw];
+    a.knn_jbits = jb;
+    a.knn_qmax = (1u << (32 - jb)) - 2u;  // below the all-ones empty-slot key
+    a.knn_scale = std::ldexp(1.0, 32 - jb) / (h->cfg.comm_radius * h->cfg.comm_radius);
+  }
   if (int rc = wait_knn_readers(h, xw, bw)) return rc;
   if (bw >= 0) h->bits_cur = bw;  // the launch that follows fills it
   if (packed) h->has_packed = true;
@@ -318,7 +337,7 @@ gf::StepArgs base_args(fe_handle* h) {
 
 int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
   gf::StepArgs a = a_in;
-  if (ctrl && !a.variant && h->R_ctrl != a.R) {
+  if (ctrl && !a.variant && !a.knn_idx && h->R_ctrl != a.R) {  // fused kNN keeps R (slices >= k)
     a.R = h->R_ctrl;
     a.bpe = (a.N + a.R - 1) / a.R;
   }
@@ -349,6 +368,11 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     if (a.dt_env) a1.dt_env = a.dt_env + B0;
     if (a.adj_bits) a1.adj_bits = a.adj_bits + e0 * Wn;
     if (a.degree_out) a1.degree_out = a.degree_out + e0;
+    if (a.knn_idx) {
+      const size_t K = h->cfg.n_neighbors;
+      a1.knn_idx = a.knn_idx + e0 * K;
+      a1.knn_obs = a.knn_obs + e0 * 4 * K;
+    }
     hipError_t e = gf::launch_step(a, dyn, uf64, ctrl, h->stream);
     if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
     if (e != hipSuccess) return fail_hip("flock_step_kernel launch", e);
@@ -381,8 +405,9 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
   return GF_OK;
 }
 
-// kNN of the current state; uses_adj: the last launch wrote this state's adjacency
-// (packed outputs), which lets agents with >= k neighbours rank only those.
+// kNN of the current state (mode: knn_mode; 0 = a full kNN with no step behind it):
+// 1: the last launch wrote this state's adjacency (packed outputs), which lets agents
+// with >= k neighbours rank only those; 2: the last launch ranked the rows it could.
 int launch_knn_cur(fe_handle* h, int mode) {
   // on kstream after everything on both step streams (both halves' state and bits)
   GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
@@ -395,8 +420,9 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.x = h->x[h->cur];
   k.adj_bits = mode == 1 ? h->adj_bits[h->bits_cur] : nullptr;
   k.degree = mode == 1 ? h->pdeg[h->bits_cur] : nullptr;
-  k.idx = h->knn_idx;
-  k.obs = h->knn_obs;
+  k.idx = h->knn_idx[h->cur];
+  k.obs = h->knn_obs[h->cur];
+  k.rim = mode == 2;
   k.N = h->cfg.n_agents;
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
@@ -470,8 +496,10 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (rc = dalloc(reinterpret_cast<double**>(&h->u), h->BN * 2)) || (rc = dalloc(&h->ctrl[0], h->BN * 2)) ||
       (rc = dalloc(&h->ctrl[1], h->BN * 2)) || (rc = dalloc(&h->sv, h->BN * 6)) ||
       (rc = dalloc(&h->net, h->BN * N)) || (rc = dalloc(&h->reward_ring, (size_t)kRewardSlots * B)) ||
-      (rc = dalloc(&h->knn_idx, h->BN * cfg->n_neighbors)) ||
-      (rc = dalloc(&h->knn_obs, h->BN * 4 * cfg->n_neighbors))) {
+      (rc = dalloc(&h->knn_idx[0], h->BN * cfg->n_neighbors)) ||
+      (rc = dalloc(&h->knn_idx[1], h->BN * cfg->n_neighbors)) ||
+      (rc = dalloc(&h->knn_obs[0], h->BN * 4 * cfg->n_neighbors)) ||
+      (rc = dalloc(&h->knn_obs[1], h->BN * 4 * cfg->n_neighbors))) {
     release(h);
     return rc;
   }
@@ -586,7 +614,7 @@ int fe_compute_helpers(fe_handle* h, int flags) {
   a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
-  const int km = knn_mode(h, flags);
+  const int km = knn_mode(h, flags, false);
   if (int rc = prepare_outputs(h, flags, a, -1)) return rc;
   if (int rc = timed_launch(h, a, false, false, ctrl)) return rc;
   if (ctrl) {
@@ -639,7 +667,7 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   a.network = (flags & FE_NO_NETWORK) ? nullptr : h->net;
   a.ctrl_out = ctrl ? h->ctrl[h->ccur ^ 1] : nullptr;
   a.reward = cur_reward(h);
-  const int km = knn_mode(h, flags);
+  const int km = knn_mode(h, flags, true);
   if (int rc = prepare_outputs(h, flags, a, h->cur ^ 1)) return rc;
   if (int rc = timed_launch(h, a, true, uf64, ctrl)) return rc;
   h->cur ^= 1;
@@ -810,8 +838,10 @@ int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs) {
   const size_t K = h->cfg.n_neighbors, N = h->cfg.n_agents;
   const size_t off = env < 0 ? 0 : env * N;
   const size_t cnt = env < 0 ? h->BN : N;
-  if (idx) GF_HIP(hipMemcpyAsync(idx, h->knn_idx + off * K, cnt * K * 4, hipMemcpyDeviceToHost, h->stream));
-  if (obs) GF_HIP(hipMemcpyAsync(obs, h->knn_obs + off * 4 * K, cnt * 4 * K * 4, hipMemcpyDeviceToHost, h->stream));
+  const int32_t* kidx = h->knn_idx[h->cur];
+  const float* kobs = h->knn_obs[h->cur];
+  if (idx) GF_HIP(hipMemcpyAsync(idx, kidx + off * K, cnt * K * 4, hipMemcpyDeviceToHost, h->stream));
+  if (obs) GF_HIP(hipMemcpyAsync(obs, kobs + off * 4 * K, cnt * 4 * K * 4, hipMemcpyDeviceToHost, h->stream));
   GF_HIP(hipStreamSynchronize(h->stream));
   return GF_OK;
 }
@@ -826,8 +856,8 @@ int fe_device_buffers(fe_handle* h, fe_buffers* out) {
   out->network = h->net;
   out->controls = h->ctrl[h->ccur];
   out->rewards = cur_reward(h);
-  out->knn_idx = h->knn_idx;
-  out->knn_obs = h->knn_obs;
+  out->knn_idx = h->knn_idx[h->cur];  // the current state's (they alternate with the state)
+  out->knn_obs = h->knn_obs[h->cur];
   out->stream = h->stream;
   out->adj_bits = h->adj_bits[h->bits_cur];
   out->degree = h->pdeg[h->bits_cur];

@@ -19,8 +19,11 @@ constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float6
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
 constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
-constexpr int kKnnFewSlow = 16;     // kNN: up to this many full-scan rows per workgroup
-                                    // go wave-cooperative, more go one row per thread
+constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
+// kNN LDS: positions (16 B per agent), the grid's cell offsets, agent indices by cell
+constexpr size_t knn_lds_bytes(int N) {
+  return (size_t)N * 16 + (size_t)(kKnnGridCells + 1) * 4 + (((size_t)N * 2 + 15) / 16) * 16;
+}
 
 // One batched hot-path launch. Pointers are device pointers; all per-env arrays
 // are [B][N][...] contiguous.
@@ -61,7 +64,18 @@ struct StepArgs {
   const double* dt_env;   // (B) per-env dt of this step, or nullptr (dt)
   uint64_t* adj_bits;     // (B,N,Wn) packed adjacency or nullptr
   int32_t* degree_out;    // (B,N) degrees or nullptr
+  // Flocking-v0 k-nearest selection fused into the feature pass (kStepFusedK neighbours):
+  // rows the step can rank exactly get idx + obs; the others get idx[row*K] = -1 and
+  // are finished by flock_knn_kernel in rim mode. Key of a neighbour pair:
+  // (min(floor(r2 * knn_scale), knn_qmax) << knn_jbits) | j (see the kernel).
+  int32_t* knn_idx;       // (B,N,K) or nullptr: no fused selection
+  float* knn_obs;         // (B,N,4K)
+  double knn_scale;
+  unsigned knn_qmax;
+  int knn_jbits;
 };
+
+constexpr int kStepFusedK = 7;  // Flocking-v0's n_neighbors (flocking.py:9)
 
 struct KnnArgs {
   const double* x;        // (B,N,4) current state
@@ -70,6 +84,7 @@ struct KnnArgs {
   int N, B, K;
   const uint64_t* adj_bits;  // (B,N,Wn) adjacency of x from the step, or nullptr
   const int32_t* degree;     // (B,N) with adj_bits
+  int rim;                   // only rows the fused step left unranked (idx[row*K] < 0)
   int diag;                  // ablation: 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path
 };
 
@@ -88,6 +103,9 @@ int step_tile(int N);
 size_t step_lds_bytes(int N, int R, int T, bool ctrl);
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
+// Whether a step of this geometry can carry the fused k-nearest selection (K ==
+// kStepFusedK, no variant, no tile prefetch, at least K word-slices per row).
+bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
 // Diagnostic: stream `bytes` of float4 stores into p (nt = non-temporal), the

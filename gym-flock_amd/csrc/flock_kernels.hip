@@ -469,6 +469,12 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 #ifndef GF_STEP_WAVES_CTRL
 #define GF_STEP_WAVES_CTRL 6
 #endif
+#ifndef GF_STEP_WAVES_KNN
+#define GF_STEP_WAVES_KNN 6
+#endif
+#ifndef GF_STEP_WAVES_KNN_CTRL
+#define GF_STEP_WAVES_KNN_CTRL 5
+#endif
 // Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
 // wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
 // its HW_ID / XCC_ID, for scripts/phase_timeline.py. Product builds compile it out.
@@ -487,8 +493,14 @@ __device__ unsigned long long gf_stamp_buf[8192 * 16];
 // path carries none of their instructions.
 // PF (1 or 2): each tile's global loads are issued PF tiles ahead (raw x/u in registers,
 // T <= 2 * kThreads), for envs of many tiles; its register budget is that of 4 waves.
-template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0>
-__global__ __launch_bounds__(kThreads, VAR ? 1 : (PF ? GF_STEP_WAVES_PF : (CTRL ? GF_STEP_WAVES_CTRL : GF_STEP_WAVES_PLAIN)))
+// KN > 0 (Flocking-v0, flocking.py:20-25): each (row, slice) thread also keeps the KN
+// smallest keys of its neighbours, the S slices of a row are merged after the last
+// feature pass, and the row's k nearest indices and observation are written (below).
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
+__global__ __launch_bounds__(kThreads, VAR ? 1
+                                           : (PF ? GF_STEP_WAVES_PF
+                                                 : (KN ? (CTRL ? GF_STEP_WAVES_KNN_CTRL : GF_STEP_WAVES_KNN)
+                                                       : (CTRL ? GF_STEP_WAVES_CTRL : GF_STEP_WAVES_PLAIN))))
 void flock_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
@@ -547,6 +559,17 @@ void flock_step_kernel(StepArgs a) {
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
 
   const int i_row = i0 + fr;  // global row of this thread's feature slice
+  // Fused k-nearest selection (KN > 0). A neighbour's key is
+  //   (q << jbits) | j,  q = min(floor(r2 * knn_scale), knn_qmax),
+  // a 32-bit integer whose order is (q, j): q never decreases as r2 grows, so keys of
+  // different q are in true (r2, j) order. Each thread keeps its KN smallest keys sorted
+  // (a min/max exchange chain, 2 VALU per entry, no branches); columns arrive in
+  // ascending j per thread, but the order does not matter here.
+  [[maybe_unused]] unsigned kk[KN > 0 ? KN : 1];
+  if constexpr (KN > 0) {
+#pragma unroll
+    for (int m = 0; m < KN; ++m) kk[m] = 0xFFFFFFFFu;
+  }
   // one neighbour pair (row fr = me, tile column c): features and controller gradient.
   // The row's state is read from LDS per feature pass, so it holds no registers
   // through pass 1.
@@ -554,6 +577,19 @@ void flock_step_kernel(StepArgs a) {
     const St o = tile[c];
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
+    if constexpr (KN > 0) {
+      if (isadj) {
+        const double qd = r2 * a.knn_scale;  // r2 < comm_radius^2 here: 0 <= qd <~ 2^qbits
+        const unsigned q = qd < static_cast<double>(a.knn_qmax) ? static_cast<unsigned>(qd) : a.knn_qmax;
+        unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
+#pragma unroll
+        for (int m = 0; m < KN; ++m) {
+          const unsigned lo = min(kk[m], v);
+          v = max(kk[m], v);
+          kk[m] = lo;
+        }
+      }
+    }
     // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
     // reference's two divisions; far inside the float32 outputs' tolerance)
     const double ir = 1.0 / r2, irr = ir * ir;
@@ -769,6 +805,54 @@ void flock_step_kernel(StepArgs a) {
   feature_pass(jl, nchl);
   GF_STAMP(9);
 
+  if constexpr (KN > 0) {
+    // Merge the S slices' lists of each row (S consecutive lanes): KN + 1 rounds of an
+    // S-lane minimum; the lane whose head won pops it (keys are distinct: j differs).
+    // Round m's winner is the row's m-th nearest; lane fs keeps winner fs. The result
+    // is the reference's argsort order (ties to the lower index, as the kNN kernel)
+    // when the KN + 1 smallest keys have distinct q: then the top KN are strictly
+    // closer than every other agent and strictly ordered among themselves. A row with
+    // fewer than KN neighbours (its KN nearest include non-neighbours) or equal q among
+    // those keys gets idx = -1 and is ranked exactly by flock_knn_kernel (rim mode).
+    const int jb = a.knn_jbits;
+    unsigned mine = 0xFFFFFFFFu, prevq = 0xFFFFFFFFu;
+    bool slow = false;
+#pragma unroll
+    for (int m = 0; m <= KN; ++m) {
+      unsigned w = kk[0];
+      for (int o = 1; o < S; o <<= 1) w = min(w, static_cast<unsigned>(__shfl_xor(static_cast<int>(w), o)));
+      const bool pop = kk[0] == w;
+#pragma unroll
+      for (int q = 0; q + 1 < KN; ++q) kk[q] = pop ? kk[q + 1] : kk[q];
+      kk[KN - 1] = pop ? 0xFFFFFFFFu : kk[KN - 1];
+      const bool real = w != 0xFFFFFFFFu;
+      if (m < KN) {
+        mine = (fs == m) ? w : mine;
+        slow |= !real;
+      }
+      const unsigned qw = w >> jb;
+      slow |= real && m > 0 && qw == prevq;
+      prevq = qw;
+    }
+    if (frow) {
+      const size_t g = env0 + i_row;
+      if (slow) {
+        if (fs == 0) a.knn_idx[g * KN] = -1;
+      } else if (fs < KN) {
+        const int j = static_cast<int>(mine & ((1u << jb) - 1u));
+        a.knn_idx[g * KN + fs] = j;
+        const St o = state_from_raw<DYN, UF64>(a, load_raw<DYN, UF64>(a, env0 + j));
+        const St me = rows[fr];
+        float4 ob;
+        ob.x = static_cast<float>(me.px - o.px);
+        ob.y = static_cast<float>(me.py - o.py);
+        ob.z = static_cast<float>(me.vx - o.vx);
+        ob.w = static_cast<float>(me.vy - o.vy);
+        reinterpret_cast<float4*>(a.knn_obs)[g * KN + fs] = ob;
+      }
+    }
+  }
+
   const St me = frow ? rows[fr] : St{0, 0, 0, 0};
   step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
                                       frow && fs == 0, S, tid);
@@ -780,127 +864,41 @@ void flock_step_kernel(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// Full-scan kNN row without a sorted insertion per column (the insertions diverge: in a
-// dispersed swarm ~80 % of the columns trigger one in some lane of the wave).
-//   A: float32 r2 to every column, folded into 2K group minima (column j -> group j mod
-//      2K); the K-th smallest group minimum B bounds the row's K-th smallest float32 r2
-//      from above (K distinct columns reach it).
-//   B: every column whose float32 r2 <= B + margin is a candidate (packed u16 indices
-//      in registers). The margin covers the float32 error of both r2 (positions rounded
-//      to float32, coordinates <= P: |r2_f - r2| <= 2^-20.5 P sqrt(r2) + 2^-23 r2 +
-//      2^-44 P^2), so every column of the exact top K is a candidate.
-//   C: the candidates are ranked exactly (float64 r2, ties to the lower index).
-// Returns false (the caller scans with insertions) when the bound is not finite, the
-// coordinates are huge, or the candidates overflow the register list.
+// Flocking-v0 observation (flocking.py:20-25): the K nearest agents by r2 (self
+// excluded by its infinite r2), ties to the lower index. One thread per agent.
+//  * Neighbour path: when the step left this state's adjacency behind (adj_bits) and
+//    the agent has at least K neighbours, its K nearest are all neighbours (every
+//    non-neighbour is farther: r2 >= comm_radius^2 > any neighbour's), so only its ~deg
+//    set bits are ranked.
+//  * Rim mode: the fused step already ranked every row it could (idx >= 0); only the
+//    others are ranked here.
+//  * Every remaining row is ranked through a uniform grid of the env's agents, built
+//    in LDS by the workgroup (counting sort of agent indices by cell, ~2 agents per
+//    cell): the row visits rings of cells around its own, Chebyshev distance d = 0, 1,
+//    ..., ranking each agent there exactly (float64 r2, sorted (r2, j) insertion). An
+//    agent in a ring beyond d is at least d*h - err away (h: cell size, err: the
+//    rounding of cell assignment), so the row stops once its K-th r2 is below that
+//    bound squared. The visiting order does not matter: the insertion is a total order
+//    on (r2, j). Non-finite or extreme coordinates fall back to a scan of every column.
 template <int K>
-__device__ __forceinline__ bool knn_bounded_scan(const double2* lpos, const float2* lpf, int N, int i, int r0,
-                                                 double pxi, double pyi, float Pf, double (&kr)[K], int (&kj)[K]) {
-  constexpr int G = 2 * K;
-  constexpr int C = K <= 8 ? 32 : 64;  // candidate capacity (C / 2 registers)
-  const f2v me = {static_cast<float>(pxi), static_cast<float>(pyi)};
-  const f2v* lp = reinterpret_cast<const f2v*>(lpf);
-  auto r2f = [&](int j) {  // packed: one subtract and one multiply for x and y
-    const f2v d = me - lp[j];
-    const f2v d2 = d * d;
-    return d2.x + d2.y;
-  };
-  // The columns split into three ranges: the wave's own 64 rows [r0, r1) (each lane's
-  // self is among them: checked) and the rest (no check). r0 is wave-uniform.
-  const int r1 = min(N, r0 + 64);
-  float m[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) m[g] = __builtin_inff();
-  // groups: any partition into G disjoint column sets gives a valid bound
-  auto groups = [&](int s, int e, auto self) {
-    int j = s;
-    for (; j + G <= e; j += G) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float r = r2f(j + g);
-        m[g] = fminf(m[g], (decltype(self)::value && j + g == i) ? __builtin_inff() : r);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (j + g < e && !(decltype(self)::value && j + g == i)) m[g] = fminf(m[g], r2f(j + g));
-  };
-  groups(0, r0, std::false_type{});
-  groups(r0, r1, std::true_type{});
-  groups(r1, N, std::false_type{});
-  float sk[K];  // the K smallest group minima, branch-free
-#pragma unroll
-  for (int q = 0; q < K; ++q) sk[q] = __builtin_inff();
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float v = m[g];
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-      const float lo = fminf(sk[q], v);
-      v = fmaxf(sk[q], v);
-      sk[q] = lo;
-    }
-  }
-  if (!(sk[K - 1] < __builtin_inff()) || !(Pf < 1.0e15f)) return false;
-  const double Bd = sk[K - 1], P = static_cast<double>(Pf) * (1.0 + 0x1p-20);
-  const double lim = Bd + ldexp(P * (sqrt(Bd) + 1.0) + Bd + 1.0, -18) + ldexp(P * P, -39);
-  float thr = static_cast<float>(lim);
-  if (static_cast<double>(thr) < lim) thr = nextafterf(thr, __builtin_inff());
-
-  unsigned cand[C / 2];
-#pragma unroll
-  for (int q = 0; q < C / 2; ++q) cand[q] = 0;
-  int cnt = 0;
-  auto push = [&](int j) {
-    if (cnt < C) {
-#pragma unroll
-      for (int q = C / 2 - 1; q > 0; --q) cand[q] = (cand[q] << 16) | (cand[q - 1] >> 16);
-      cand[0] = (cand[0] << 16) | static_cast<unsigned>(j);
-    }
-    ++cnt;
-  };
-  // 8 columns per round: their loads and compares are independent, and a lane appends
-  // only in the rounds where it has a hit
-  auto cands = [&](int s, int e, auto self) {
-    constexpr int U = 8;
-    int jb = s;
-    for (; jb + U <= e; jb += U) {
-      unsigned hm = 0;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        hm |= static_cast<unsigned>(r2f(jb + u) <= thr && !(decltype(self)::value && jb + u == i)) << u;
-      while (hm) {
-        const int u = __builtin_ctz(hm);
-        hm &= hm - 1;
-        push(jb + u);
-      }
-    }
-    for (int j = jb; j < e; ++j)
-      if (r2f(j) <= thr && !(decltype(self)::value && j == i)) push(j);
-  };
-  cands(0, r0, std::false_type{});
-  cands(r0, r1, std::true_type{});
-  cands(r1, N, std::false_type{});
-  if (cnt > C) return false;
-  for (int q = 0; q < cnt; ++q) {
-    const int j = static_cast<int>(cand[0] & 0xffffu);
-#pragma unroll
-    for (int p = 0; p + 1 < C / 2; ++p) cand[p] = (cand[p] >> 16) | (cand[p + 1] << 16);
-    cand[C / 2 - 1] >>= 16;
-    const double2 p = lpos[j];
-    const double dx = pxi - p.x, dy = pyi - p.y;
-    knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
-  }
-  return true;
+__device__ __forceinline__ void knn_consider(double (&kr)[K], int (&kj)[K], double pxi, double pyi, double2 p,
+                                             int j) {
+  const double dx = pxi - p.x, dy = pyi - p.y;
+  knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
 }
 
-// ---------------------------------------------------------------------------------
-// Flocking-v0 observation (flocking.py:20-25): the K nearest agents by r2 (self
-// excluded by its infinite r2). One thread per agent. When the step left this
-// state's adjacency behind (adj_bits) and the agent has at least K neighbours, its K
-// nearest are all neighbours (every non-neighbour is farther: r2 >= comm_radius^2 >
-// any neighbour's), so only its ~deg set bits are ranked. Every other agent (few: the
-// swarm's sparse rim) is ranked by its whole wave: lanes scan columns lane, lane+64,
-// ... into lane-local K-lists, and K rounds of a wave-wide (r2, j) minimum merge them.
+struct KnnGrid {
+  double x0, y0, invh, bound_h, err;  // origin, 1/h, h, cell-assignment error (distance)
+  int nx, ny;
+};
+
+__device__ __forceinline__ int knn_cell_x(const KnnGrid& G, double x) {
+  return min(G.nx - 1, max(0, static_cast<int>((x - G.x0) * G.invh)));
+}
+__device__ __forceinline__ int knn_cell_y(const KnnGrid& G, double y) {
+  return min(G.ny - 1, max(0, static_cast<int>((y - G.y0) * G.invh)));
+}
+
 template <int K, bool LDS>
 __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -909,25 +907,35 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / bpe;
   const int i = (L - b * bpe) * kThreads + threadIdx.x;
-  const int lane = threadIdx.x & 63;
+  const int tid = threadIdx.x;
   const bool vi = i < N;
   const double* xb = a.x + (size_t)b * N * 4;
+  const size_t g = (size_t)b * N + i;
+  // rim mode: the fused step ranked every row but those it marked with idx = -1; a
+  // workgroup without such rows leaves before staging anything
+  const bool rim_done = a.rim && (!vi || a.idx[g * K] >= 0);
+  if (a.rim && __syncthreads_count(!rim_done) == 0) return;
   // positions: the whole env staged in LDS (N <= kKnnLdsMax), else read from L2
   const double2* gpos = reinterpret_cast<const double2*>(xb);
   double2* lpos = reinterpret_cast<double2*>(smem);
-  float2* lpf = reinterpret_cast<float2*>(lpos + N);  // float32 copies (bounded scan)
-  __shared__ float kred[4];
-  float Pf = 0.f;  // max |coordinate| of the env's float32 positions (LDS only)
+  int* cell_end = reinterpret_cast<int*>(lpos + N);                          // kKnnGridCells + 1
+  unsigned short* sorted = reinterpret_cast<unsigned short*>(cell_end + kKnnGridCells + 1);  // N
+  __shared__ double kred[4][4];
+  __shared__ KnnGrid grid;
+  __shared__ int grid_ok;
+  double bx[4] = {-__builtin_inf(), -__builtin_inf(), -__builtin_inf(), -__builtin_inf()};
+  bool finite = true;
   if (LDS) {
-    float pm = 0.f;
-    for (int t = threadIdx.x; t < N; t += kThreads) {
+    for (int t = tid; t < N; t += kThreads) {
       const double2 p = gpos[2 * (size_t)t];
       lpos[t] = p;
-      const float2 q = make_float2(static_cast<float>(p.x), static_cast<float>(p.y));
-      lpf[t] = q;
-      pm = fmaxf(pm, fmaxf(fabsf(q.x), fabsf(q.y)));
+      finite &= __builtin_isfinite(p.x) && __builtin_isfinite(p.y);
+      bx[0] = fmax(bx[0], -p.x);  // -min x
+      bx[1] = fmax(bx[1], -p.y);
+      bx[2] = fmax(bx[2], p.x);
+      bx[3] = fmax(bx[3], p.y);
     }
-    Pf = block_max(pm, kred);  // also publishes the staged positions
+    finite = __syncthreads_and(finite);  // also publishes the staged positions
   }
   auto pos = [&](int j) -> double2 { return LDS ? lpos[j] : gpos[2 * (size_t)j]; };
   double pxi = 0, pyi = 0;
@@ -942,8 +950,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
     kr[m] = __builtin_inf();
     kj[m] = INT_MAX;
   }
-  const size_t g = (size_t)b * N + i;
-  const bool fast = vi && a.adj_bits && a.degree[g] >= K && !GF_ABLATE(a, 0x8000);
+  const bool fast = vi && !a.rim && a.adj_bits && a.degree[g] >= K && !GF_ABLATE(a, 0x8000);
   if (fast) {  // rank the neighbours only
     const int Wn = (N + 63) >> 6;
     const uint64_t* bits = a.adj_bits + g * Wn;
@@ -969,78 +976,125 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
       for (int m = 1; m < K; ++m) kj[m] = kj[0];
     }
   }
-  // Agents the neighbour ranking cannot serve: when a workgroup holds only a few, its
-  // waves rank each of them together (lanes scan columns lane, lane+64, ... into
-  // lane-local lists, then K rounds of a wave-wide (r2, j) minimum merge them); when it
-  // holds many (a dispersed swarm), every thread scans its own row, which keeps the
-  // lanes busy on distinct rows.
-  const int nslow = __syncthreads_count(vi && !fast);
-  if (nslow > kKnnFewSlow) {
-    auto full_scan = [&]() {
-      for (int j = 0; j < N; ++j) {
-        const double2 p = pos(j);
-        const double dx = pxi - p.x, dy = pyi - p.y;
-        knn_insert<K>(kr, kj, (j == i) ? __builtin_inf() : dx * dx + dy * dy, j);
+  const bool need = vi && !fast && !rim_done;  // ranked through the grid (or a full scan)
+  const int nslow = __syncthreads_count(need);
+  if (nslow > 0) {
+    bool use_grid = false;
+    if (LDS && finite) {
+      // bounding box (workgroup max of -xmin, -ymin, xmax, ymax)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        for (int o = 32; o >= 1; o >>= 1) bx[q] = fmax(bx[q], __shfl_xor(bx[q], o));
+      if ((tid & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) kred[tid >> 6][q] = bx[q];
+      __syncthreads();
+      if (tid == 0) {
+        double e[4];
+        for (int q = 0; q < 4; ++q) e[q] = fmax(fmax(kred[0][q], kred[1][q]), fmax(kred[2][q], kred[3][q]));
+        const double x0 = -e[0], y0 = -e[1], ex = e[2] - x0, ey = e[3] - y0;
+        const double P = fmax(fmax(fabs(x0), fabs(y0)), fmax(fabs(e[2]), fabs(e[3])));
+        // ~2 agents per cell over the bounding box, at most kKnnGridCells cells
+        const double nt = fmax(1.0, fmin(static_cast<double>(kKnnGridCells) / 3.0, 0.5 * N));
+        double h = fmax(sqrt(ex * ey / nt), fmax(ex, ey) / nt);
+        if (!(h > 0)) h = 1.0;
+        int nx = 0, ny = 0;
+        for (int it = 0; it < 64; ++it, h *= 1.25) {
+          nx = static_cast<int>(ex / h) + 1;
+          ny = static_cast<int>(ey / h) + 1;
+          if ((long long)nx * ny <= kKnnGridCells) break;
+        }
+        // cell assignment error as a distance: (x - x0) and its product with 1/h are
+        // rounded; 2^-40 (P + ex + ey) covers both agents' errors many times over
+        const double err = ldexp(P + ex + ey, -40);
+        grid = KnnGrid{x0, y0, 1.0 / h, h, err, nx, ny};
+        grid_ok = (long long)nx * ny <= kKnnGridCells && err < 1e-3 * h && P < 1e15;
       }
-    };
-    if (LDS) {
-      if (vi && !fast && !knn_bounded_scan<K>(lpos, lpf, N, i, __builtin_amdgcn_readfirstlane(i - lane), pxi, pyi, Pf, kr, kj)) full_scan();
-    } else if (vi && !fast) {
-      full_scan();
+      __syncthreads();
+      use_grid = grid_ok;
     }
-  } else {
-    uint64_t todo = __ballot(vi && !fast);
-    while (todo) {  // wave-cooperative full scan, one row at a time
-      const int l = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const int row = __shfl(i, l);
-      const double px = __shfl(pxi, l), py = __shfl(pyi, l);
-      double lr[K];
-      int lj[K];
-#pragma unroll
-      for (int m = 0; m < K; ++m) {
-        lr[m] = __builtin_inf();
-        lj[m] = INT_MAX;
+    if (use_grid) {
+      const KnnGrid G = grid;
+      const int ncell = G.nx * G.ny;
+      // counting sort of the agents by cell: cell_end[c] = inclusive prefix count, then
+      // each agent takes slot --cell_end[c], which leaves cell_end[c] = start of cell c
+      for (int c = tid; c <= ncell; c += kThreads) cell_end[c] = 0;
+      __syncthreads();
+      for (int t = tid; t < N; t += kThreads) {
+        const double2 p = lpos[t];
+        atomicAdd(&cell_end[knn_cell_y(G, p.y) * G.nx + knn_cell_x(G, p.x)], 1);
       }
-      for (int j = lane; j < N; j += 64) {
-        const double2 p = pos(j);
-        const double dx = px - p.x, dy = py - p.y;
-        knn_insert<K>(lr, lj, (j == row) ? __builtin_inf() : dx * dx + dy * dy, j);
+      __syncthreads();
+      {  // inclusive scan over ncell counts: a contiguous chunk per thread
+        const int per = (ncell + kThreads - 1) / kThreads;
+        const int c0 = min(ncell, tid * per), c1 = min(ncell, c0 + per);
+        int s = 0;
+        for (int c = c0; c < c1; ++c) s += cell_end[c];
+        int incl = s;  // workgroup inclusive scan of the chunk sums
+        const int lane = tid & 63;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_up(incl, o);
+          if (lane >= o) incl += v;
+        }
+        __shared__ int wsum[4];
+        if (lane == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        int base = incl - s;
+        for (int w = 0; w < (tid >> 6); ++w) base += wsum[w];
+        for (int c = c0; c < c1; ++c) {
+          base += cell_end[c];
+          cell_end[c] = base;
+        }
       }
-#pragma unroll
-      for (int m = 0; m < K; ++m) {
-        double br = lr[0];
-        int bj = lj[0];
-        for (int o = 32; o > 0; o >>= 1) {
-          const double orr = __shfl_xor(br, o);
-          const int oj = __shfl_xor(bj, o);
-          if (orr < br || (orr == br && oj < bj)) {
-            br = orr;
-            bj = oj;
+      if (tid == 0) cell_end[ncell] = N;
+      __syncthreads();
+      for (int t = tid; t < N; t += kThreads) {
+        const double2 p = lpos[t];
+        const int slot = atomicSub(&cell_end[knn_cell_y(G, p.y) * G.nx + knn_cell_x(G, p.x)], 1) - 1;
+        sorted[slot] = static_cast<unsigned short>(t);
+      }
+      __syncthreads();
+      if (need) {
+        const int cx = knn_cell_x(G, pxi), cy = knn_cell_y(G, pyi);
+        const int dmax = max(max(cx, G.nx - 1 - cx), max(cy, G.ny - 1 - cy));
+        auto range = [&](int y, int xa, int xb2) {  // cells [xa, xb2] of grid row y
+          xa = max(xa, 0);
+          xb2 = min(xb2, G.nx - 1);
+          if (y < 0 || y >= G.ny || xa > xb2) return;
+          const int s0 = cell_end[y * G.nx + xa], s1 = cell_end[y * G.nx + xb2 + 1];
+          for (int s = s0; s < s1; ++s) {
+            const int j = sorted[s];
+            if (j != i) knn_consider<K>(kr, kj, pxi, pyi, lpos[j], j);
           }
-        }
-        if (lane == l) {
-          kr[m] = br;
-          kj[m] = bj;
-        }
-        if (lj[0] == bj) {  // the winner's lane pops its head (columns are disjoint per lane)
-#pragma unroll
-          for (int q = 0; q + 1 < K; ++q) {
-            lr[q] = lr[q + 1];
-            lj[q] = lj[q + 1];
+        };
+        for (int d = 0; d <= dmax; ++d) {
+          range(cy - d, cx - d, cx + d);
+          if (d > 0) {
+            range(cy + d, cx - d, cx + d);
+            for (int y = cy - d + 1; y <= cy + d - 1; ++y) {
+              range(y, cx - d, cx - d);
+              range(y, cx + d, cx + d);
+            }
           }
-          lr[K - 1] = __builtin_inf();
-          lj[K - 1] = INT_MAX;
+          // every agent not visited yet is >= d*h - 2 err away; r2 of such a pair, as
+          // computed, is at least that squared (1 - 2^-40)
+          const double lim = static_cast<double>(d) * G.bound_h - 2.0 * G.err;
+          if (lim > 0 && kr[K - 1] < lim * lim * (1.0 - 0x1p-40)) break;
         }
       }
+    } else if (need) {
+      for (int j = 0; j < N; ++j)
+        if (j != i) knn_consider<K>(kr, kj, pxi, pyi, pos(j), j);
     }
+    // self last (its r2 is inf in the reference), for k >= the agents with finite r2
+    if (need) knn_insert<K>(kr, kj, __builtin_inf(), i);
   }
-  if (!vi) return;
+  if (!vi || rim_done) return;
   const double2* xi = reinterpret_cast<const double2*>(xb) + 2 * (size_t)i;
   const double2 pi = xi[0], vv = xi[1];
 #pragma unroll
   for (int m = 0; m < K; ++m) {
-    const int j = kj[m];
+    const int j = kj[m] < N ? kj[m] : i;  // unfilled slots (non-finite r2 only): self
     a.idx[g * K + m] = j;
     const double2* xj = reinterpret_cast<const double2*>(xb) + 2 * (size_t)j;
     const double2 pj = xj[0], vj = xj[1];
@@ -1142,23 +1196,36 @@ hipError_t max_lds_once(const void* f, std::atomic<uint64_t>& done, int bytes) {
   return e;
 }
 
-template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0>
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL);
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
   // would allow
   if (!CTRL && !VAR && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
   static std::atomic<uint64_t> attr{0};
-  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF>),
-                                        attr, 160 * 1024); e != hipSuccess)
+  if (const hipError_t e = max_lds_once(
+          reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF, KN>), attr, 160 * 1024);
+      e != hipSuccess)
     return e;
   const int grid = a.B * a.bpe;
-  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR, PF>), dim3(grid), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR, PF, KN>), dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
+}
+
+bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch) {
+  return K == kStepFusedK && !variant && !prefetch && kThreads / R >= K && N <= 65536;
 }
 
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
+  if constexpr (DYN) {
+    if (a.knn_idx) {
+      if (a.variant || (a.prefetch && a.T <= 2 * kThreads && a.N > a.T) || kThreads / a.R < kStepFusedK)
+        return hipErrorInvalidValue;
+      return launch_step_tiled<DYN, UF64, CTRL, false, 0, kStepFusedK>(a, s);
+    }
+  }
+  if (a.knn_idx) return hipErrorInvalidValue;
   if (a.variant) return launch_step_tiled<DYN, UF64, CTRL, true>(a, s);
   if (a.prefetch && a.T <= 2 * kThreads && a.N > a.T) return launch_step_tiled<DYN, UF64, CTRL, false, 1>(a, s);
   return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
@@ -1175,14 +1242,14 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
   const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
   const bool lds = a.N <= kKnnLdsMax;
-  const size_t bytes = lds ? (size_t)a.N * 24 : 0;  // the env's positions, float64 + float32
+  const size_t bytes = lds ? knn_lds_bytes(a.N) : 0;
   switch (a.K) {
 #define GF_KNN_CASE(k)                                                                                  \
   case k:                                                                                               \
     if (lds) {                                                                                          \
       static std::atomic<uint64_t> attr_##k{0};                                                         \
       if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_knn_kernel<k, true>), \
-                                            attr_##k, kKnnLdsMax * 24);                                 \
+                                            attr_##k, (int)knn_lds_bytes(kKnnLdsMax));                  \
           e != hipSuccess)                                                                              \
         return e;                                                                                       \
       hipLaunchKernelGGL((flock_knn_kernel<k, true>), dim3(grid), dim3(kThreads), bytes, s, a);        \

@@ -461,25 +461,47 @@ def _knn_cases():
     x = cases["dispersed"].copy()
     x[:, :2] += 3.0e6  # large coordinates: the float32 margin is wide (candidate overflow path)
     cases["offset"] = x
+    # dense states (k = 7: the step's fused selection ranks the rows it can)
+    x = np.zeros((n, 4))
+    x[:, :2] = g[rs.permutation(n)] * 0.125  # ~20 neighbours each, exact r2 ties: equal keys
+    cases["dense_lattice"] = x
+    x = cases["dense_lattice"].copy()
+    x[:, :2] += rs.uniform(-1, 1, size=(n, 2)) * 1e-3  # ties broken: fused ranking, a few rim rows
+    x[:, 2:] = rs.uniform(-1, 1, size=(n, 2))
+    cases["dense_jitter"] = x
+    x = np.zeros((n, 4))
+    x[:, :2] = rs.uniform(-2.5, 2.5, size=(n, 2))
+    x[:, 2:] = rs.uniform(-1, 1, size=(n, 2))
+    x[100:104, :2] = x[7, :2]  # coincident agents inside a dense swarm (r2 = 0 ties)
+    x[500, :2] = x[501, :2] + np.array([3e-9, 0.0])  # keys differ by less than the q step
+    cases["dense_random"] = x
+    x = cases["dense_random"].copy()
+    x[:40, :2] += 30.0  # a detached, sparse group: rows below k neighbours in a dense env
+    x[:40, :2] += rs.uniform(-5, 5, size=(40, 2))
+    cases["dense_with_rim"] = x
     return cases
 
 
 @pytest.mark.parametrize("k", [1, 7, 16])
-@pytest.mark.parametrize("case", ["dispersed", "lattice", "lattice_jitter", "coincident_ragged", "offset"])
+@pytest.mark.parametrize("case", ["dispersed", "lattice", "lattice_jitter", "coincident_ragged", "offset",
+                                  "dense_lattice", "dense_jitter", "dense_random", "dense_with_rim"])
 def test_knn_full_scan_rows_vs_oracle(case, k):
-    """Flocking-v0 observation for states where (nearly) every agent has fewer than k
-    neighbours, so each row is a full scan (bounded two-pass scan: float32 group-minimum
-    bound, candidate list, exact float64 ranking): indices bit-exact vs the oracle's
-    stable argsort, ties to the lower index."""
+    """Flocking-v0 observation, indices bit-exact vs the oracle's stable argsort (ties to
+    the lower index) and observations exact. Sparse states: (nearly) every agent has
+    fewer than k neighbours, so each row is a full scan (bounded two-pass scan: float32
+    group-minimum bound, candidate list, exact float64 ranking). Dense states (k = 7):
+    the step's fused selection ranks rows whose k + 1 nearest keys are distinct, and
+    the rim kNN the rows with exact ties, near-equal keys or too few neighbours."""
     x0 = _knn_cases()[case]
     n = x0.shape[0]
     xb = np.stack([x0, x0[::-1].copy()])  # second env: reversed agent order (other tie winners)
     h = nat.FlockHandle(n, 2, n_neighbors=k)
     h.set_state(xb)
-    h.step(np.zeros((2, n, 2), np.float32), nat.FE_WITH_KNN)
+    u0 = np.zeros((2, n, 2), np.float32)
+    h.step(u0, nat.FE_WITH_KNN)
     for b in range(2):
         x1 = h.get_state(b)
-        np.testing.assert_array_equal(x1, xb[b])
+        np.testing.assert_array_equal(x1, orc.integrate(xb[b], u0[b]))
         idx, obs = h.knn(b)
         ridx, robs = orc.knn_observation(x1, k)
         np.testing.assert_array_equal(idx, ridx)
