@@ -78,6 +78,10 @@ struct fe_handle {
   // the previous state, and the kread events that guard x[i] guard them too
   int32_t* knn_idx[2] = {nullptr, nullptr};
   float* knn_obs[2] = {nullptr, nullptr};
+  // each ranked row's k-th nearest r2 (0: unknown), by state buffer: a fused step reads
+  // the one of two states back (complete: the step waits for that state's kNN) to pick
+  // the rows it ranks beyond their neighbours, and writes its own
+  float* knn_r2[2] = {nullptr, nullptr};
   double* vel_diffs = nullptr;
   double* min_dists = nullptr;
   int32_t* degree = nullptr;
@@ -207,7 +211,7 @@ void release(fe_handle* h) {
   if (h->kstream) hipStreamSynchronize(h->kstream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
+                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
                   h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -288,9 +292,10 @@ int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a, int xw) {
     while ((1 << jb) < N) ++jb;
     a.knn_idx = h->knn_idx[xw];
     a.knn_obs = h->knn_obs[xw];
+    a.knn_r2 = h->knn_r2[xw];
     a.knn_jbits = jb;
     a.knn_qmax = (1u << (32 - jb)) - 2u;  // below the all-ones empty-slot key
-    a.knn_scale = std::ldexp(1.0, 32 - jb) / (h->cfg.comm_radius * h->cfg.comm_radius);
+    a.knn_qscale = std::ldexp(1.0, 32 - jb);
   }
   if (int rc = wait_knn_readers(h, xw, bw)) return rc;
   if (bw >= 0) h->bits_cur = bw;  // the launch that follows fills it
@@ -372,6 +377,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
       const size_t K = h->cfg.n_neighbors;
       a1.knn_idx = a.knn_idx + e0 * K;
       a1.knn_obs = a.knn_obs + e0 * 4 * K;
+      a1.knn_r2 = a.knn_r2 + e0;
     }
     hipError_t e = gf::launch_step(a, dyn, uf64, ctrl, h->stream);
     if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
@@ -423,6 +429,7 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.idx = h->knn_idx[h->cur];
   k.obs = h->knn_obs[h->cur];
   k.rim = mode == 2;
+  k.r2k = h->knn_r2[h->cur];
   k.N = h->cfg.n_agents;
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
@@ -436,6 +443,15 @@ int launch_knn_cur(fe_handle* h, int mode) {
   h->k_pending = true;
   h->has_knn = true;
   return GF_OK;
+}
+
+// The kNN radius history describes states the handle no longer holds once the state is
+// replaced: forget it (the fused steps then rank neighbours only until it is rebuilt).
+hipError_t clear_knn_history(fe_handle* h) {
+  for (float* p : h->knn_r2)
+    if (p)
+      if (hipError_t e = hipMemsetAsync(p, 0, h->BN * sizeof(float), h->stream); e != hipSuccess) return e;
+  return hipSuccess;
 }
 
 int d2h(fe_handle* h, void* dst, const void* src, size_t bytes) {
@@ -499,7 +515,8 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (rc = dalloc(&h->knn_idx[0], h->BN * cfg->n_neighbors)) ||
       (rc = dalloc(&h->knn_idx[1], h->BN * cfg->n_neighbors)) ||
       (rc = dalloc(&h->knn_obs[0], h->BN * 4 * cfg->n_neighbors)) ||
-      (rc = dalloc(&h->knn_obs[1], h->BN * 4 * cfg->n_neighbors))) {
+      (rc = dalloc(&h->knn_obs[1], h->BN * 4 * cfg->n_neighbors)) ||
+      (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_r2[0], h->BN)) || (rc = dalloc(&h->knn_r2[1], h->BN))))) {
     release(h);
     return rc;
   }
@@ -518,6 +535,7 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     return fail_hip("event create", e);
   }
   if ((e = hipMemsetAsync(h->reward_ring, 0, sizeof(double) * kRewardSlots * B, h->stream)) != hipSuccess ||
+      (e = clear_knn_history(h)) != hipSuccess ||
       (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
     release(h);
     return fail_hip("init", e);
@@ -541,6 +559,7 @@ int fe_set_state(fe_handle* h, const double* x) {
   if (!h || !x) return fail(GF_EINVAL, "null argument");
   if (int rc = use_dev(h)) return rc;
   GF_HIP(hipMemcpyAsync(h->x[h->cur], x, h->BN * 4 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  GF_HIP(clear_knn_history(h));
   GF_HIP(hipStreamSynchronize(h->stream));
   h->has_state = true;
   h->has_ctrl = h->has_obs = h->has_knn = false;
@@ -580,6 +599,7 @@ int fe_set_state_env(fe_handle* h, int env, const double* x) {
   if (int rc = use_dev(h)) return rc;
   const size_t n = (size_t)h->cfg.n_agents * 4;
   GF_HIP(hipMemcpyAsync(h->x[h->cur] + env * n, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  GF_HIP(clear_knn_history(h));
   GF_HIP(hipStreamSynchronize(h->stream));
   h->has_state = true;
   h->has_ctrl = h->has_obs = h->has_knn = false;

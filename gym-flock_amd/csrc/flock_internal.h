@@ -20,6 +20,8 @@ constexpr int kTileDefault = 512;   // default tile (measured best, see step_til
 constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
+constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
+                                    // scanned wave-cooperatively from L2, more through the grid
 // kNN LDS: positions (16 B per agent), the grid's cell offsets, agent indices by cell
 constexpr size_t knn_lds_bytes(int N) {
   return (size_t)N * 16 + (size_t)(kKnnGridCells + 1) * 4 + (((size_t)N * 2 + 15) / 16) * 16;
@@ -66,13 +68,15 @@ struct StepArgs {
   int32_t* degree_out;    // (B,N) degrees or nullptr
   // Flocking-v0 k-nearest selection fused into the feature pass (kStepFusedK neighbours):
   // rows the step can rank exactly get idx + obs; the others get idx[row*K] = -1 and
-  // are finished by flock_knn_kernel in rim mode. Key of a neighbour pair:
-  // (min(floor(r2 * knn_scale), knn_qmax) << knn_jbits) | j (see the kernel).
+  // are finished by flock_knn_kernel in rim mode. Key of a ranked pair:
+  // (min(floor(r2 * knn_qscale / Tr), knn_qmax) << knn_jbits) | j (see the kernel).
   int32_t* knn_idx;       // (B,N,K) or nullptr: no fused selection
   float* knn_obs;         // (B,N,4K)
-  double knn_scale;
-  unsigned knn_qmax;
-  int knn_jbits;
+  float* knn_r2;          // (B,N) k-th nearest r2 of the state two steps back (0: none),
+                          // replaced by this state's for the rows ranked here
+  double knn_qscale;      // 2^qbits
+  unsigned knn_qmax;      // 2^qbits - 2
+  int knn_jbits;          // bits of the agent index (qbits = 32 - jbits)
 };
 
 constexpr int kStepFusedK = 7;  // Flocking-v0's n_neighbors (flocking.py:9)
@@ -85,7 +89,9 @@ struct KnnArgs {
   const uint64_t* adj_bits;  // (B,N,Wn) adjacency of x from the step, or nullptr
   const int32_t* degree;     // (B,N) with adj_bits
   int rim;                   // only rows the fused step left unranked (idx[row*K] < 0)
-  int diag;                  // ablation: 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path
+  float* r2k;                // (B,N) or nullptr: each ranked row's k-th nearest r2
+  int diag;                  // ablation: 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path,
+                             // 0x1000 grid built but no search, 0x2000 no grid / scan, 0x0800 no outputs
 };
 
 struct StatsArgs {
@@ -100,7 +106,7 @@ struct StatsArgs {
 // Launch-geometry helpers shared by host and tests.
 int step_rows_per_block(int N);
 int step_tile(int N);
-size_t step_lds_bytes(int N, int R, int T, bool ctrl);
+size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn);
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
 // Whether a step of this geometry can carry the fused k-nearest selection (K ==

@@ -284,6 +284,25 @@ __device__ __forceinline__ float uniform_f(float v) {
 // the compiler applies the constant-bus and lane-select hazard rules itself.
 extern "C" __device__ int gf_writelane_i32(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
+// Minimum over aligned groups of S lanes (S a power of two): DPP lane swaps inside rows
+// of 16 (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), shuffles beyond.
+__device__ __forceinline__ unsigned dpp_u32(unsigned v, int ctrl) {
+  switch (ctrl) {  // the control word must be a compile-time constant
+    case 0xB1: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+    case 0x4E: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
+    case 0x141: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x141, 0xF, 0xF, false));
+    default: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x140, 0xF, 0xF, false));
+  }
+}
+__device__ __forceinline__ unsigned group_min_u32(unsigned w, int S) {
+  if (S > 1) w = min(w, dpp_u32(w, 0xB1));
+  if (S > 2) w = min(w, dpp_u32(w, 0x4E));
+  if (S > 4) w = min(w, dpp_u32(w, 0x141));
+  if (S > 8) w = min(w, dpp_u32(w, 0x140));
+  for (int o = 16; o < S; o <<= 1) w = min(w, static_cast<unsigned>(__shfl_xor(static_cast<int>(w), o)));
+  return w;
+}
+
 // Lane l of (w0, w1) takes the wave-uniform 64-bit mask m.
 __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m, int l) {
   w0 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m), l, static_cast<int>(w0)));
@@ -470,10 +489,10 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 #define GF_STEP_WAVES_CTRL 6
 #endif
 #ifndef GF_STEP_WAVES_KNN
-#define GF_STEP_WAVES_KNN 6
+#define GF_STEP_WAVES_KNN 5
 #endif
 #ifndef GF_STEP_WAVES_KNN_CTRL
-#define GF_STEP_WAVES_KNN_CTRL 5
+#define GF_STEP_WAVES_KNN_CTRL 4
 #endif
 // Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
 // wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
@@ -510,9 +529,11 @@ void flock_step_kernel(StepArgs a) {
   St* rows = tile + T;                                         // this block's rows, R
   uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
   uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
-  double* red = reinterpret_cast<double*>(nearb + (CTRL ? (size_t)R * Wt : 0));
+  uint64_t* candb = nearb + (CTRL ? (size_t)R * Wt : 0);       // (predicted rows) x Wt kNN candidates
+  double* red = reinterpret_cast<double*>(candb + (KN ? (size_t)R * Wt : 0));
   float* redf = reinterpret_cast<float*>(red + 4);
   float* inv = reinterpret_cast<float*>(red + 8);
+  [[maybe_unused]] float* rthr = inv + R;                      // R kNN candidate radii^2 (0: none)
 
   // the plain step deals the reward blocks out first (195 vs 200 us at config 2; with
   // the controller it measured 1 us slower); diag 8192 forces the plain remap (A/B)
@@ -557,14 +578,21 @@ void flock_step_kernel(StepArgs a) {
   double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
   double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
+  // kNN rows predicted to lack k neighbours (their k-th nearest two states back was
+  // at >= 0.8 comm_radius): predm (wave-uniform) marks them, rthr[r] holds row r's
+  // candidate radius^2 thr
+  [[maybe_unused]] uint64_t predm = 0;
 
   const int i_row = i0 + fr;  // global row of this thread's feature slice
-  // Fused k-nearest selection (KN > 0). A neighbour's key is
-  //   (q << jbits) | j,  q = min(floor(r2 * knn_scale), knn_qmax),
+  // Fused k-nearest selection (KN > 0). Every pair the feature pass visits is ranked:
+  // the neighbours and, for a predicted row, its candidates: agents whose float32 d2
+  // is below a bound covering every agent with r2 < thr (2.25 x the row's k-th nearest
+  // r2 two states back, knn_r2). The ranked set thus holds every agent with
+  // r2 < Tr = max(thr, comm_radius^2). A pair's key is
+  //   (q << jbits) | j,  q = min(floor(r2 * 2^qbits / Tr), 2^qbits - 2),
   // a 32-bit integer whose order is (q, j): q never decreases as r2 grows, so keys of
   // different q are in true (r2, j) order. Each thread keeps its KN smallest keys sorted
-  // (a min/max exchange chain, 2 VALU per entry, no branches); columns arrive in
-  // ascending j per thread, but the order does not matter here.
+  // (a min/max exchange chain, 2 VALU per entry, no branches).
   [[maybe_unused]] unsigned kk[KN > 0 ? KN : 1];
   if constexpr (KN > 0) {
 #pragma unroll
@@ -573,22 +601,21 @@ void flock_step_kernel(StepArgs a) {
   // one neighbour pair (row fr = me, tile column c): features and controller gradient.
   // The row's state is read from LDS per feature pass, so it holds no registers
   // through pass 1.
-  auto pair_terms = [&](const St& me, int j0, int c, bool isadj, bool isnear) {
+  auto pair_terms = [&](const St& me, int j0, int c, bool isadj, bool isnear, double ksc) {
     const St o = tile[c];
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
     if constexpr (KN > 0) {
-      if (isadj) {
-        const double qd = r2 * a.knn_scale;  // r2 < comm_radius^2 here: 0 <= qd <~ 2^qbits
-        const unsigned q = qd < static_cast<double>(a.knn_qmax) ? static_cast<unsigned>(qd) : a.knn_qmax;
-        unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
+      const double qd = r2 * ksc;
+      const unsigned q = qd < static_cast<double>(a.knn_qmax) ? static_cast<unsigned>(qd) : a.knn_qmax;
+      unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
 #pragma unroll
-        for (int m = 0; m < KN; ++m) {
-          const unsigned lo = min(kk[m], v);
-          v = max(kk[m], v);
-          kk[m] = lo;
-        }
+      for (int m = 0; m < KN; ++m) {
+        const unsigned lo = min(kk[m], v);
+        v = max(kk[m], v);
+        kk[m] = lo;
       }
+      if (!isadj && !(CTRL && isnear)) return;  // a candidate only: no features
     }
     // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
     // reference's two divisions; far inside the float32 outputs' tolerance)
@@ -619,16 +646,25 @@ void flock_step_kernel(StepArgs a) {
   auto feature_pass = [&](int j0, int nch) {
     if (!frow || GF_ABLATE(a, 2)) return;
     const St me = rows[fr];
+    // kNN: this row's candidate words (predicted rows) and key scale 2^qbits / Tr
+    [[maybe_unused]] const uint64_t* crow = nullptr;
+    [[maybe_unused]] double ksc = 0.0;
+    if constexpr (KN > 0) {
+      const bool pr = (predm >> fr) & 1ull;
+      crow = pr ? candb + (size_t)__popcll(predm & ((1ull << fr) - 1ull)) * Wt : nullptr;
+      ksc = a.knn_qscale / (pr ? fmax(static_cast<double>(rthr[fr]), a.cr2) : a.cr2);
+    }
     const int wpt = (nch + S - 1) / S;
     const int wb = fs * wpt, we = min(nch, wb + wpt);
     for (int w = wb; w < we; ++w) {
       const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
       const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
-      uint64_t m = am | nm;
+      const uint64_t cm = (KN && crow) ? crow[w] : 0ull;
+      uint64_t m = am | nm | cm;
       while (m) {
         const int k = __builtin_ctzll(m);
         m &= m - 1;
-        pair_terms(me, j0, (w << 6) + k, (am >> k) & 1ull, CTRL && ((nm >> k) & 1ull));
+        pair_terms(me, j0, (w << 6) + k, (am >> k) & 1ull, CTRL && ((nm >> k) & 1ull), ksc);
       }
     }
   };
@@ -662,6 +698,12 @@ void flock_step_kernel(StepArgs a) {
         ry32 = static_cast<float>(ri.py);
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
+      if constexpr (KN > 0) {
+        const float h = (lane < nrows && a.knn_r2) ? a.knn_r2[env0 + i0 + lane] : 0.f;
+        const bool pr = h >= static_cast<float>(0.64 * a.cr2) && h < 1.0e30f;
+        predm = __ballot(pr);
+        if (wid == 0 && lane < nrows) rthr[lane] = pr ? 2.25f * h : 0.f;
+      }
     }
     const float Pt = block_max(pt, redf);  // also the barrier that publishes the tile
     if (ti < 2) GF_STAMP(2 + 3 * ti);
@@ -755,6 +797,41 @@ void flock_step_kernel(StepArgs a) {
           if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
         }
       }
+      if constexpr (KN > 0) {
+        // the predicted rows' candidate words: lane p collects predicted row p's
+        if (predm) {
+          // row lane's candidate test: float32 d2 < tcr covers every agent with r2 < thr
+          // (float32 error of d2 at |d| <= sqrt(thr): 2^-23 |d| (Pi + Pj + |d|) +
+          // 2^-22 r2, taken x8); none at huge coordinates (those rows go to the rim kNN)
+          float tcr = -1.f;
+          const float th = lane < nrows ? rthr[lane] : 0.f;
+          if (th > 0.f && pu < 1.0e5f) {
+            const double t = th;
+            const double dc = ldexp((static_cast<double>(pu) + 4.0) * (sqrt(t) + 1.0) + t, -20);
+            tcr = static_cast<float>(t + dc);
+            if (static_cast<double>(tcr) < t + dc) tcr = nextafterf(tcr, __builtin_inff());
+          }
+          unsigned ca0 = 0, ca1 = 0, cb0 = 0, cb1 = 0;
+          int p = 0, rp = 0;
+          for (uint64_t pm = predm; pm; pm &= pm - 1, ++p) {
+            const int r = __builtin_ctzll(pm);
+            if (lane == p) rp = r;
+            const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r), tc = readlane_f(tcr, r);
+            const f2v dx = xi - qx, dy = yi - qy;
+            const f2v d2 = dx * dx + dy * dy;
+            put_lane(ca0, ca1, __ballot(d2.x < tc), p);
+            put_lane(cb0, cb1, __ballot(d2.y < tc), p);
+          }
+          if (lane < p) {
+            const int dl = i0 + rp - (j0 + (ca << 6));
+            const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
+            const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
+            uint64_t* crow = candb + (size_t)lane * Wt + ca;
+            crow[0] = ((static_cast<uint64_t>(ca1) << 32) | ca0) & ka;
+            if (has_b) crow[1] = ((static_cast<uint64_t>(cb1) << 32) | cb0) & kb;
+          }
+        }
+      }
     }
     __syncthreads();
     if (ti < 2) GF_STAMP(3 + 3 * ti);
@@ -805,32 +882,34 @@ void flock_step_kernel(StepArgs a) {
   feature_pass(jl, nchl);
   GF_STAMP(9);
 
+  [[maybe_unused]] RawState<UF64> kraw{};
+  [[maybe_unused]] bool kgo = false;
   if constexpr (KN > 0) {
+   if (!GF_ABLATE(a, 1)) {  // diag 1: no merge / kNN outputs (timing only)
     // Merge the S slices' lists of each row (S consecutive lanes): KN + 1 rounds of an
     // S-lane minimum; the lane whose head won pops it (keys are distinct: j differs).
     // Round m's winner is the row's m-th nearest; lane fs keeps winner fs. The result
     // is the reference's argsort order (ties to the lower index, as the kNN kernel)
-    // when the KN + 1 smallest keys have distinct q: then the top KN are strictly
-    // closer than every other agent and strictly ordered among themselves. A row with
-    // fewer than KN neighbours (its KN nearest include non-neighbours) or equal q among
-    // those keys gets idx = -1 and is ranked exactly by flock_knn_kernel (rim mode).
+    // when (a) the KN-th key has q <= 2^qbits - 4, so its r2 < Tr and every agent left
+    // out of the ranking (r2 >= Tr) is farther, and (b) the KN + 1 smallest keys have
+    // distinct q: then the top KN are strictly closer than every other agent and
+    // strictly ordered among themselves. Any other row (too few agents ranked, equal
+    // q) gets idx = -1 and is ranked exactly by flock_knn_kernel (rim mode).
     const int jb = a.knn_jbits;
     unsigned mine = 0xFFFFFFFFu, prevq = 0xFFFFFFFFu;
     bool slow = false;
 #pragma unroll
     for (int m = 0; m <= KN; ++m) {
       unsigned w = kk[0];
-      for (int o = 1; o < S; o <<= 1) w = min(w, static_cast<unsigned>(__shfl_xor(static_cast<int>(w), o)));
+      w = group_min_u32(w, S);
       const bool pop = kk[0] == w;
 #pragma unroll
       for (int q = 0; q + 1 < KN; ++q) kk[q] = pop ? kk[q + 1] : kk[q];
       kk[KN - 1] = pop ? 0xFFFFFFFFu : kk[KN - 1];
       const bool real = w != 0xFFFFFFFFu;
-      if (m < KN) {
-        mine = (fs == m) ? w : mine;
-        slow |= !real;
-      }
       const unsigned qw = w >> jb;
+      if (m < KN) mine = (fs == m) ? w : mine;
+      if (m == KN - 1) slow |= qw > a.knn_qmax - 2u;
       slow |= real && m > 0 && qw == prevq;
       prevq = qw;
     }
@@ -841,21 +920,35 @@ void flock_step_kernel(StepArgs a) {
       } else if (fs < KN) {
         const int j = static_cast<int>(mine & ((1u << jb) - 1u));
         a.knn_idx[g * KN + fs] = j;
-        const St o = state_from_raw<DYN, UF64>(a, load_raw<DYN, UF64>(a, env0 + j));
-        const St me = rows[fr];
-        float4 ob;
-        ob.x = static_cast<float>(me.px - o.px);
-        ob.y = static_cast<float>(me.py - o.py);
-        ob.z = static_cast<float>(me.vx - o.vx);
-        ob.w = static_cast<float>(me.vy - o.vy);
-        reinterpret_cast<float4*>(a.knn_obs)[g * KN + fs] = ob;
+        // the neighbour's state: its loads are issued here and used after the
+        // epilogue, so their latency runs under the epilogue's sums
+        if (!GF_ABLATE(a, 32)) {  // diag 32: no observation gather (timing only)
+          kraw = load_raw<DYN, UF64>(a, env0 + j);
+          kgo = true;
+        }
       }
     }
+   }
   }
 
   const St me = frow ? rows[fr] : St{0, 0, 0, 0};
   step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
                                       frow && fs == 0, S, tid);
+  if constexpr (KN > 0) {
+    if (kgo) {  // Flocking-v0 observation x_i - x_j of this lane's neighbour (flocking.py:24)
+      const St o = state_from_raw<DYN, UF64>(a, kraw);
+      if (fs == KN - 1 && a.knn_r2) {  // the row's k-th nearest r2: candidate radius two steps on
+        const double dx = me.px - o.px, dy = me.py - o.py;
+        a.knn_r2[env0 + i_row] = static_cast<float>(dx * dx + dy * dy);
+      }
+      float4 ob;
+      ob.x = static_cast<float>(me.px - o.px);
+      ob.y = static_cast<float>(me.py - o.py);
+      ob.z = static_cast<float>(me.vx - o.vx);
+      ob.w = static_cast<float>(me.vy - o.vy);
+      reinterpret_cast<float4*>(a.knn_obs)[(env0 + i_row) * KN + fs] = ob;
+    }
+  }
   GF_STAMP(10);
 #if defined(GF_STAMPS) && GF_STAMPS >= 2
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -899,6 +992,85 @@ __device__ __forceinline__ int knn_cell_y(const KnnGrid& G, double y) {
   return min(G.ny - 1, max(0, static_cast<int>((y - G.y0) * G.invh)));
 }
 
+// Row `i` of lane l, ranked by the whole wave: lanes scan columns lane, lane + 64, ...
+// into lane-local K-lists, then K rounds of a wave-wide (r2, j) minimum merge them into
+// lane l's (kr, kj). pos(j): the agent's position.
+template <int K, class Pos>
+__device__ __forceinline__ void knn_wave_scan(const Pos& pos, int N, int l, int i, double pxi, double pyi,
+                                              double (&kr)[K], int (&kj)[K]) {
+  const int lane = threadIdx.x & 63;
+  const int row = __shfl(i, l);
+  const double px = __shfl(pxi, l), py = __shfl(pyi, l);
+  double lr[K];
+  int lj[K];
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    lr[m] = __builtin_inf();
+    lj[m] = INT_MAX;
+  }
+  constexpr int U = 4;  // positions of U columns in flight per lane
+  for (int j0 = lane; j0 < N; j0 += U * 64) {
+    double2 p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (j0 + u * 64 < N) p[u] = pos(j0 + u * 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * 64;
+      if (j < N && j != row) knn_consider<K>(lr, lj, px, py, p[u], j);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    double br = lr[0];
+    int bj = lj[0];
+    for (int o = 32; o > 0; o >>= 1) {
+      const double orr = __shfl_xor(br, o);
+      const int oj = __shfl_xor(bj, o);
+      if (orr < br || (orr == br && oj < bj)) {
+        br = orr;
+        bj = oj;
+      }
+    }
+    if (lane == l) {
+      kr[m] = br;
+      kj[m] = bj;
+    }
+    if (lj[0] == bj) {  // the winner's lane pops its head (columns are disjoint per lane)
+#pragma unroll
+      for (int q = 0; q + 1 < K; ++q) {
+        lr[q] = lr[q + 1];
+        lj[q] = lj[q + 1];
+      }
+      lr[K - 1] = __builtin_inf();
+      lj[K - 1] = INT_MAX;
+    }
+  }
+}
+
+// One ranked row's outputs: indices, observation x_i - x_j (flocking.py:24) and its k-th
+// nearest r2 (the fused steps' candidate radius).
+template <int K>
+__device__ __forceinline__ void knn_write_row(const KnnArgs& a, const double* xb, size_t g, int i, int N,
+                                              const double (&kr)[K], const int (&kj)[K]) {
+  if (a.r2k) a.r2k[g] = static_cast<float>(kr[K - 1]);
+  const double2* xi = reinterpret_cast<const double2*>(xb) + 2 * (size_t)i;
+  const double2 pi = xi[0], vv = xi[1];
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    const int j = kj[m] < N ? kj[m] : i;  // unfilled slots (non-finite r2 only): self
+    a.idx[g * K + m] = j;
+    const double2* xj = reinterpret_cast<const double2*>(xb) + 2 * (size_t)j;
+    const double2 pj = xj[0], vj = xj[1];
+    float4 o;
+    o.x = static_cast<float>(pi.x - pj.x);
+    o.y = static_cast<float>(pi.y - pj.y);
+    o.z = static_cast<float>(vv.x - vj.x);
+    o.w = static_cast<float>(vv.y - vj.y);
+    reinterpret_cast<float4*>(a.obs + g * 4 * K)[m] = o;
+  }
+}
+
 template <int K, bool LDS>
 __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -913,6 +1085,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   const size_t g = (size_t)b * N + i;
   // rim mode: the fused step ranked every row but those it marked with idx = -1; a
   // workgroup without such rows leaves before staging anything
+  if (GF_ABLATE(a, 0x0400)) return;  // ablation 0x0400: no kNN kernel work (timing only)
   const bool rim_done = a.rim && (!vi || a.idx[g * K] >= 0);
   if (a.rim && __syncthreads_count(!rim_done) == 0) return;
   // positions: the whole env staged in LDS (N <= kKnnLdsMax), else read from L2
@@ -923,21 +1096,6 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   __shared__ double kred[4][4];
   __shared__ KnnGrid grid;
   __shared__ int grid_ok;
-  double bx[4] = {-__builtin_inf(), -__builtin_inf(), -__builtin_inf(), -__builtin_inf()};
-  bool finite = true;
-  if (LDS) {
-    for (int t = tid; t < N; t += kThreads) {
-      const double2 p = gpos[2 * (size_t)t];
-      lpos[t] = p;
-      finite &= __builtin_isfinite(p.x) && __builtin_isfinite(p.y);
-      bx[0] = fmax(bx[0], -p.x);  // -min x
-      bx[1] = fmax(bx[1], -p.y);
-      bx[2] = fmax(bx[2], p.x);
-      bx[3] = fmax(bx[3], p.y);
-    }
-    finite = __syncthreads_and(finite);  // also publishes the staged positions
-  }
-  auto pos = [&](int j) -> double2 { return LDS ? lpos[j] : gpos[2 * (size_t)j]; };
   double pxi = 0, pyi = 0;
   if (vi) {
     pxi = xb[4 * (size_t)i];
@@ -951,6 +1109,35 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
     kj[m] = INT_MAX;
   }
   const bool fast = vi && !a.rim && a.adj_bits && a.degree[g] >= K && !GF_ABLATE(a, 0x8000);
+  const bool need = vi && !fast && !rim_done;  // ranked by a scan (few rows) or the grid
+  const int nslow = __syncthreads_count(need);
+  const int nfast = a.adj_bits ? __syncthreads_count(fast) : 0;
+  // the env's positions go to LDS for the neighbour path and for the grid; a workgroup
+  // with only a few rows to scan (the rim of a compact swarm) reads them from L2
+  const bool staged = LDS && (nfast > 0 || nslow > kKnnFewSlow);
+  double bx[4] = {-__builtin_inf(), -__builtin_inf(), -__builtin_inf(), -__builtin_inf()};
+  bool finite = true;
+  if (staged) {
+    constexpr int U = 4;  // loads of U agents in flight per thread
+    for (int t0 = tid; t0 < N; t0 += U * kThreads) {
+      double2 p[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (t0 + u * kThreads < N) p[u] = gpos[2 * (size_t)(t0 + u * kThreads)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (t0 + u * kThreads >= N) break;
+        lpos[t0 + u * kThreads] = p[u];
+        finite &= __builtin_isfinite(p[u].x) && __builtin_isfinite(p[u].y);
+        bx[0] = fmax(bx[0], -p[u].x);  // -min x
+        bx[1] = fmax(bx[1], -p[u].y);
+        bx[2] = fmax(bx[2], p[u].x);
+        bx[3] = fmax(bx[3], p[u].y);
+      }
+    }
+    finite = __syncthreads_and(finite);  // also publishes the staged positions
+  }
+  auto pos = [&](int j) -> double2 { return staged ? lpos[j] : gpos[2 * (size_t)j]; };
   if (fast) {  // rank the neighbours only
     const int Wn = (N + 63) >> 6;
     const uint64_t* bits = a.adj_bits + g * Wn;
@@ -976,11 +1163,18 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
       for (int m = 1; m < K; ++m) kj[m] = kj[0];
     }
   }
-  const bool need = vi && !fast && !rim_done;  // ranked through the grid (or a full scan)
-  const int nslow = __syncthreads_count(need);
-  if (nslow > 0) {
+  if (nslow > 0 && nslow <= kKnnFewSlow) {
+    // few rows: each is scanned by its whole wave (knn_wave_scan)
+    uint64_t todo = __ballot(need);
+    while (todo) {
+      const int l = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      knn_wave_scan<K>(pos, N, l, i, pxi, pyi, kr, kj);
+    }
+    if (need) knn_insert<K>(kr, kj, __builtin_inf(), i);  // self last (r2 = inf in the reference)
+  } else if (nslow > 0) {
     bool use_grid = false;
-    if (LDS && finite) {
+    if (staged && finite) {
       // bounding box (workgroup max of -xmin, -ymin, xmax, ymax)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -1013,6 +1207,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
       __syncthreads();
       use_grid = grid_ok;
     }
+    if (GF_ABLATE(a, 0x2000)) use_grid = false;  // ablation: no grid, no search (timing only)
     if (use_grid) {
       const KnnGrid G = grid;
       const int ncell = G.nx * G.ny;
@@ -1054,7 +1249,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
         sorted[slot] = static_cast<unsigned short>(t);
       }
       __syncthreads();
-      if (need) {
+      if (need && !GF_ABLATE(a, 0x1000)) {  // ablation 0x1000: grid only, no search
         const int cx = knn_cell_x(G, pxi), cy = knn_cell_y(G, pyi);
         const int dmax = max(max(cx, G.nx - 1 - cx), max(cy, G.ny - 1 - cy));
         auto range = [&](int y, int xa, int xb2) {  // cells [xa, xb2] of grid row y
@@ -1082,29 +1277,15 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
           if (lim > 0 && kr[K - 1] < lim * lim * (1.0 - 0x1p-40)) break;
         }
       }
-    } else if (need) {
+    } else if (need && !GF_ABLATE(a, 0x2000)) {
       for (int j = 0; j < N; ++j)
         if (j != i) knn_consider<K>(kr, kj, pxi, pyi, pos(j), j);
     }
     // self last (its r2 is inf in the reference), for k >= the agents with finite r2
     if (need) knn_insert<K>(kr, kj, __builtin_inf(), i);
   }
-  if (!vi || rim_done) return;
-  const double2* xi = reinterpret_cast<const double2*>(xb) + 2 * (size_t)i;
-  const double2 pi = xi[0], vv = xi[1];
-#pragma unroll
-  for (int m = 0; m < K; ++m) {
-    const int j = kj[m] < N ? kj[m] : i;  // unfilled slots (non-finite r2 only): self
-    a.idx[g * K + m] = j;
-    const double2* xj = reinterpret_cast<const double2*>(xb) + 2 * (size_t)j;
-    const double2 pj = xj[0], vj = xj[1];
-    float4 o;
-    o.x = static_cast<float>(pi.x - pj.x);
-    o.y = static_cast<float>(pi.y - pj.y);
-    o.z = static_cast<float>(vv.x - vj.x);
-    o.w = static_cast<float>(vv.y - vj.y);
-    reinterpret_cast<float4*>(a.obs + g * 4 * K)[m] = o;
-  }
+  if (!vi || rim_done || GF_ABLATE(a, 0x0800)) return;  // ablation 0x0800: no outputs
+  knn_write_row<K>(a, xb, g, i, N, kr, kj);
 }
 
 // get_stats (:136-143): vel_diffs_i = |v_i - mean v|, min_dists_i = sqrt(min_j r2_ij)
@@ -1175,11 +1356,11 @@ int step_tile(int N) {
   return t < kTileDefault ? t : kTileDefault;
 }
 
-size_t step_lds_bytes(int N, int R, int T, bool ctrl) {
+size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
-  s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0);
-  s += 8 * sizeof(double) + (((size_t)R * 4 + 15) / 16) * 16;
+  s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
+  s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 2 : 1) + 15) / 16) * 16;
   return s;
 }
 
@@ -1198,7 +1379,7 @@ hipError_t max_lds_once(const void* f, std::atomic<uint64_t>& done, int bytes) {
 
 template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
-  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL);
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0);
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
   // would allow
   if (!CTRL && !VAR && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;

@@ -20,6 +20,8 @@ def main():
     steps = int(os.environ.get("KSTEPS", "50"))
     knn = os.environ.get("KNN", "1") == "1"
     env = VecFlockingRelative(B, N, n_neighbors=7)
+    if os.environ.get("DIAG"):  # ablation switches (diagnostic build: GYMFLOCK_LIB=build/lib_diag/...)
+        env.h.diag_switches(int(os.environ["DIAG"], 0))
     x0 = env.reset(seed=0)
     env.set_actions(np.random.RandomState(1234).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
     t0 = time.perf_counter()

@@ -5,17 +5,19 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 rows = [r for r in rows if "flock_" in r["Kernel_Name"]]
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
-REPS = 5
-# per state: (plain steps to reach it), then REPS x (fused step, rim kNN), REPS x full kNN, 1 stats
-i = 0
-for t in (0, 25, 50, 100, 200):
-    while i < len(rows) and "stats" not in rows[i]["Kernel_Name"]:
-        i += 1
-    i += 1  # the stats kernel of h.stats()
-    fused = [dur(rows[i + 2 * k]) for k in range(REPS)]
-    rim = [dur(rows[i + 2 * k + 1]) for k in range(REPS)]
-    i += 2 * REPS
-    full = [dur(rows[i + k]) for k in range(REPS)]
-    i += REPS
-    med = lambda v: sorted(v)[len(v) // 2]
-    print("t=%3d  fused step %.1f us  rim kNN %.1f us  full kNN %.1f us" % (t, med(fused), med(rim), med(full)))
+med = lambda v: sorted(v)[len(v) // 2] if v else float("nan")
+# groups start after each stats kernel (h.stats() of a new state)
+groups, cur = [], None
+for r in rows:
+    if "stats" in r["Kernel_Name"]:
+        cur = []
+        groups.append(cur)
+    elif cur is not None:
+        cur.append(r)
+for t, g in zip((0, 25, 50, 100, 200), groups):
+    plain = [dur(r) for r in g if "step" in r["Kernel_Name"] and r["Kernel_Name"].rstrip(")").split(",")[-2:] != [] and ", 7>" not in r["Kernel_Name"]]
+    fused = [dur(r) for r in g if ", 7>" in r["Kernel_Name"]]
+    knn = [dur(r) for r in g if "knn" in r["Kernel_Name"]]
+    rim, full = knn[:len(fused)], knn[len(fused):]
+    print("t=%3d  plain step %.1f us  fused step %.1f us  rim kNN %.1f us  full kNN %.1f us"
+          % (t, med(plain[:5]), med(fused), med(rim), med(full)))

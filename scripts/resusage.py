@@ -11,7 +11,7 @@ for line in open(sys.argv[1]):
         cur = m.group(1)
         rows[cur] = {}
         continue
-    m = re.search(r"remark:.*?:\s+(VGPRs|VGPRs Spill|AGPRs|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\d+)", line)
+    m = re.search(r"remark:\s.*?(VGPRs Spill|VGPRs|AGPRs|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\d+)", line)
     if m and cur:
         rows[cur][m.group(1)] = int(m.group(2))
 for name, r in rows.items():

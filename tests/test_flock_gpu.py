@@ -538,6 +538,36 @@ def test_knn_pipelined_back_to_back():
     h.close()
 
 
+@pytest.mark.parametrize("spread", [1.0, 2.5])
+def test_knn_radius_history_continuous(spread):
+    """Flocking-v0 over 30 continuous steps (split steps, resident actions): from the
+    third step on, the fused step ranks the rows whose k-th nearest two states back lay
+    beyond 0.8 comm_radius against candidates within 1.5x that distance, and leaves the
+    rest of the sparse rows to the rim kNN. spread 2.5: a swarm 2.5x wider (most agents
+    below 7 neighbours). Indices bit-exact and observations exact against the oracle
+    every third step, and the state chain bit-exact."""
+    n, B = 300, 4
+    x0 = synthetic_batch(B, n, seed0=77)
+    x0[:, :, :2] *= spread
+    rs = np.random.RandomState(78)
+    u = rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7)
+    h.set_state(x0)
+    h.set_actions(u)
+    x = x0.copy()
+    for t in range(1, 31):
+        h.step(None, nat.FE_U_RESIDENT | nat.FE_WITH_KNN)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        if t % 3 == 0:
+            np.testing.assert_array_equal(h.get_state(), x)
+            idx, obs = h.knn()
+            for b in range(B):
+                ridx, robs = orc.knn_observation(x[b])
+                np.testing.assert_array_equal(idx[b], ridx)
+                np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
+    h.close()
+
+
 def test_full_config5_batch_sampled_parity():
     """BASELINE.json configs[4] at full size: 32 envs x N=8192 (8.6 GB of network), one
     step with the fused controller. Whole batch: every env's state bit-exact and its
