@@ -439,7 +439,11 @@ def main():
                     "float32 network; the pair work, not HBM, bounds this mode"}
 
     # Flocking-v0 (§8f rank 1): the same step plus the 7-nearest-neighbour observation
-    # (flocking.py:20-25), dense network kept; a second handle with n_neighbors=7
+    # (flocking.py:20-25), dense network kept; a second handle with n_neighbors=7. The
+    # first handle is closed first: each handle runs three HIP streams, and six streams
+    # share the process's 4 hardware queues (GPU_MAX_HW_QUEUES), which serialises the
+    # step halves and the kNN stream (271 vs 230 us per step with both handles alive)
+    env.close()
     if not args.no_knn_line:
         envk = VecFlockingRelative(B, N, device=local_rank, env_offset=rank * B, n_neighbors=7)
         envk.set_state(x_init)
@@ -455,7 +459,6 @@ def main():
             "note": "Flocking-v0 step: FlockingRelative step + 7-NN observation (idx + obs), from the "
                     "synthetic init under the same random actions"}
         envk.close()
-    env.close()
 
     if rank == 0:
         value = world * B * N * K / elapsed

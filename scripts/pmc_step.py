@@ -18,7 +18,8 @@ h = nat.FlockHandle(N, B)
 h.set_streams(1)
 h.set_state(synthetic_batch(B, N))
 h.set_actions(np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
-h.diag_switches(int(os.environ.get("DIAG", 0)))
+if os.environ.get("DIAG"):  # ablation switches: diagnostic build only (GYMFLOCK_LIB=build/lib_diag/...)
+    h.diag_switches(int(os.environ["DIAG"], 0))
 for _ in range(STEPS):
     h.step(None, nat.FE_U_RESIDENT)
 if os.environ.get("FILL"):
