@@ -63,6 +63,9 @@ struct cov_handle {
   bool has_graph = false, has_state = false;
   // greedy expert (allocated on first use)
   uint16_t* tm_cost = nullptr;
+  uint8_t* tm_cost8 = nullptr;   // uint8 copy of the cost rows (envs that fit), greedy step
+  uint8_t* tm_wide = nullptr;    // (B) 1: the env's matrix needed uint16 entries
+  std::vector<uint8_t> tm_wide_host;
   int16_t* tm_prevT = nullptr;
   uint8_t* tm_flags = nullptr;
   uint8_t* needs_random = nullptr;
@@ -115,7 +118,7 @@ void cov_release(cov_handle* h) {
   gf::CovArgs& a = h->a;
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
-                  a.receivers, a.obs_step, a.axy, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_prevT,
+                  a.receivers, a.obs_step, a.axy, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT,
                   h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
                   h->goff};
   for (void* p : bufs)
@@ -162,8 +165,10 @@ int ensure_time_matrix(cov_handle* h) {
         (rc = calloc_dev(&h->tm_flags, (size_t)B * nchunk * kcap)) ||
         (rc = calloc_dev(&h->needs_random, (size_t)B * h->cfg.n_robots)) || (rc = calloc_dev(&h->tm_envsel, (size_t)B)) ||
         (rc = calloc_dev(&h->tm_sched, (size_t)B * sched_stride)) || (rc = calloc_dev(&h->tm_nslots, (size_t)B)) ||
-        (rc = calloc_dev(&h->tm_nlev, (size_t)B)) || (rc = calloc_dev(&h->tm_overflow, (size_t)B)))
+        (rc = calloc_dev(&h->tm_nlev, (size_t)B)) || (rc = calloc_dev(&h->tm_overflow, (size_t)B)) ||
+        (rc = calloc_dev(&h->tm_cost8, (size_t)B * Tm * Tm)) || (rc = calloc_dev(&h->tm_wide, (size_t)B)))
       return rc;
+    h->tm_wide_host.assign(B, 0);
   }
   std::vector<int32_t> sel;
   int t_lds = 0, e_max = 0;
@@ -192,6 +197,7 @@ int ensure_time_matrix(cov_handle* h) {
   t.receivers = h->a.receivers;
   t.flags = h->tm_flags;
   t.cost = h->tm_cost;
+  t.cost8 = h->tm_cost8;
   t.prevT = h->tm_prevT;
   t.sched = h->tm_sched;
   t.nslots = h->tm_nslots;
@@ -225,6 +231,10 @@ int ensure_time_matrix(cov_handle* h) {
     CV_HIP(hipStreamSynchronize(h->stream));
   }
   h->tm_wide_envs += (int64_t)wide.size();
+  for (int b : sel) h->tm_wide_host[b] = 0;
+  for (int b : wide) h->tm_wide_host[b] = 1;
+  CV_HIP(hipMemcpyAsync(h->tm_wide, h->tm_wide_host.data(), B, hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
   for (int b : sel) h->tm_valid[b] = 1;
   return GF_OK;
 }
@@ -568,6 +578,8 @@ int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random
   g.dirty = a.dirty;
   g.cur = a.cur;
   g.cost = h->tm_cost;
+  g.cost8 = h->tm_cost8;
+  g.wide = h->tm_wide;
   g.prevT = h->tm_prevT;
   g.visited = a.visited;
   g.nvisited = a.nvisited;

@@ -47,6 +47,8 @@ struct CovTmArgs {
   const int32_t* receivers;  // (B,4M)
   uint8_t* flags;            // (B,nchunk,kcap): bit 0 changed, bit 1 some entry inf
   uint16_t* cost;            // (B,Tmax,Tmax) [source][target], 0xFFFF = inf
+  uint8_t* cost8;            // (B,Tmax,Tmax) the same as uint8 (255 = inf), written by the
+                             // uint8 pass only (envs whose hop counts all fit)
   int16_t* prevT;            // (B,Tmax,Tmax) [q][source] = graph_previous[source, q]
   uint32_t* sched;           // (B,sched_stride) batched edge schedule
   int32_t* nslots;           // (B) schedule length
@@ -63,6 +65,8 @@ struct CovGreedyArgs {
   const uint8_t* dirty;
   const int32_t* cur;
   const uint16_t* cost;
+  const uint8_t* cost8;      // used for envs with wide[b] == 0 (half the bytes per row)
+  const uint8_t* wide;       // (B) 1: the env's matrix needed uint16 entries
   const int16_t* prevT;
   const uint8_t* visited;
   const int32_t* nvisited;
