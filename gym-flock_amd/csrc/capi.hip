@@ -525,7 +525,9 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (e = hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreate(&h->tw[0])) != hipSuccess || (e = hipEventCreate(&h->tw[1])) != hipSuccess ||
-      (e = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking)) != hipSuccess ||
+      // the kNN stream only for handles that rank neighbours: a plain handle runs two
+      // streams, so two of them fit the process's 4 hardware queues (GPU_MAX_HW_QUEUES)
+      (cfg->n_neighbors > 0 && (e = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking)) != hipSuccess) ||
       (e = hipEventCreateWithFlags(&h->ev_kin[0], hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kin[1], hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kjoin, hipEventDisableTiming)) != hipSuccess ||
