@@ -82,6 +82,7 @@ struct fe_handle {
   // the one of two states back (complete: the step waits for that state's kNN) to pick
   // the rows it ranks beyond their neighbours, and writes its own
   float* knn_r2[2] = {nullptr, nullptr};
+  uint8_t* knn_rimflag[2] = {nullptr, nullptr};  // per state buffer: blocks with rim rows
   double* vel_diffs = nullptr;
   double* min_dists = nullptr;
   int32_t* degree = nullptr;
@@ -211,7 +212,7 @@ void release(fe_handle* h) {
   if (h->kstream) hipStreamSynchronize(h->kstream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
+                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
                   h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -293,6 +294,7 @@ int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a, int xw) {
     a.knn_idx = h->knn_idx[xw];
     a.knn_obs = h->knn_obs[xw];
     a.knn_r2 = h->knn_r2[xw];
+    a.knn_rimflag = h->knn_rimflag[xw];
     a.knn_jbits = jb;
     a.knn_qmax = (1u << (32 - jb)) - 2u;  // below the all-ones empty-slot key
     a.knn_qscale = std::ldexp(1.0, 32 - jb);
@@ -378,6 +380,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
       a1.knn_idx = a.knn_idx + e0 * K;
       a1.knn_obs = a.knn_obs + e0 * 4 * K;
       a1.knn_r2 = a.knn_r2 + e0;
+      a1.knn_rimflag = a.knn_rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
     }
     hipError_t e = gf::launch_step(a, dyn, uf64, ctrl, h->stream);
     if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
@@ -430,6 +433,7 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.obs = h->knn_obs[h->cur];
   k.rim = mode == 2;
   k.r2k = h->knn_r2[h->cur];
+  k.rimflag = h->knn_rimflag[h->cur];
   k.N = h->cfg.n_agents;
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
@@ -451,6 +455,10 @@ hipError_t clear_knn_history(fe_handle* h) {
   for (float* p : h->knn_r2)
     if (p)
       if (hipError_t e = hipMemsetAsync(p, 0, h->BN * sizeof(float), h->stream); e != hipSuccess) return e;
+  const size_t nf = (size_t)h->cfg.n_envs * ((h->cfg.n_agents + 255) / 256);
+  for (uint8_t* p : h->knn_rimflag)
+    if (p)
+      if (hipError_t e = hipMemsetAsync(p, 0, nf, h->stream); e != hipSuccess) return e;
   return hipSuccess;
 }
 
@@ -516,7 +524,9 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (rc = dalloc(&h->knn_idx[1], h->BN * cfg->n_neighbors)) ||
       (rc = dalloc(&h->knn_obs[0], h->BN * 4 * cfg->n_neighbors)) ||
       (rc = dalloc(&h->knn_obs[1], h->BN * 4 * cfg->n_neighbors)) ||
-      (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_r2[0], h->BN)) || (rc = dalloc(&h->knn_r2[1], h->BN))))) {
+      (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_r2[0], h->BN)) || (rc = dalloc(&h->knn_r2[1], h->BN)))) ||
+      (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_rimflag[0], B * ((N + 255) / 256))) ||
+                                (rc = dalloc(&h->knn_rimflag[1], B * ((N + 255) / 256)))))) {
     release(h);
     return rc;
   }

@@ -20,6 +20,7 @@ constexpr int kTileDefault = 512;   // default tile (measured best, see step_til
 constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
+constexpr int kKnnRimGrid = 256;    // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
                                     // scanned wave-cooperatively from L2, more through the grid
 // kNN LDS: positions (16 B per agent), the grid's cell offsets, agent indices by cell
@@ -74,6 +75,8 @@ struct StepArgs {
   float* knn_obs;         // (B,N,4K)
   float* knn_r2;          // (B,N) k-th nearest r2 of the state two steps back (0: none),
                           // replaced by this state's for the rows ranked here
+  uint8_t* knn_rimflag;   // (B, ceil(N/256)): set for each 256-row block holding a row
+                          // left to the rim kNN (its workgroups read only this byte)
   double knn_qscale;      // 2^qbits
   unsigned knn_qmax;      // 2^qbits - 2
   int knn_jbits;          // bits of the agent index (qbits = 32 - jbits)
@@ -90,6 +93,7 @@ struct KnnArgs {
   const int32_t* degree;     // (B,N) with adj_bits
   int rim;                   // only rows the fused step left unranked (idx[row*K] < 0)
   float* r2k;                // (B,N) or nullptr: each ranked row's k-th nearest r2
+  uint8_t* rimflag;          // rim mode: (B, ceil(N/256)) blocks the step marked (cleared here)
   int diag;                  // ablation: 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path,
                              // 0x1000 grid built but no search, 0x2000 no grid / scan, 0x0800 no outputs
 };

@@ -916,7 +916,10 @@ void flock_step_kernel(StepArgs a) {
     if (frow) {
       const size_t g = env0 + i_row;
       if (slow) {
-        if (fs == 0) a.knn_idx[g * KN] = -1;
+        if (fs == 0) {
+          a.knn_idx[g * KN] = -1;
+          a.knn_rimflag[b * ((N + kThreads - 1) / kThreads) + i_row / kThreads] = 1;
+        }
       } else if (fs < KN) {
         const int j = static_cast<int>(mine & ((1u << jb) - 1u));
         a.knn_idx[g * KN + fs] = j;
@@ -1071,12 +1074,11 @@ __device__ __forceinline__ void knn_write_row(const KnnArgs& a, const double* xb
   }
 }
 
+// One 256-row block L (env L / bpe) of the kNN kernel.
 template <int K, bool LDS>
-__global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void knn_block(const KnnArgs& a, const int L, unsigned char* smem) {
   const int N = a.N;
   const int bpe = (N + kThreads - 1) / kThreads;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / bpe;
   const int i = (L - b * bpe) * kThreads + threadIdx.x;
   const int tid = threadIdx.x;
@@ -1086,8 +1088,12 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   // rim mode: the fused step ranked every row but those it marked with idx = -1; a
   // workgroup without such rows leaves before staging anything
   if (GF_ABLATE(a, 0x0400)) return;  // ablation 0x0400: no kNN kernel work (timing only)
+  // rim mode: only blocks the step flagged hold rows it left unranked
+  if (a.rim && a.rimflag[L] == 0) return;
   const bool rim_done = a.rim && (!vi || a.idx[g * K] >= 0);
-  if (a.rim && __syncthreads_count(!rim_done) == 0) return;
+  const int nrim = a.rim ? __syncthreads_count(!rim_done) : 1;  // every thread has read the flag
+  if (a.rim && threadIdx.x == 0) a.rimflag[L] = 0;
+  if (nrim == 0) return;
   // positions: the whole env staged in LDS (N <= kKnnLdsMax), else read from L2
   const double2* gpos = reinterpret_cast<const double2*>(xb);
   double2* lpos = reinterpret_cast<double2*>(smem);
@@ -1288,6 +1294,24 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   knn_write_row<K>(a, xb, g, i, N, kr, kj);
 }
 
+// Rim mode runs a small grid that walks the blocks (kKnnRimGrid workgroups): it is
+// enqueued beside the next step, whose workgroups hold most CU slots, and a full grid of
+// mostly idle workgroups took ~150 us to drain between them. Other modes: one
+// workgroup per block.
+template <int K, bool LDS>
+__global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (a.rim) {
+    const int nblk = a.B * ((a.N + kThreads - 1) / kThreads);
+    for (int L = blockIdx.x; L < nblk; L += gridDim.x) {
+      knn_block<K, LDS>(a, L, smem);
+      __syncthreads();  // the block's LDS is free for the next one
+    }
+  } else {
+    knn_block<K, LDS>(a, xcd_remap(blockIdx.x, gridDim.x), smem);
+  }
+}
+
 // get_stats (:136-143): vel_diffs_i = |v_i - mean v|, min_dists_i = sqrt(min_j r2_ij)
 // (r2 is exactly symmetric, so the reference's column min equals this row min), plus
 // the degree used by reset()'s acceptance test (:177-184).
@@ -1421,7 +1445,8 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 }
 
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
-  const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
+  int grid = a.B * ((a.N + kThreads - 1) / kThreads);
+  if (a.rim) grid = min(grid, kKnnRimGrid);
   const bool lds = a.N <= kKnnLdsMax;
   const size_t bytes = lds ? knn_lds_bytes(a.N) : 0;
   switch (a.K) {
