@@ -124,13 +124,23 @@ struct fe_handle {
   // step t and beside step t+1. A step that writes the state buffer x[i] (or a bits
   // buffer) an unfinished kNN reads waits for that kNN's event first; every other API
   // call joins kstream into `stream` (use_dev).
-  hipStream_t kstream = nullptr;
+  // After a split step the rim kNN goes out as two launches too: envs [0, B0) on
+  // kstream after `stream`'s half, [B0, B) on kstream2 after stream2's, and each half
+  // of the step after next waits only for its own. One kNN launch after both halves
+  // joined them every step (the step after next waited for it on both streams), so the
+  // halves never drifted out of phase (Flocking-v0).
+  hipStream_t kstream = nullptr, kstream2 = nullptr;
   hipEvent_t ev_kin[2] = {nullptr, nullptr};  // stream / stream2 -> kstream
   hipEvent_t ev_kjoin = nullptr;              // kstream -> stream
+  hipEvent_t ev_kjoin2 = nullptr;             // kstream2 -> stream
   bool k_pending = false;                     // kstream holds work `stream` has not waited for
+  bool k2_pending = false;                    // likewise kstream2
+  int last_b0 = 0;                            // B0 of the last launch if it was split, else 0
   struct KnnReader {
-    hipEvent_t ev = nullptr;
+    hipEvent_t ev = nullptr;                  // the kNN launch (envs [0, B0) if split)
+    hipEvent_t ev2 = nullptr;                 // split: the launch of envs [B0, B) on kstream2
     bool live = false;
+    bool split = false;
     unsigned bmask = 0;                       // bits buffers it reads
   } kread[2];                                 // by the state buffer x[i] the kNN reads
 };
@@ -154,20 +164,40 @@ int join_k(fe_handle* h) {
     GF_HIP(hipEventRecord(h->ev_kjoin, h->kstream));
     GF_HIP(hipStreamWaitEvent(h->stream, h->ev_kjoin, 0));
     h->k_pending = false;
-    for (auto& r : h->kread) r.live = false, r.bmask = 0;
   }
+  if (h->k2_pending) {
+    GF_HIP(hipEventRecord(h->ev_kjoin2, h->kstream2));
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ev_kjoin2, 0));
+    h->k2_pending = false;
+  }
+  for (auto& r : h->kread) r.live = false, r.bmask = 0;
   return GF_OK;
 }
 
+// Whether the next step launch of B envs goes out as two half-batch launches.
+bool split_next(const fe_handle* h, int B) { return h->nsplit > 1 && B >= 2 && h->stream2 && !h->other_work; }
+
 // Before a step writes x[xw] (xw < 0: no state write) and bits buffer bw (bw < 0: none):
-// both step streams wait for the unfinished kNN launches that read them.
+// both step streams wait for the unfinished kNN launches that read them. A kNN split like
+// the step that follows (same halves) orders each half after its own launch only.
 int wait_knn_readers(fe_handle* h, int xw, int bw) {
+  const bool halves = split_next(h, h->cfg.n_envs);
   for (int i = 0; i < 2; ++i) {
     auto& r = h->kread[i];
     if (r.live && (i == xw || (bw >= 0 && ((r.bmask >> bw) & 1u)))) {
-      GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
-      GF_HIP(hipStreamWaitEvent(h->stream2, r.ev, 0));
+      if (r.split && halves) {
+        GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
+        GF_HIP(hipStreamWaitEvent(h->stream2, r.ev2, 0));
+      } else {
+        GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
+        GF_HIP(hipStreamWaitEvent(h->stream2, r.ev, 0));
+        if (r.split) {
+          GF_HIP(hipStreamWaitEvent(h->stream, r.ev2, 0));
+          GF_HIP(hipStreamWaitEvent(h->stream2, r.ev2, 0));
+        }
+      }
       r.live = false;
+      r.split = false;
       r.bmask = 0;
     }
   }
@@ -210,6 +240,7 @@ void release(fe_handle* h) {
   if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
   if (h->kstream) hipStreamSynchronize(h->kstream);
+  if (h->kstream2) hipStreamSynchronize(h->kstream2);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
                   h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
@@ -222,9 +253,10 @@ void release(fe_handle* h) {
   for (hipEvent_t e : h->ag_ev)
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
-                       h->kread[0].ev, h->kread[1].ev})
+                       h->ev_kjoin2, h->kread[0].ev, h->kread[1].ev, h->kread[0].ev2, h->kread[1].ev2})
     if (e) hipEventDestroy(e);
   if (h->kstream) hipStreamDestroy(h->kstream);
+  if (h->kstream2) hipStreamDestroy(h->kstream2);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->comm_stream) hipStreamDestroy(h->comm_stream);
@@ -349,8 +381,9 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     a.bpe = (a.N + a.R - 1) / a.R;
   }
   a.store_fast = h->store_fast[ctrl ? 1 : 0];
-  const bool split = h->nsplit > 1 && a.B >= 2 && h->stream2 && !h->other_work;
+  const bool split = split_next(h, a.B);
   h->other_work = false;
+  h->last_b0 = split ? (a.B + 1) / 2 : 0;
   if (split) {
     // two launches: envs [0, B0) on `stream`, [B0, B) on `stream2`, each after its own
     // half of the previous step; stream2 also waits for whatever `stream` was given
@@ -418,13 +451,13 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
 // 1: the last launch wrote this state's adjacency (packed outputs), which lets agents
 // with >= k neighbours rank only those; 2: the last launch ranked the rows it could.
 int launch_knn_cur(fe_handle* h, int mode) {
-  // on kstream after everything on both step streams (both halves' state and bits)
-  GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
-  GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[0], 0));
-  if (h->s2_pending) {
-    GF_HIP(hipEventRecord(h->ev_kin[1], h->stream2));
-    GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[1], 0));
+#ifdef GF_DIAG
+  if (mode == 2 && (h->diag & 0x80000)) {  // ablation: no rim kNN launch (timing only)
+    h->has_knn = true;
+    return GF_OK;
   }
+#endif
+  auto& r = h->kread[h->cur];
   gf::KnnArgs k{};
   k.x = h->x[h->cur];
   k.adj_bits = mode == 1 ? h->adj_bits[h->bits_cur] : nullptr;
@@ -437,12 +470,55 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.N = h->cfg.n_agents;
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
-  k.diag = h->diag;
+  k.diag = (h->diag >> 12) & 0xfc00;  // kNN kernel switches: 0x400000.. -> 0x0400.. (KnnArgs.diag)
+  if (mode == 2 && h->last_b0 > 0 && h->s2_pending && h->kstream2) {
+    // rim kNN of a split step: each half after its own half of the step (see kstream2)
+    const int B0 = h->last_b0, N = k.N, K = k.K;
+    const size_t e0 = (size_t)B0 * N;
+    gf::KnnArgs k1 = k;
+    k.B = B0;
+    k1.B = h->cfg.n_envs - B0;
+    k1.x = k.x + e0 * 4;
+    k1.idx = k.idx + e0 * K;
+    k1.obs = k.obs + e0 * 4 * K;
+    k1.r2k = k.r2k + e0;
+    k1.rimflag = k.rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
+    k.grid_cap = k1.grid_cap = gf::kKnnRimGrid / 2;
+#ifdef GF_DIAG
+    if (h->diag & 0x100000) {  // experiment: each half's rim kNN in its own step stream
+      hipError_t e = gf::launch_knn(k, h->stream);
+      if (e == hipSuccess) e = gf::launch_knn(k1, h->stream2);
+      if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
+      h->has_knn = true;
+      return GF_OK;
+    }
+#endif
+    GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
+    GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[0], 0));
+    GF_HIP(hipEventRecord(h->ev_kin[1], h->stream2));
+    GF_HIP(hipStreamWaitEvent(h->kstream2, h->ev_kin[1], 0));
+    hipError_t e = gf::launch_knn(k, h->kstream);
+    if (e == hipSuccess) e = gf::launch_knn(k1, h->kstream2);
+    if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
+    GF_HIP(hipEventRecord(r.ev, h->kstream));
+    GF_HIP(hipEventRecord(r.ev2, h->kstream2));
+    r.live = r.split = true;
+    h->k_pending = h->k2_pending = true;
+    h->has_knn = true;
+    return GF_OK;
+  }
+  // on kstream after everything on both step streams (both halves' state and bits)
+  GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
+  GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[0], 0));
+  if (h->s2_pending) {
+    GF_HIP(hipEventRecord(h->ev_kin[1], h->stream2));
+    GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[1], 0));
+  }
   hipError_t e = gf::launch_knn(k, h->kstream);
   if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
-  auto& r = h->kread[h->cur];
   GF_HIP(hipEventRecord(r.ev, h->kstream));
   r.live = true;
+  r.split = false;
   if (mode == 1) r.bmask |= 1u << h->bits_cur;
   h->k_pending = true;
   h->has_knn = true;
@@ -538,6 +614,10 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       // the kNN stream only for handles that rank neighbours: a plain handle runs two
       // streams, so two of them fit the process's 4 hardware queues (GPU_MAX_HW_QUEUES)
       (cfg->n_neighbors > 0 && (e = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking)) != hipSuccess) ||
+      (cfg->n_neighbors > 0 && (e = hipStreamCreateWithFlags(&h->kstream2, hipStreamNonBlocking)) != hipSuccess) ||
+      (e = hipEventCreateWithFlags(&h->ev_kjoin2, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->kread[0].ev2, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->kread[1].ev2, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kin[0], hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kin[1], hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kjoin, hipEventDisableTiming)) != hipSuccess ||
@@ -968,9 +1048,9 @@ int fe_kernel_timing(fe_handle* h, int enable, double* avg_ms, int64_t* launches
 int fe_diag(fe_handle* h, int what, int reps, double* avg_ms) {
   if (!h || reps < 1) return fail(GF_EINVAL, "bad argument");
   if (int rc = use_dev(h)) return rc;
-  if (what >= 0x10000) {  // set ablation switches (low 16 bits) for subsequent step launches
+  if (what >= 0x10000) {  // set ablation switches (all bits but 0x10000) for subsequent launches
 #ifdef GF_DIAG
-    h->diag = what & 0xffff;
+    h->diag = what & ~0x10000;
     return GF_OK;
 #else
     return fail(GF_EINVAL, "ablation switches need the diagnostic build (make -C gym-flock_amd/csrc diag)");

@@ -17,9 +17,13 @@ namespace gf {
 constexpr int kThreads = 256;   // 4 wave64s per workgroup
 constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float64 state)
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
-constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
+#ifndef GF_LDS_PLAIN_FLOOR_KIB  // (a compile-time knob for A/B builds, scripts/build_variant.sh)
+#define GF_LDS_PLAIN_FLOOR_KIB 24
+#endif
+constexpr size_t kStepLdsPlainFloor = GF_LDS_PLAIN_FLOOR_KIB * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
+constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
 constexpr int kKnnRimGrid = 256;    // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
                                     // scanned wave-cooperatively from L2, more through the grid
@@ -94,7 +98,8 @@ struct KnnArgs {
   int rim;                   // only rows the fused step left unranked (idx[row*K] < 0)
   float* r2k;                // (B,N) or nullptr: each ranked row's k-th nearest r2
   uint8_t* rimflag;          // rim mode: (B, ceil(N/256)) blocks the step marked (cleared here)
-  int diag;                  // ablation: 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path,
+  int grid_cap;              // rim mode: workgroups (0: kKnnRimGrid)
+  int diag;                  // ablation (fe_diag bits << 12, apart from the step's): 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path,
                              // 0x1000 grid built but no search, 0x2000 no grid / scan, 0x0800 no outputs
 };
 

@@ -230,6 +230,158 @@ __device__ __forceinline__ void knn_insert_asc(double (&kr)[K], int (&kj)[K], do
   }
 }
 
+template <int K>
+__device__ __forceinline__ void knn_consider(double (&kr)[K], int (&kj)[K], double pxi, double pyi, double2 p,
+                                             int j) {
+  const double dx = pxi - p.x, dy = pyi - p.y;
+  knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
+}
+
+// Row `i` of lane l, ranked by the whole wave: lanes scan columns lane, lane + 64, ...
+// into lane-local K-lists, then K rounds of a wave-wide (r2, j) minimum merge them into
+// lane l's (kr, kj). pos(j): the agent's position.
+template <int K, class Pos>
+__device__ __forceinline__ void knn_wave_scan(const Pos& pos, int N, int l, int i, double pxi, double pyi,
+                                              double (&kr)[K], int (&kj)[K]) {
+  const int lane = threadIdx.x & 63;
+  const int row = __shfl(i, l);
+  const double px = __shfl(pxi, l), py = __shfl(pyi, l);
+  double lr[K];
+  int lj[K];
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    lr[m] = __builtin_inf();
+    lj[m] = INT_MAX;
+  }
+  constexpr int U = 4;  // positions of U columns in flight per lane
+  for (int j0 = lane; j0 < N; j0 += U * 64) {
+    double2 p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (j0 + u * 64 < N) p[u] = pos(j0 + u * 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * 64;
+      if (j < N && j != row) knn_consider<K>(lr, lj, px, py, p[u], j);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    double br = lr[0];
+    int bj = lj[0];
+    for (int o = 32; o > 0; o >>= 1) {
+      const double orr = __shfl_xor(br, o);
+      const int oj = __shfl_xor(bj, o);
+      if (orr < br || (orr == br && oj < bj)) {
+        br = orr;
+        bj = oj;
+      }
+    }
+    if (lane == l) {
+      kr[m] = br;
+      kj[m] = bj;
+    }
+    if (lj[0] == bj) {  // the winner's lane pops its head (columns are disjoint per lane)
+#pragma unroll
+      for (int q = 0; q + 1 < K; ++q) {
+        lr[q] = lr[q + 1];
+        lj[q] = lj[q + 1];
+      }
+      lr[K - 1] = __builtin_inf();
+      lj[K - 1] = INT_MAX;
+    }
+  }
+}
+
+// Inline rim of the fused kNN step: the wave's rows in `todo` (lane bits; lane l holds
+// row il with post-update state me), one at a time. Each is scanned by the whole wave
+// over every agent's post-update position (recomputed from x_in and u, bit-identical to
+// the step's) exactly as knn_wave_scan does, but round m's winner stays in lane m, so
+// lanes 0..K-1 write the row's outputs as knn_write_row does (self inserted last with
+// r2 = inf, the k-th nearest r2 for the fused steps' candidate radius).
+template <bool DYN, bool UF64, int KN>
+__device__ __forceinline__ void step_inline_rim(const StepArgs& a, size_t env0, uint64_t todo, int il,
+                                                const St& me) {
+  const int N = a.N, lane = threadIdx.x & 63;
+  for (; todo; todo &= todo - 1) {
+    const int l = __builtin_ctzll(todo);
+    const int row = __shfl(il, l);
+    const double px = __shfl(me.px, l), py = __shfl(me.py, l);
+    double lr[KN];
+    int lj[KN];
+#pragma unroll
+    for (int m = 0; m < KN; ++m) {
+      lr[m] = __builtin_inf();
+      lj[m] = INT_MAX;
+    }
+    constexpr int U = UF64 ? 2 : 4;  // columns in flight per lane
+    for (int j0 = lane; j0 < N; j0 += U * 64) {
+      St p[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j0 + u * 64 < N) p[u] = load_state<DYN, UF64>(a, env0 + j0 + u * 64);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * 64;
+        if (j < N && j != row) knn_consider<KN>(lr, lj, px, py, make_double2(p[u].px, p[u].py), j);
+      }
+    }
+    double rr = __builtin_inf();
+    int rj = INT_MAX;
+#pragma unroll
+    for (int m = 0; m < KN; ++m) {
+      double br = lr[0];
+      int bj = lj[0];
+      for (int o = 32; o > 0; o >>= 1) {
+        const double orr = __shfl_xor(br, o);
+        const int oj = __shfl_xor(bj, o);
+        if (orr < br || (orr == br && oj < bj)) {
+          br = orr;
+          bj = oj;
+        }
+      }
+      if (lane == m) {
+        rr = br;
+        rj = bj;
+      }
+      if (lj[0] == bj) {  // the winner's lane pops its head (columns are disjoint per lane)
+#pragma unroll
+        for (int q = 0; q + 1 < KN; ++q) {
+          lr[q] = lr[q + 1];
+          lj[q] = lj[q + 1];
+        }
+        lr[KN - 1] = __builtin_inf();
+        lj[KN - 1] = INT_MAX;
+      }
+    }
+    // self last, (inf, row) in (r2, j) order: lanes past its slot shift up by one
+    const int pslot = __popcll(__ballot(lane < KN && (rr < __builtin_inf() || (rr == __builtin_inf() && rj < row))));
+    const double ur = __shfl_up(rr, 1);
+    const int uj = __shfl_up(rj, 1);
+    if (lane > pslot) {
+      rr = ur;
+      rj = uj;
+    } else if (lane == pslot) {
+      rr = __builtin_inf();
+      rj = row;
+    }
+    const double vx = __shfl(me.vx, l), vy = __shfl(me.vy, l);
+    if (lane < KN) {
+      const size_t g = env0 + row;
+      if (lane == KN - 1 && a.knn_r2) a.knn_r2[g] = static_cast<float>(rr);
+      const int j = rj < N ? rj : row;  // unfilled slots (non-finite r2 only): self
+      a.knn_idx[g * KN + lane] = j;
+      const St o = load_state<DYN, UF64>(a, env0 + j);
+      float4 ob;
+      ob.x = static_cast<float>(px - o.px);
+      ob.y = static_cast<float>(py - o.py);
+      ob.z = static_cast<float>(vx - o.vx);
+      ob.w = static_cast<float>(vy - o.vy);
+      reinterpret_cast<float4*>(a.knn_obs)[g * KN + lane] = ob;
+    }
+  }
+}
+
 __device__ __forceinline__ double clip10(double v) {  // np.clip(v, -10, 10); NaN stays NaN
   return v < -10.0 ? -10.0 : (v > 10.0 ? 10.0 : v);
 }
@@ -292,6 +444,56 @@ __device__ __forceinline__ unsigned dpp_u32(unsigned v, int ctrl) {
     case 0x4E: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
     case 0x141: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x141, 0xF, 0xF, false));
     default: return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x140, 0xF, 0xF, false));
+  }
+}
+// group_min_u32 with the group size a compile-time constant (the fused kNN merge: a
+// runtime S left a branch around every DPP step)
+template <int S>
+__device__ __forceinline__ unsigned group_min_u32c(unsigned w) {
+  if constexpr (S > 1) w = min(w, dpp_u32(w, 0xB1));
+  if constexpr (S > 2) w = min(w, dpp_u32(w, 0x4E));
+  if constexpr (S > 4) w = min(w, dpp_u32(w, 0x141));
+  if constexpr (S > 8) w = min(w, dpp_u32(w, 0x140));
+#pragma unroll
+  for (int o = 16; o < S; o <<= 1) w = min(w, static_cast<unsigned>(__shfl_xor(static_cast<int>(w), o)));
+  return w;
+}
+// Sum over groups of S consecutive lanes (S a power of two), the xor butterfly's tree:
+// DPP lane swaps (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror) give each
+// lane the same partial sums a shfl_xor by 1, 2, 4, 8 would (the lanes of each half group
+// already agree), so every lane ends with identical bits and the same order of additions,
+// without the LDS round trips of ds_bpermute.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl) {
+  const int lo = static_cast<int>(dpp_u32(static_cast<unsigned>(__double2loint(v)), ctrl));
+  const int hi = static_cast<int>(dpp_u32(static_cast<unsigned>(__double2hiint(v)), ctrl));
+  return __hiloint2double(hi, lo);
+}
+template <int S, class V>
+__device__ __forceinline__ V group_sum_c(V v) {
+  if constexpr (sizeof(V) == 8) {
+    if constexpr (S > 1) v += dpp_f64(v, 0xB1);
+    if constexpr (S > 2) v += dpp_f64(v, 0x4E);
+    if constexpr (S > 4) v += dpp_f64(v, 0x141);
+    if constexpr (S > 8) v += dpp_f64(v, 0x140);
+  } else {
+    if constexpr (S > 1) v += static_cast<V>(dpp_u32(static_cast<unsigned>(v), 0xB1));
+    if constexpr (S > 2) v += static_cast<V>(dpp_u32(static_cast<unsigned>(v), 0x4E));
+    if constexpr (S > 4) v += static_cast<V>(dpp_u32(static_cast<unsigned>(v), 0x141));
+    if constexpr (S > 8) v += static_cast<V>(dpp_u32(static_cast<unsigned>(v), 0x140));
+  }
+#pragma unroll
+  for (int o = 16; o < S; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// f(std::integral_constant<int, S>) for the runtime slice count S in {4, 8, 16, 32, 64}
+template <class F>
+__device__ __forceinline__ void with_slices(int S, F&& f) {
+  switch (S) {
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 16: f(std::integral_constant<int, 16>{}); break;
+    case 32: f(std::integral_constant<int, 32>{}); break;
+    default: f(std::integral_constant<int, 64>{}); break;
   }
 }
 __device__ __forceinline__ unsigned group_min_u32(unsigned w, int S) {
@@ -386,19 +588,20 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
                                               int i0, int i_row, bool writer, int S, int tid) {
   const int N = a.N, T = a.T;
   const size_t env0 = (size_t)b * N;
-  // combine the S slices of each row (xor butterfly: identical bits in every lane)
-  for (int o = 1; o < S; o <<= 1) {
-    f0 += __shfl_xor(f0, o);
-    f1 += __shfl_xor(f1, o);
-    f2 += __shfl_xor(f2, o);
-    f3 += __shfl_xor(f3, o);
-    f4 += __shfl_xor(f4, o);
-    f5 += __shfl_xor(f5, o);
+  // combine the S slices of each row (butterfly: identical bits in every lane)
+  with_slices(S, [&](auto Sc) {
+    constexpr int SS = decltype(Sc)::value;
+    f0 = group_sum_c<SS>(f0);
+    f1 = group_sum_c<SS>(f1);
+    f2 = group_sum_c<SS>(f2);
+    f3 = group_sum_c<SS>(f3);
+    f4 = group_sum_c<SS>(f4);
+    f5 = group_sum_c<SS>(f5);
     if constexpr (CTRL) {
-      gx += __shfl_xor(gx, o);
-      gy += __shfl_xor(gy, o);
+      gx = group_sum_c<SS>(gx);
+      gy = group_sum_c<SS>(gy);
     }
-  }
+  });
 
   const double Svx = block_sum(svx, red);
   const double Svy = block_sum(svy, red);
@@ -568,6 +771,14 @@ void flock_step_kernel(StepArgs a) {
     if (T < N) issue(T, pfb);
   }
 
+  // kNN: lane r's row's k-th nearest r2 two states back (predicted rows, below), loaded
+  // before everything else: issued later, its round trip sat between the tile loads and
+  // pass 1 of every workgroup
+  [[maybe_unused]] float khist = 0.f;
+  if constexpr (KN > 0) {
+    if (lane < nrows && a.knn_r2) khist = a.knn_r2[env0 + i0 + lane];
+  }
+
   // rows owned by this workgroup (post-update state)
   for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
 
@@ -606,6 +817,7 @@ void flock_step_kernel(StepArgs a) {
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
     if constexpr (KN > 0) {
+     if (!GF_ABLATE(a, 0x200000)) {  // diag 0x200000: no insertion (timing only)
       const double qd = r2 * ksc;
       const unsigned q = qd < static_cast<double>(a.knn_qmax) ? static_cast<unsigned>(qd) : a.knn_qmax;
       unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
@@ -615,6 +827,7 @@ void flock_step_kernel(StepArgs a) {
         v = max(kk[m], v);
         kk[m] = lo;
       }
+     }
       if (!isadj && !(CTRL && isnear)) return;  // a candidate only: no features
     }
     // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
@@ -699,8 +912,9 @@ void flock_step_kernel(StepArgs a) {
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
       if constexpr (KN > 0) {
-        const float h = (lane < nrows && a.knn_r2) ? a.knn_r2[env0 + i0 + lane] : 0.f;
-        const bool pr = h >= static_cast<float>(0.64 * a.cr2) && h < 1.0e30f;
+        const float h = khist;
+        // diag 0x20000: no predicted rows (timing only)
+        const bool pr = h >= static_cast<float>(0.64 * a.cr2) && h < 1.0e30f && !GF_ABLATE(a, 0x20000);
         predm = __ballot(pr);
         if (wid == 0 && lane < nrows) rthr[lane] = pr ? 2.25f * h : 0.f;
       }
@@ -862,7 +1076,7 @@ void flock_step_kernel(StepArgs a) {
       const int wb = fs * wpt, we = min(Wn, wb + wpt);
       for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
     }
-    for (int o = 1; o < S; o <<= 1) deg += __shfl_xor(deg, o);
+    with_slices(S, [&](auto Sc) { deg = group_sum_c<decltype(Sc)::value>(deg); });
     if (frow && fs == 0) {
       inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
       if (a.degree_out) a.degree_out[env0 + i0 + fr] = deg;
@@ -884,6 +1098,7 @@ void flock_step_kernel(StepArgs a) {
 
   [[maybe_unused]] RawState<UF64> kraw{};
   [[maybe_unused]] bool kgo = false;
+  [[maybe_unused]] bool kinl = false;  // this row is ranked by its wave at the end (inline rim)
   if constexpr (KN > 0) {
    if (!GF_ABLATE(a, 1)) {  // diag 1: no merge / kNN outputs (timing only)
     // Merge the S slices' lists of each row (S consecutive lanes): KN + 1 rounds of an
@@ -898,31 +1113,40 @@ void flock_step_kernel(StepArgs a) {
     const int jb = a.knn_jbits;
     unsigned mine = 0xFFFFFFFFu, prevq = 0xFFFFFFFFu;
     bool slow = false;
+    auto merge = [&](auto Sc) {
+      constexpr int SS = decltype(Sc)::value;
 #pragma unroll
-    for (int m = 0; m <= KN; ++m) {
-      unsigned w = kk[0];
-      w = group_min_u32(w, S);
-      const bool pop = kk[0] == w;
+      for (int m = 0; m <= KN; ++m) {
+        const unsigned w = group_min_u32c<SS>(kk[0]);
+        const bool pop = kk[0] == w;
 #pragma unroll
-      for (int q = 0; q + 1 < KN; ++q) kk[q] = pop ? kk[q + 1] : kk[q];
-      kk[KN - 1] = pop ? 0xFFFFFFFFu : kk[KN - 1];
-      const bool real = w != 0xFFFFFFFFu;
-      const unsigned qw = w >> jb;
-      if (m < KN) mine = (fs == m) ? w : mine;
-      if (m == KN - 1) slow |= qw > a.knn_qmax - 2u;
-      slow |= real && m > 0 && qw == prevq;
-      prevq = qw;
-    }
+        for (int q = 0; q + 1 < KN; ++q) kk[q] = pop ? kk[q + 1] : kk[q];
+        kk[KN - 1] = pop ? 0xFFFFFFFFu : kk[KN - 1];
+        const bool real = w != 0xFFFFFFFFu;
+        const unsigned qw = w >> jb;
+        if (m < KN) mine = (fs == m) ? w : mine;
+        if (m == KN - 1) slow |= qw > a.knn_qmax - 2u;
+        slow |= real && m > 0 && qw == prevq;
+        prevq = qw;
+      }
+    };
+    with_slices(S, merge);  // S >= KN + 1 = 8 here (step_fused_knn_ok)
+    // a wave with at most kStepInlineRim such rows ranks them itself after the epilogue
+    // (an exact scan of the env, as the rim kernel's few-rows path); more go to the rim
+    // kernel (idx = -1, block flagged)
+    // diag 0x40000: every such row to the rim kernel (timing only)
+    const bool inl = __popcll(__ballot(frow && slow && fs == 0)) <= kStepInlineRim && !GF_ABLATE(a, 0x40000);
     if (frow) {
       const size_t g = env0 + i_row;
       if (slow) {
-        if (fs == 0) {
+        kinl = inl;
+        if (fs == 0 && !inl) {
           a.knn_idx[g * KN] = -1;
           a.knn_rimflag[b * ((N + kThreads - 1) / kThreads) + i_row / kThreads] = 1;
         }
       } else if (fs < KN) {
         const int j = static_cast<int>(mine & ((1u << jb) - 1u));
-        a.knn_idx[g * KN + fs] = j;
+        if (!GF_ABLATE(a, 0x20000000)) a.knn_idx[g * KN + fs] = j;  // diag: no idx/obs stores
         // the neighbour's state: its loads are issued here and used after the
         // epilogue, so their latency runs under the epilogue's sums
         if (!GF_ABLATE(a, 32)) {  // diag 32: no observation gather (timing only)
@@ -949,8 +1173,13 @@ void flock_step_kernel(StepArgs a) {
       ob.y = static_cast<float>(me.py - o.py);
       ob.z = static_cast<float>(me.vx - o.vx);
       ob.w = static_cast<float>(me.vy - o.vy);
-      reinterpret_cast<float4*>(a.knn_obs)[(env0 + i_row) * KN + fs] = ob;
+      if (!GF_ABLATE(a, 0x20000000)) reinterpret_cast<float4*>(a.knn_obs)[(env0 + i_row) * KN + fs] = ob;
     }
+    // inline rim: the wave's remaining rows, each scanned by the whole wave over every
+    // agent's post-update position (recomputed from x_in and u, bit-identical to the
+    // step's), with the rim kernel's ranking and outputs (knn_wave_scan, knn_write_row)
+    const uint64_t todo = __ballot(kinl && fs == 0);
+    if (todo) step_inline_rim<DYN, UF64, KN>(a, env0, todo, i_row, me);
   }
   GF_STAMP(10);
 #if defined(GF_STAMPS) && GF_STAMPS >= 2
@@ -976,13 +1205,6 @@ void flock_step_kernel(StepArgs a) {
 //    rounding of cell assignment), so the row stops once its K-th r2 is below that
 //    bound squared. The visiting order does not matter: the insertion is a total order
 //    on (r2, j). Non-finite or extreme coordinates fall back to a scan of every column.
-template <int K>
-__device__ __forceinline__ void knn_consider(double (&kr)[K], int (&kj)[K], double pxi, double pyi, double2 p,
-                                             int j) {
-  const double dx = pxi - p.x, dy = pyi - p.y;
-  knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
-}
-
 struct KnnGrid {
   double x0, y0, invh, bound_h, err;  // origin, 1/h, h, cell-assignment error (distance)
   int nx, ny;
@@ -993,62 +1215,6 @@ __device__ __forceinline__ int knn_cell_x(const KnnGrid& G, double x) {
 }
 __device__ __forceinline__ int knn_cell_y(const KnnGrid& G, double y) {
   return min(G.ny - 1, max(0, static_cast<int>((y - G.y0) * G.invh)));
-}
-
-// Row `i` of lane l, ranked by the whole wave: lanes scan columns lane, lane + 64, ...
-// into lane-local K-lists, then K rounds of a wave-wide (r2, j) minimum merge them into
-// lane l's (kr, kj). pos(j): the agent's position.
-template <int K, class Pos>
-__device__ __forceinline__ void knn_wave_scan(const Pos& pos, int N, int l, int i, double pxi, double pyi,
-                                              double (&kr)[K], int (&kj)[K]) {
-  const int lane = threadIdx.x & 63;
-  const int row = __shfl(i, l);
-  const double px = __shfl(pxi, l), py = __shfl(pyi, l);
-  double lr[K];
-  int lj[K];
-#pragma unroll
-  for (int m = 0; m < K; ++m) {
-    lr[m] = __builtin_inf();
-    lj[m] = INT_MAX;
-  }
-  constexpr int U = 4;  // positions of U columns in flight per lane
-  for (int j0 = lane; j0 < N; j0 += U * 64) {
-    double2 p[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (j0 + u * 64 < N) p[u] = pos(j0 + u * 64);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = j0 + u * 64;
-      if (j < N && j != row) knn_consider<K>(lr, lj, px, py, p[u], j);
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < K; ++m) {
-    double br = lr[0];
-    int bj = lj[0];
-    for (int o = 32; o > 0; o >>= 1) {
-      const double orr = __shfl_xor(br, o);
-      const int oj = __shfl_xor(bj, o);
-      if (orr < br || (orr == br && oj < bj)) {
-        br = orr;
-        bj = oj;
-      }
-    }
-    if (lane == l) {
-      kr[m] = br;
-      kj[m] = bj;
-    }
-    if (lj[0] == bj) {  // the winner's lane pops its head (columns are disjoint per lane)
-#pragma unroll
-      for (int q = 0; q + 1 < K; ++q) {
-        lr[q] = lr[q + 1];
-        lj[q] = lj[q + 1];
-      }
-      lr[K - 1] = __builtin_inf();
-      lj[K - 1] = INT_MAX;
-    }
-  }
 }
 
 // One ranked row's outputs: indices, observation x_i - x_j (flocking.py:24) and its k-th
@@ -1446,7 +1612,7 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
   int grid = a.B * ((a.N + kThreads - 1) / kThreads);
-  if (a.rim) grid = min(grid, kKnnRimGrid);
+  if (a.rim) grid = min(grid, a.grid_cap > 0 ? a.grid_cap : kKnnRimGrid);
   const bool lds = a.N <= kKnnLdsMax;
   const size_t bytes = lds ? knn_lds_bytes(a.N) : 0;
   switch (a.K) {
