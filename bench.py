@@ -258,9 +258,11 @@ def bench_config4(args, with_greedy=False):
     starts, unvisited sets and actions differ per env; actions stay resident in HBM."""
     from gym_flock.envs.spatial.maps import generate_targets
     from gym_flock.vec import VecCoverage
-    # a Coverage step is ~11 us of latency-bound work: at least 200 steps per window, so
-    # the window's fixed start/end cost (~0.1 ms) does not dominate (20 steps: 15.7 us)
-    R, B, M, K, W = 200, 512, 1000, max(200, args.steps), args.warmup
+    # a Coverage step is ~9 us of latency-bound work: at least 1000 steps and 20 warm-up
+    # steps per window, so neither the window's fixed start/end cost (~0.1 ms) nor the
+    # first steps after the reset dominate (200-step windows after 5 warm-up steps read
+    # 8.7-12.4 us on one build, profiles/r02/v5)
+    R, B, M, K, W = 200, 512, 1000, max(1000, args.steps), max(20, args.warmup)
     np.random.seed(8)
     targets = generate_targets()
     v = VecCoverage(B, R, max_nodes=M, episode_length=10 ** 9)

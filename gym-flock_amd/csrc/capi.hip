@@ -483,7 +483,7 @@ int launch_knn_cur(fe_handle* h, int mode) {
     k1.obs = k.obs + e0 * 4 * K;
     k1.r2k = k.r2k + e0;
     k1.rimflag = k.rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
-    k.grid_cap = k1.grid_cap = gf::kKnnRimGrid / 2;
+    k.grid_cap = k1.grid_cap = GF_RIM_HALF_GRID;
 #ifdef GF_DIAG
     if (h->diag & 0x100000) {  // experiment: each half's rim kNN in its own step stream
       hipError_t e = gf::launch_knn(k, h->stream);

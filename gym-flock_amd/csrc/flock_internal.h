@@ -24,7 +24,10 @@ constexpr size_t kStepLdsPlainFloor = GF_LDS_PLAIN_FLOOR_KIB * 1024;  // plain s
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
-constexpr int kKnnRimGrid = 256;    // rim kNN: workgroups walking the flagged blocks
+constexpr int kKnnRimGrid = 256;
+#ifndef GF_RIM_HALF_GRID  // rim kNN workgroups per half-batch launch (A/B builds)
+#define GF_RIM_HALF_GRID (gf::kKnnRimGrid / 2)
+#endif    // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
                                     // scanned wave-cooperatively from L2, more through the grid
 // kNN LDS: positions (16 B per agent), the grid's cell offsets, agent indices by cell
