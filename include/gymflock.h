@@ -219,7 +219,7 @@ int cov_get_obs(cov_handle* h, int env, float* nodes, float* edges, int32_t* sen
                 int64_t* step);
 int cov_get_rewards(cov_handle* h, double* reward, uint8_t* done);   /* (B), (B) */
 int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes); /* closest_targets :427 */
-int cov_get_visited(cov_handle* h, int env, uint8_t* visited);
+int cov_get_visited(cov_handle* h, int env, uint8_t* visited); /* (max_nodes - R): reset()'s layout */
 int cov_get_n_motion(cov_handle* h, int32_t* n_motion);
 /* Back-to-back cov_step calls go out as two half-batch launches on two streams (as
  * fe_set_streams; cov_set_streams(h, 1) for one); every other call, cov_sync

@@ -1,0 +1,235 @@
+// Host AddressSanitizer driver for the C-ABI (include/gymflock.h). Built by
+// tests/asan/Makefile with the host side of every translation unit instrumented
+// (-Xarch_host -fsanitize=address; device code is not instrumented: GPU ASan is not
+// available on this pool). Without a GPU it runs every argument-validation and
+// no-device path; with one (MI355X box) it also runs a short FlockingRelative /
+// Flocking-v0 / Coverage / graph-helper session through the borrowed-host-pointer
+// entry points, so that ASan sees every host buffer the library reads or writes.
+// Exit code 0 = all checks passed and ASan reported nothing (it aborts otherwise).
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "gymflock.h"
+
+static int failures = 0;
+#define CHECK(cond)                                                              \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      std::fprintf(stderr, "FAIL %s:%d: %s (last error: %s)\n", __FILE__, __LINE__, \
+                   #cond, fe_last_error());                                      \
+      ++failures;                                                                \
+    }                                                                            \
+  } while (0)
+
+static fe_config flock_cfg(int n, int b, int k) {
+  fe_config c{};
+  c.n_agents = n;
+  c.n_envs = b;
+  c.comm_radius = 0.9;
+  c.dt = 0.01;
+  c.action_scalar = 10.0;
+  c.mean_pooling = 1;
+  c.centralized = 1;
+  c.n_neighbors = k;
+  c.device = 0;
+  return c;
+}
+
+static void validation_paths() {
+  CHECK(fe_abi_version() >= 1);
+  fe_handle* h = reinterpret_cast<fe_handle*>(0x1);
+  CHECK(fe_create(nullptr, &h) != 0);
+  CHECK(h == reinterpret_cast<fe_handle*>(0x1));  // untouched on a null config
+  fe_config c = flock_cfg(0, 1, 0);
+  CHECK(fe_create(&c, &h) != 0 && h == nullptr);
+  c = flock_cfg(16, 0, 0);
+  CHECK(fe_create(&c, &h) != 0);
+  c = flock_cfg(16, 1, 9);  // k not in the supported set
+  CHECK(fe_create(&c, &h) != 0);
+  c = flock_cfg(4, 1, 7);  // k > n_agents
+  CHECK(fe_create(&c, &h) != 0);
+  c = flock_cfg(16, 1, 0);
+  c.comm_radius = 0.0;
+  CHECK(fe_create(&c, &h) != 0);
+  CHECK(std::strlen(fe_last_error()) > 0);
+  // null handles on every entry point that takes one
+  CHECK(fe_destroy(nullptr) == 0);
+  CHECK(fe_step(nullptr, nullptr, 0) != 0);
+  CHECK(fe_sync(nullptr) != 0);
+  CHECK(fe_get_rewards(nullptr, nullptr) != 0);
+  CHECK(fe_get_state(nullptr, nullptr) != 0);
+  CHECK(fe_set_state(nullptr, nullptr) != 0);
+  CHECK(fe_controller(nullptr, 1, nullptr) != 0);
+  CHECK(fe_get_knn(nullptr, 0, nullptr, nullptr) != 0);
+  cov_handle* ch = nullptr;
+  CHECK(cov_create(nullptr, &ch) != 0);
+  cov_config cc{};
+  cc.n_robots = 0;
+  cc.n_envs = 1;
+  cc.max_nodes = 100;
+  cc.episode_length = 75;
+  cc.res = 5.5;
+  cc.motion_radius = 6.6;
+  CHECK(cov_create(&cc, &ch) != 0);
+  CHECK(cov_destroy(nullptr) == 0);
+  CHECK(gu_create(0, nullptr) != 0);
+}
+
+static bool have_device() {
+  fe_config c = flock_cfg(16, 1, 0);
+  fe_handle* h = nullptr;
+  const int rc = fe_create(&c, &h);
+  if (rc == 0) {
+    fe_destroy(h);
+    return true;
+  }
+  // the no-device path must fail loudly, not crash
+  CHECK(std::strstr(fe_last_error(), "device") != nullptr || std::strstr(fe_last_error(), "HIP") != nullptr);
+  return false;
+}
+
+static void flocking_session() {
+  const int N = 96, B = 3, K = 7;
+  fe_config c = flock_cfg(N, B, K);
+  fe_handle* h = nullptr;
+  CHECK(fe_create(&c, &h) == 0);
+  if (!h) return;
+  CHECK(fe_reset_synthetic(h, 11, 5.0) == 0);
+  std::vector<double> x((size_t)B * N * 4);
+  CHECK(fe_get_state(h, x.data()) == 0);
+  std::vector<float> u((size_t)B * N * 2);
+  for (size_t i = 0; i < u.size(); ++i) u[i] = static_cast<float>((i % 17) / 8.5 - 1.0);
+  for (int s = 0; s < 4; ++s) CHECK(fe_step(h, u.data(), FE_WITH_KNN) == 0);
+  CHECK(fe_set_actions(h, u.data(), 0) == 0);
+  for (int s = 0; s < 4; ++s) CHECK(fe_step(h, nullptr, FE_U_RESIDENT | FE_WITH_KNN) == 0);
+  CHECK(fe_step(h, nullptr, FE_U_RESIDENT | FE_WITH_CONTROLLER) == 0);
+  CHECK(fe_step(h, nullptr, FE_U_EXPERT | FE_WITH_CONTROLLER) == 0);
+  std::vector<double> ctl((size_t)B * N * 2);
+  CHECK(fe_controller(h, 1, ctl.data()) == 0);
+  std::vector<float> sv((size_t)N * 6), net((size_t)N * N);
+  std::vector<double> rew(B), vd(N), md(N), ctrl_env((size_t)N * 2);
+  std::vector<int32_t> idx((size_t)B * N * K), deg(N);
+  std::vector<float> obs((size_t)B * N * 4 * K);
+  for (int e = 0; e < B; ++e) {
+    CHECK(fe_get_state_values(h, e, sv.data()) == 0);
+    CHECK(fe_get_network(h, e, net.data()) == 0);
+    CHECK(fe_get_network_rows(h, e, N - 5, 5, net.data()) == 0);
+    CHECK(fe_get_controls(h, e, ctrl_env.data()) == 0);
+    CHECK(fe_get_stats_ex(h, e, vd.data(), md.data(), deg.data()) == 0);
+  }
+  CHECK(fe_get_rewards(h, rew.data()) == 0);
+  CHECK(fe_get_knn(h, -1, idx.data(), obs.data()) == 0);
+  for (int32_t j : idx) CHECK(j >= 0 && j < N);
+  CHECK(fe_get_state_values(h, B, sv.data()) != 0);  // env out of range
+  CHECK(fe_get_network_rows(h, 0, N - 2, 5, net.data()) != 0);
+  std::vector<uint64_t> bits((size_t)N * ((N + 63) / 64));
+  CHECK(fe_step(h, nullptr, FE_U_RESIDENT | FE_PACKED_NETWORK) == 0);
+  CHECK(fe_get_network_packed(h, 1, bits.data(), deg.data()) == 0);
+  fe_variant v{};
+  v.n_frozen = 2;
+  v.n_vel_zero = 2;
+  v.u_scale = 10.0;
+  v.x_scale = 1.0;
+  CHECK(fe_set_variant(h, &v) == 0);
+  CHECK(fe_step(h, u.data(), FE_WITH_CONTROLLER) == 0);
+  std::vector<double> dts(B, 0.01);
+  CHECK(fe_set_dt(h, dts.data()) == 0);
+  CHECK(fe_step(h, u.data(), 0) == 0);
+  CHECK(fe_set_state_env(h, 1, x.data()) == 0);
+  CHECK(fe_get_state_env(h, 2, x.data()) == 0);
+  fe_buffers bufs{};
+  CHECK(fe_device_buffers(h, &bufs) == 0 && bufs.x != nullptr);
+  CHECK(fe_sync(h) == 0);
+  CHECK(fe_destroy(h) == 0);
+}
+
+static void coverage_session() {
+  const int R = 6, B = 2, M = 200;
+  cov_config cc{};
+  cc.n_robots = R;
+  cc.n_envs = B;
+  cc.max_nodes = M;
+  cc.episode_length = 75;
+  cc.res = 5.5;
+  cc.motion_radius = 6.6;
+  cc.device = 0;
+  cc.horizon = -1;
+  cov_handle* h = nullptr;
+  CHECK(cov_create(&cc, &h) == 0);
+  if (!h) return;
+  // a 10 x 8 lattice of targets, spacing res
+  const int T = 80;
+  std::vector<double> tg((size_t)T * 2);
+  for (int i = 0; i < T; ++i) {
+    tg[2 * i] = 5.5 * (i % 10);
+    tg[2 * i + 1] = 5.5 * (i / 10);
+  }
+  CHECK(cov_set_targets(h, -1, T, tg.data()) == 0);
+  std::vector<int32_t> start((size_t)B * R);
+  for (int i = 0; i < B * R; ++i) start[i] = (7 * i) % T;
+  std::vector<uint8_t> visited((size_t)B * (M - R), 0);  // [B][max_nodes - R]
+  CHECK(cov_reset(h, start.data(), visited.data()) == 0);
+  std::vector<int32_t> act((size_t)B * R);
+  std::vector<uint8_t> rnd((size_t)B * R);
+  int64_t nrnd = 0;
+  for (int s = 0; s < 6; ++s) {
+    CHECK(cov_controller_greedy(h, act.data(), rnd.data(), &nrnd) == 0);
+    for (int i = 0; i < B * R; ++i)
+      if (rnd[i]) act[i] = i % 4;
+    CHECK(cov_step(h, act.data(), 0) == 0);
+  }
+  std::vector<float> nodes((size_t)M * 3), edges((size_t)4 * M);
+  std::vector<int32_t> snd((size_t)4 * M), rcv((size_t)4 * M), rn(R);
+  int64_t step = 0;
+  CHECK(cov_get_obs(h, 1, nodes.data(), edges.data(), snd.data(), rcv.data(), &step) == 0);
+  std::vector<double> rew(B), xr((size_t)R * 2);
+  std::vector<uint8_t> done(B), vis(M - R);  // cov_get_visited: max_nodes - R entries
+  CHECK(cov_get_rewards(h, rew.data(), done.data()) == 0);
+  CHECK(cov_get_robots(h, 0, xr.data(), rn.data()) == 0);
+  CHECK(cov_get_visited(h, 0, vis.data()) == 0);
+  std::vector<int32_t> cost((size_t)T * T), prev((size_t)T * T);
+  CHECK(cov_get_time_matrix(h, 0, cost.data(), prev.data()) == 0);
+  CHECK(cov_get_obs(h, B, nodes.data(), edges.data(), snd.data(), rcv.data(), &step) != 0);
+  CHECK(cov_sync(h) == 0);
+  CHECK(cov_destroy(h) == 0);
+}
+
+static void graph_session() {
+  gu_graph* g = nullptr;
+  CHECK(gu_create(0, &g) == 0);
+  if (!g) return;
+  const int n = 40;
+  std::vector<double> p((size_t)n * 2);
+  for (int i = 0; i < n; ++i) {
+    p[2 * i] = 0.37 * i;
+    p[2 * i + 1] = 0.11 * (i % 7);
+  }
+  int64_t ne = 0;
+  CHECK(gu_radius_edges(g, p.data(), n, nullptr, n, 1.0, 0, &ne) == 0 && ne > 0);
+  CHECK(gu_radius_edges(g, p.data(), -1, nullptr, n, 1.0, 0, &ne) != 0);
+  std::vector<int32_t> s(ne > 0 ? ne : 1), r(ne > 0 ? ne : 1);
+  std::vector<double> d(ne > 0 ? ne : 1), diff(ne > 0 ? 2 * ne : 2);
+  CHECK(gu_get_edges(g, s.data(), r.data(), d.data(), diff.data()) == 0);
+  CHECK(gu_destroy(g) == 0);
+}
+
+int main() {
+  validation_paths();
+  if (have_device()) {
+    std::printf("device present: running the GPU sessions\n");
+    flocking_session();
+    coverage_session();
+    graph_session();
+  } else {
+    std::printf("no device: validation and no-device paths only\n");
+  }
+  if (failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  std::printf("capi_asan: ok\n");
+  return 0;
+}
