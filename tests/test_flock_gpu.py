@@ -568,6 +568,42 @@ def test_knn_radius_history_continuous(spread):
     h.close()
 
 
+@pytest.mark.parametrize("per_wave", [1, 2, 3, 8])
+def test_knn_unranked_rows_inline_and_rim(per_wave):
+    """Rows the fused step cannot rank (here: outliers 3 comm radii from everyone, with
+    no radius history yet) go to the wave's own exact scan when a wave (8 rows at N=256)
+    holds at most two of them, and to the rim kNN kernel otherwise. per_wave outliers in
+    every 8-row group: 1 and 2 take the inline scan, 3 and 8 the rim kernel (env 1 mixes
+    the two: outliers only in its even groups). Indices bit-exact and observations exact
+    against the oracle for 4 continuous steps (the history then ranks them in the step)."""
+    n, B = 256, 3
+    x0 = synthetic_batch(B, n, seed0=91)
+    for b in range(B):
+        for g in range(n // 8):
+            if b == 1 and g % 2:
+                continue
+            for k in range(per_wave):
+                i = 8 * g + k
+                ang = 2.399963 * i  # spread on a circle far outside the swarm
+                x0[b, i, 0] = (30.0 + 2.7 * i) * np.cos(ang)
+                x0[b, i, 1] = (30.0 + 2.7 * i) * np.sin(ang)
+    u = np.random.RandomState(92).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7)
+    h.set_state(x0)
+    h.set_actions(u)
+    x = x0.copy()
+    for t in range(4):
+        h.step(None, nat.FE_U_RESIDENT | nat.FE_WITH_KNN)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        np.testing.assert_array_equal(h.get_state(), x)
+        idx, obs = h.knn()
+        for b in range(B):
+            ridx, robs = orc.knn_observation(x[b])
+            np.testing.assert_array_equal(idx[b], ridx)
+            np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
+    h.close()
+
+
 def test_full_config5_batch_sampled_parity():
     """BASELINE.json configs[4] at full size: 32 envs x N=8192 (8.6 GB of network), one
     step with the fused controller. Whole batch: every env's state bit-exact and its
