@@ -802,12 +802,18 @@ void flock_step_kernel(StepArgs a) {
   // r2 < Tr = max(thr, comm_radius^2). A pair's key is
   //   (q << jbits) | j,  q = min(floor(r2 * 2^qbits / Tr), 2^qbits - 2),
   // a 32-bit integer whose order is (q, j): q never decreases as r2 grows, so keys of
-  // different q are in true (r2, j) order. Each thread keeps its KN smallest keys sorted
-  // (a min/max exchange chain, 2 VALU per entry, no branches).
-  [[maybe_unused]] unsigned kk[KN > 0 ? KN : 1];
+  // different q are in true (r2, j) order. Each thread keeps its KL smallest keys sorted
+  // (a min/max exchange chain, 2 VALU per entry, no branches); a slice with more keys
+  // drops its largest. A drop matters only if the dropped key is among the row's KN + 1
+  // smallest (agents indexed in spatial order put a row's nearest in one slice); the
+  // merge detects the only way that can happen and leaves such a row unranked. (Lists
+  // of 4 or 5 measured no faster: with 4, ~1 % of the rows hold 5 of their 8 nearest in
+  // one slice and fall to the exact scan.)
+  constexpr int KL = KN > 0 ? (KN < GF_KNN_SLICE_LIST ? KN : GF_KNN_SLICE_LIST) : 1;
+  [[maybe_unused]] unsigned kk[KL];
   if constexpr (KN > 0) {
 #pragma unroll
-    for (int m = 0; m < KN; ++m) kk[m] = 0xFFFFFFFFu;
+    for (int m = 0; m < KL; ++m) kk[m] = 0xFFFFFFFFu;
   }
   // one neighbour pair (row fr = me, tile column c): features and controller gradient.
   // The row's state is read from LDS per feature pass, so it holds no registers
@@ -822,7 +828,7 @@ void flock_step_kernel(StepArgs a) {
       const unsigned q = qd < static_cast<double>(a.knn_qmax) ? static_cast<unsigned>(qd) : a.knn_qmax;
       unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
 #pragma unroll
-      for (int m = 0; m < KN; ++m) {
+      for (int m = 0; m < KL; ++m) {
         const unsigned lo = min(kk[m], v);
         v = max(kk[m], v);
         kk[m] = lo;
@@ -1108,20 +1114,23 @@ void flock_step_kernel(StepArgs a) {
     // when (a) the KN-th key has q <= 2^qbits - 4, so its r2 < Tr and every agent left
     // out of the ranking (r2 >= Tr) is farther, and (b) the KN + 1 smallest keys have
     // distinct q: then the top KN are strictly closer than every other agent and
-    // strictly ordered among themselves. Any other row (too few agents ranked, equal
-    // q) gets idx = -1 and is ranked exactly by flock_knn_kernel (rim mode).
+    // strictly ordered among themselves; and (c) no slice that filled its list had all
+    // of it popped: a slice's dropped keys exceed its kept ones, so only then can one
+    // of them be among the KN + 1 smallest. Any other row (too few agents ranked, equal
+    // q, (c)) is left unranked (inline scan or rim kernel).
     const int jb = a.knn_jbits;
     unsigned mine = 0xFFFFFFFFu, prevq = 0xFFFFFFFFu;
     bool slow = false;
     auto merge = [&](auto Sc) {
       constexpr int SS = decltype(Sc)::value;
+      const bool kfull = kk[KL - 1] != 0xFFFFFFFFu;
 #pragma unroll
       for (int m = 0; m <= KN; ++m) {
         const unsigned w = group_min_u32c<SS>(kk[0]);
         const bool pop = kk[0] == w;
 #pragma unroll
-        for (int q = 0; q + 1 < KN; ++q) kk[q] = pop ? kk[q + 1] : kk[q];
-        kk[KN - 1] = pop ? 0xFFFFFFFFu : kk[KN - 1];
+        for (int q = 0; q + 1 < KL; ++q) kk[q] = pop ? kk[q + 1] : kk[q];
+        kk[KL - 1] = pop ? 0xFFFFFFFFu : kk[KL - 1];
         const bool real = w != 0xFFFFFFFFu;
         const unsigned qw = w >> jb;
         if (m < KN) mine = (fs == m) ? w : mine;
@@ -1129,6 +1138,7 @@ void flock_step_kernel(StepArgs a) {
         slow |= real && m > 0 && qw == prevq;
         prevq = qw;
       }
+      slow |= group_min_u32c<SS>((kfull && kk[0] == 0xFFFFFFFFu) ? 0u : 1u) == 0u;  // (c)
     };
     with_slices(S, merge);  // S >= KN + 1 = 8 here (step_fused_knn_ok)
     // a wave with at most kStepInlineRim such rows ranks them itself after the epilogue

@@ -604,6 +604,36 @@ def test_knn_unranked_rows_inline_and_rim(per_wave):
     h.close()
 
 
+def test_knn_spatially_indexed_line():
+    """Agents indexed in spatial order along a jittered line (spacing 0.1 < comm_radius):
+    each row's 8 nearest sit in one feature-pass slice (128 consecutive columns), which
+    holds more than 7 of the row's neighbours and drops the rest. The merge must see that
+    the dropped keys include the row's 8th nearest (needed for the exactness test of the
+    7th) and leave the row to the exact scan. Indices and observations against the
+    oracle for 3 steps."""
+    n, B = 1024, 2
+    rs = np.random.RandomState(93)
+    x0 = np.zeros((B, n, 4))
+    for b in range(B):
+        x0[b, :, 0] = 0.1 * np.arange(n) + 1e-9 * rs.standard_normal(n)
+        x0[b, :, 1] = 0.02 * np.sin(0.37 * np.arange(n)) * b
+        x0[b, :, 2:] = rs.uniform(-0.01, 0.01, size=(n, 2))
+    u = rs.uniform(-0.01, 0.01, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7)
+    h.set_state(x0)
+    h.set_actions(u)
+    x = x0.copy()
+    for t in range(3):
+        h.step(None, nat.FE_U_RESIDENT | nat.FE_WITH_KNN)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        idx, obs = h.knn()
+        for b in range(B):
+            ridx, robs = orc.knn_observation(x[b])
+            np.testing.assert_array_equal(idx[b], ridx)
+            np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
+    h.close()
+
+
 def test_full_config5_batch_sampled_parity():
     """BASELINE.json configs[4] at full size: 32 envs x N=8192 (8.6 GB of network), one
     step with the fused controller. Whole batch: every env's state bit-exact and its
