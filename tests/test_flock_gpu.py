@@ -604,19 +604,25 @@ def test_knn_unranked_rows_inline_and_rim(per_wave):
     h.close()
 
 
-def test_knn_spatially_indexed_line():
-    """Agents indexed in spatial order along a jittered line (spacing 0.1 < comm_radius):
-    each row's 8 nearest sit in one feature-pass slice (128 consecutive columns), which
-    holds more than 7 of the row's neighbours and drops the rest. The merge must see that
-    the dropped keys include the row's 8th nearest (needed for the exactness test of the
-    7th) and leave the row to the exact scan. Indices and observations against the
-    oracle for 3 steps."""
-    n, B = 1024, 2
+@pytest.mark.parametrize("n,layout", [(1024, "line"), (300, "line"), (4096, "grid")])
+def test_knn_spatially_indexed_line(n, layout):
+    """Agents indexed in spatial order: along a jittered line (spacing 0.1 < comm_radius)
+    each row's 8 nearest sit in one feature-pass slice (consecutive columns), which holds
+    more than 7 of the row's neighbours and drops the rest. The merge must see that the
+    dropped keys may include the row's 8th nearest (needed for the exactness test of the
+    7th) and leave the row to the exact scan. "grid": a jittered square lattice indexed
+    row-major (spacing 0.3). Indices and observations against the oracle for 3 steps."""
+    B = 2
     rs = np.random.RandomState(93)
     x0 = np.zeros((B, n, 4))
     for b in range(B):
-        x0[b, :, 0] = 0.1 * np.arange(n) + 1e-9 * rs.standard_normal(n)
-        x0[b, :, 1] = 0.02 * np.sin(0.37 * np.arange(n)) * b
+        if layout == "line":
+            x0[b, :, 0] = 0.1 * np.arange(n) + 1e-9 * rs.standard_normal(n)
+            x0[b, :, 1] = 0.02 * np.sin(0.37 * np.arange(n)) * b
+        else:
+            w = int(np.sqrt(n))
+            x0[b, :, 0] = 0.3 * (np.arange(n) % w) + 1e-3 * rs.standard_normal(n)
+            x0[b, :, 1] = 0.3 * (np.arange(n) // w) + 1e-3 * rs.standard_normal(n)
         x0[b, :, 2:] = rs.uniform(-0.01, 0.01, size=(n, 2))
     u = rs.uniform(-0.01, 0.01, size=(B, n, 2)).astype(np.float32)
     h = nat.FlockHandle(n, B, n_neighbors=7)
