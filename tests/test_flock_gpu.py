@@ -640,6 +640,58 @@ def test_knn_spatially_indexed_line(n, layout):
     h.close()
 
 
+def _ordered_layout(kind, n, rs):
+    """Agent positions whose indices follow space (users often build swarms that way)."""
+    if kind == "disk_by_x":
+        p = rs.uniform(-1, 1, size=(4 * n, 2))
+        p = p[np.hypot(p[:, 0], p[:, 1]) < 1][:n] * np.sqrt(n) ** 0.5
+        return p[np.argsort(p[:, 0], kind="stable")]
+    if kind == "clusters":
+        c = rs.uniform(-6, 6, size=(8, 2))
+        lab = np.sort(rs.randint(0, 8, size=n))
+        return c[lab] + 0.25 * rs.standard_normal((n, 2))
+    if kind == "zorder":
+        p = rs.uniform(0, 4, size=(n, 2)) * np.sqrt(n) / 8
+        q = (p / p.max() * 1023).astype(np.int64)
+        key = np.zeros(n, np.int64)
+        for bit in range(10):
+            key |= ((q[:, 0] >> bit) & 1) << (2 * bit) | ((q[:, 1] >> bit) & 1) << (2 * bit + 1)
+        return p[np.argsort(key, kind="stable")]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("n", [64, 513, 1024])
+@pytest.mark.parametrize("kind", ["disk_by_x", "clusters", "zorder"])
+def test_knn_fused_spatial_orders(kind, n):
+    """Flocking-v0 on swarms whose agent indices follow space (sorted by x, grouped by
+    cluster, Z-order), so a row's nearest crowd into few feature-pass slices: 4
+    continuous steps (radius history included), states, adjacency, indices and
+    observations against the oracle every step."""
+    B = 2
+    rs = np.random.RandomState(1000 + n)
+    x0 = np.zeros((B, n, 4))
+    for b in range(B):
+        x0[b, :, :2] = _ordered_layout(kind, n, rs)
+        x0[b, :, 2:] = rs.uniform(-1, 1, size=(n, 2))
+    u = rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7)
+    h.set_state(x0)
+    h.set_actions(u)
+    x = x0.copy()
+    for t in range(4):
+        h.step(None, nat.FE_U_RESIDENT | nat.FE_WITH_KNN)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        np.testing.assert_array_equal(h.get_state(), x)
+        idx, obs = h.knn()
+        net = h.network()
+        for b in range(B):
+            ridx, robs = orc.knn_observation(x[b])
+            np.testing.assert_array_equal(idx[b], ridx)
+            np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
+            np.testing.assert_array_equal(net[b] > 0, orc.pair_geometry(x[b])[4] < 0.9 * 0.9)
+    h.close()
+
+
 def test_full_config5_batch_sampled_parity():
     """BASELINE.json configs[4] at full size: 32 envs x N=8192 (8.6 GB of network), one
     step with the fused controller. Whole batch: every env's state bit-exact and its
