@@ -374,6 +374,32 @@ gf::StepArgs base_args(fe_handle* h) {
   return a;
 }
 
+// The launch arguments of envs [b0, b0 + nb) of a batched launch a.
+gf::StepArgs env_range(const fe_handle* h, const gf::StepArgs& a, int b0, int nb, bool uf64) {
+  const int N = a.N;
+  const size_t Wn = (N + 63) / 64, e0 = (size_t)b0 * N;
+  gf::StepArgs r = a;
+  r.B = nb;
+  r.x_in = a.x_in + e0 * 4;
+  if (a.x_out) r.x_out = a.x_out + e0 * 4;
+  if (a.u) r.u = static_cast<const char*>(a.u) + e0 * 2 * (uf64 ? 8 : 4);
+  if (a.state_values) r.state_values = a.state_values + e0 * 6;
+  if (a.network) r.network = a.network + e0 * N;
+  if (a.ctrl_out) r.ctrl_out = a.ctrl_out + e0 * 2;
+  if (a.reward) r.reward = a.reward + b0;
+  if (a.dt_env) r.dt_env = a.dt_env + b0;
+  if (a.adj_bits) r.adj_bits = a.adj_bits + e0 * Wn;
+  if (a.degree_out) r.degree_out = a.degree_out + e0;
+  if (a.knn_idx) {
+    const size_t K = h->cfg.n_neighbors;
+    r.knn_idx = a.knn_idx + e0 * K;
+    r.knn_obs = a.knn_obs + e0 * 4 * K;
+    r.knn_r2 = a.knn_r2 + e0;
+    r.knn_rimflag = a.knn_rimflag + (size_t)b0 * ((N + gf::kThreads - 1) / gf::kThreads);
+  }
+  return r;
+}
+
 int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
   gf::StepArgs a = a_in;
   if (ctrl && !a.variant && !a.knn_idx && h->R_ctrl != a.R) {  // fused kNN keeps R (slices >= k)
@@ -388,35 +414,31 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     // two launches: envs [0, B0) on `stream`, [B0, B) on `stream2`, each after its own
     // half of the previous step; stream2 also waits for whatever `stream` was given
     // since (host action copies, state uploads, consumers of the last outputs)
-    if (h->main_dirty) {
+    const int B = a.B, B0 = (B + 1) / 2;
+    const gf::StepArgs a1 = env_range(h, a, B0, B - B0, uf64);
+    hipError_t e = hipSuccess;
+    if (h->main_dirty && GF_DEPHASE && B0 >= 2) {
+      // both streams idle (the first split step after other work): the second half
+      // would start beside the first and the two would run in phase for many steps.
+      // The first half's first quarter goes alone, the second half starts after it, and
+      // the rest of the first half runs beside that, so the halves start a quarter
+      // period apart.
+      const int Bq = B0 / 2;
+      e = gf::launch_step(env_range(h, a, 0, Bq, uf64), dyn, uf64, ctrl, h->stream);
       GF_HIP(hipEventRecord(h->ev_main, h->stream));
       GF_HIP(hipStreamWaitEvent(h->stream2, h->ev_main, 0));
       h->main_dirty = false;
+      if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
+      if (e == hipSuccess) e = gf::launch_step(env_range(h, a, Bq, B0 - Bq, uf64), dyn, uf64, ctrl, h->stream);
+    } else {
+      if (h->main_dirty) {
+        GF_HIP(hipEventRecord(h->ev_main, h->stream));
+        GF_HIP(hipStreamWaitEvent(h->stream2, h->ev_main, 0));
+        h->main_dirty = false;
+      }
+      e = gf::launch_step(env_range(h, a, 0, B0, uf64), dyn, uf64, ctrl, h->stream);
+      if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
     }
-    const int B = a.B, B0 = (B + 1) / 2, N = a.N;
-    const size_t Wn = (N + 63) / 64, e0 = (size_t)B0 * N;
-    gf::StepArgs a1 = a;
-    a.B = B0;
-    a1.B = B - B0;
-    a1.x_in = a.x_in + e0 * 4;
-    if (a.x_out) a1.x_out = a.x_out + e0 * 4;
-    if (a.u) a1.u = static_cast<const char*>(a.u) + e0 * 2 * (uf64 ? 8 : 4);
-    if (a.state_values) a1.state_values = a.state_values + e0 * 6;
-    if (a.network) a1.network = a.network + e0 * N;
-    if (a.ctrl_out) a1.ctrl_out = a.ctrl_out + e0 * 2;
-    if (a.reward) a1.reward = a.reward + B0;
-    if (a.dt_env) a1.dt_env = a.dt_env + B0;
-    if (a.adj_bits) a1.adj_bits = a.adj_bits + e0 * Wn;
-    if (a.degree_out) a1.degree_out = a.degree_out + e0;
-    if (a.knn_idx) {
-      const size_t K = h->cfg.n_neighbors;
-      a1.knn_idx = a.knn_idx + e0 * K;
-      a1.knn_obs = a.knn_obs + e0 * 4 * K;
-      a1.knn_r2 = a.knn_r2 + e0;
-      a1.knn_rimflag = a.knn_rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
-    }
-    hipError_t e = gf::launch_step(a, dyn, uf64, ctrl, h->stream);
-    if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
     if (e != hipSuccess) return fail_hip("flock_step_kernel launch", e);
     h->s2_pending = true;
     if (h->timing) h->tw_steps++;

@@ -23,6 +23,9 @@ constexpr int kTileDefault = 512;   // default tile (measured best, see step_til
 constexpr size_t kStepLdsPlainFloor = GF_LDS_PLAIN_FLOOR_KIB * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
+#ifndef GF_DEPHASE  // split steps: de-phase the halves at the first split step (A/B builds)
+#define GF_DEPHASE 1
+#endif
 #ifndef GF_KNN_SLICE_LIST  // fused kNN: keys each feature-pass slice keeps (A/B builds)
 #define GF_KNN_SLICE_LIST 7
 #endif
