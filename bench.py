@@ -442,8 +442,8 @@ def main():
 
     # Flocking-v0 (§8f rank 1): the same step plus the 7-nearest-neighbour observation
     # (flocking.py:20-25), dense network kept; a second handle with n_neighbors=7. The
-    # first handle is closed first: each handle runs three HIP streams, and six streams
-    # share the process's 4 hardware queues (GPU_MAX_HW_QUEUES), which serialises the
+    # first handle is closed first: the kNN handle runs four HIP streams, the process's 4
+    # hardware queues (GPU_MAX_HW_QUEUES); a second live handle shares them, which serialises the
     # step halves and the kNN stream (271 vs 230 us per step with both handles alive)
     env.close()
     if not args.no_knn_line:
