@@ -78,3 +78,27 @@ def test_two_ranks_rendezvous_and_whole_vector_check(corrupt):
         assert m0 and not m1 and not e0 and not e1
     else:
         assert m0 and m1 and e0 and e1
+
+
+@pytest.mark.timeout(180)
+def test_eight_ranks_rendezvous_and_whole_vector_check():
+    """The driver's 8-GPU shape (one rank per GPU) on the CPU: 8 ranks meet over the host
+    channel, share rank 0's unique id, agree on the max time, and each verifies the whole
+    gathered vector (5 envs over 8 ranks: some ranks hold none)."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, False, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _rewards_for(0, TOTAL_ENVS)
+    for rank, uid, gathered, mine, every, tmax, imported_torch in res:
+        assert uid == res[0][1] and len(uid) == 128
+        assert tmax == world - 0.5
+        assert mine and every and not imported_torch
+        np.testing.assert_array_equal(gathered, want)
