@@ -27,7 +27,15 @@ def main():
     if os.environ.get("DIAG"):  # ablation switches (diagnostic build: GYMFLOCK_LIB=build/lib_diag/...)
         env.h.diag_switches(int(os.environ["DIAG"], 0))
     x0 = env.reset(seed=0)
-    env.set_actions(np.random.RandomState(1234).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
+    u = np.random.RandomState(1234).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    if os.environ.get("LAYOUT") == "lattice":  # worst case: exact ties in every row, every step
+        w = int(np.ceil(np.sqrt(N)))
+        x0 = np.zeros((B, N, 4))
+        x0[:, :, 0] = 0.25 * (np.arange(N) % w)
+        x0[:, :, 1] = 0.25 * (np.arange(N) // w)
+        u[:] = 0.0
+        env.reset(x=x0)
+    env.set_actions(u)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < float(os.environ.get("CLOCK_S", "0.3")):
         for _ in range(8):
