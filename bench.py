@@ -455,9 +455,15 @@ def main():
         for _ in range(min(W, 5)):
             envk.step(resident=True, knn=True)
         ek, kk_ms = timed(envk, ranks, K, lambda s: envk.step(resident=True, knn=True))
+        # the step's bytes + per agent idx (7 x int32), obs (28 x float32) and the k-th
+        # nearest r2 (float32) written, the history r2 read
+        kb = B * (step_bytes(N) + N * (7 * 4 + 28 * 4 + 4 + 4))
         extra["flocking_v0_knn7"] = {
             "value": world * B * N * K / ek, "unit": "agent-steps/s", "ms_per_step": 1e3 * ek / K,
             "region_ms_per_step": kk_ms, "ratio_to_plain_step": ek / elapsed,
+            "algorithmic_bytes_per_step": kb,
+            "achieved_GBs": kb / (kk_ms * 1e-3) / 1e9 if kk_ms > 0 else None,
+            "frac_of_hbm_peak": kb / (kk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if kk_ms > 0 else None,
             "note": "Flocking-v0 step: FlockingRelative step + 7-NN observation (idx + obs), from the "
                     "synthetic init under the same random actions"}
         envk.close()
