@@ -18,7 +18,7 @@ np.random.seed(8)
 targets = generate_targets()
 v = VecCoverage(B, R, max_nodes=M, episode_length=10 ** 9)
 v.set_targets(targets)
-if os.environ.get("STREAMS"):  # launches per step (cov_set_streams: 1, 2 or 4)
+if os.environ.get("STREAMS"):  # launches per step (cov_set_streams: 1 or 2)
     v.h.set_streams(int(os.environ["STREAMS"]))
 rs = np.random.RandomState(7)
 walls, kern = [], []
