@@ -317,11 +317,13 @@ def test_config5_size_sampled_rows():
     h.close()
 
 
-def test_split_steps_match_single_stream():
+@pytest.mark.parametrize("B", [3, 5, 8])
+def test_split_steps_match_single_stream(B):
     """Two half-batch launches per step on two streams (the default) give the same bits
     as one launch per step, over resident, host and closed-loop steps mixed with
-    getters, kNN and packed outputs (the join / ordering rules of fe_set_streams)."""
-    n, B = 300, 5
+    getters, kNN and packed outputs (the join / ordering rules of fe_set_streams), and
+    back-to-back fused kNN steps (de-phased first split step, rim kNN per half)."""
+    n = 300
     x0 = synthetic_batch(B, n, seed0=3000)
     rs = np.random.RandomState(3001)
     us = [rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32) for _ in range(6)]
@@ -342,6 +344,11 @@ def test_split_steps_match_single_stream():
         got += [h.controls()]
         h.step(us[2], nat.FE_PACKED_NETWORK)
         got += [h.get_state(), h.network_packed()[0], h.rewards()]
+        h.set_actions(us[3])
+        for _ in range(5):  # back-to-back Flocking-v0 steps
+            h.step(None, nat.FE_U_RESIDENT | nat.FE_WITH_KNN)
+        idx, obs = h.knn()
+        got += [h.get_state(), idx, obs, h.rewards()]
         outs.append(got)
         h.close()
     for a, b in zip(*outs):
