@@ -389,7 +389,16 @@ def main():
     gather = None
     if multi:
         uid = group.broadcast_bytes(env.h.comm_unique_id() if rank == 0 else b"")
-        gather = RcclRewardGather(env.h, world, rank, uid)
+        # RCCL prints a version banner on the process's stdout at communicator init; the
+        # bench's stdout carries only the JSON line, so fd 1 points at stderr meanwhile
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            gather = RcclRewardGather(env.h, world, rank, uid)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     log("setup %.1fs: N=%d B=%d per GPU, world=%d" % (time.perf_counter() - t_setup, N, B, world))
 
     def plain(s):

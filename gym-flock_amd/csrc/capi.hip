@@ -105,6 +105,7 @@ struct fe_handle {
   int nranks = 1, rank = 0;
   double* gather = nullptr;             // kBlocks x nranks x kGatherBlock x B
   hipEvent_t step_ev = nullptr;
+  hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
   hipEvent_t ag_ev[kBlocks] = {};
   bool ag_pending[kBlocks] = {};
@@ -249,6 +250,7 @@ void release(fe_handle* h) {
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
   if (h->step_ev) hipEventDestroy(h->step_ev);
+  if (h->step_ev2) hipEventDestroy(h->step_ev2);
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
   for (hipEvent_t e : h->ag_ev)
     if (e) hipEventDestroy(e);
@@ -1123,6 +1125,7 @@ int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
   h->rank = rank;
   GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
   GF_HIP(hipEventCreateWithFlags(&h->step_ev, hipEventDisableTiming));
+  GF_HIP(hipEventCreateWithFlags(&h->step_ev2, hipEventDisableTiming));
   for (auto& e : h->ag_ev) GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (int rc = dalloc(&h->gather, (size_t)kBlocks * nranks * kGatherBlock * h->cfg.n_envs)) return rc;
   return GF_OK;
@@ -1131,7 +1134,11 @@ int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
 int fe_allgather_rewards(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->comm) return fail(GF_ESTATE, "fe_comm_init not called");
-  if (int rc = use_dev(h)) return rc;
+  // a step-path call: the gather's stream waits for both step streams' latest work
+  // (events only), so back-to-back split steps around it stay split and out of phase
+  // (use_dev's join would make the next step a single launch: every 8th step of the
+  // multi-rank bench)
+  if (int rc = use_dev_step(h)) return rc;
   const size_t B = h->cfg.n_envs;
   const int blk = h->rslot / kGatherBlock;
   const int count = h->rslot % kGatherBlock + 1;  // steps of this block written so far
@@ -1139,6 +1146,10 @@ int fe_allgather_rewards(fe_handle* h) {
   double* dst = h->gather + (size_t)blk * h->nranks * kGatherBlock * B;
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
   GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
+  if (h->stream2) {
+    GF_HIP(hipEventRecord(h->step_ev2, h->stream2));
+    GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev2, 0));
+  }
   ncclResult_t r = ncclAllGather(src, dst, (size_t)count * B, ncclFloat64, h->comm, h->comm_stream);
   if (r != ncclSuccess) return fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
   GF_HIP(hipEventRecord(h->ag_ev[blk], h->comm_stream));
