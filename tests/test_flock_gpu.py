@@ -728,3 +728,42 @@ def test_full_config5_batch_sampled_parity():
         close_sv(sv[b][rows], ref["state_values"])
         np.testing.assert_allclose(ctrl[b][rows], ref["ctrl"], rtol=1e-9, atol=1e-12)
     h.close()
+
+
+def test_knn_bench_workload_long_run():
+    """The bench's Flocking-v0 line at full size (BASELINE.json configs[1]: 256 envs x
+    N=1024, the bench's synthetic init and resident random actions, split steps) for 220
+    continuous steps, over which the swarm spreads until every agent is sparse (rows
+    ranked from the radius history, the inline scan and the rim kernel all take part).
+    Whole batch: the state chain bit-exact against the oracle; every row's 7 indices
+    distinct, not the row itself, and in non-decreasing distance. Sampled envs: indices
+    bit-exact and observations exact against the oracle at t = 1, 2, 3, 25, 60, 120, 220."""
+    n, B = 1024, 256
+    env = VecFlockingRelative(B, n, n_neighbors=7)
+    x = env.reset(seed=0).copy()
+    u = np.random.RandomState(1234).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    env.set_actions(u)
+    sampled = (0, 1, 77, 128, 200, 255)
+    checks = {1, 2, 3, 25, 60, 120, 220}
+    rows = np.arange(n)[:, None]
+    for t in range(1, 221):
+        env.step(resident=True, knn=True)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        if t not in checks:
+            continue
+        np.testing.assert_array_equal(env.get_state(), x)
+        idx_all, obs_all = env.knn()
+        for b in range(B):
+            idx, obs = idx_all[b], obs_all[b]
+            assert idx.min() >= 0 and idx.max() < n
+            assert not (idx == rows).any()
+            s = np.sort(idx, axis=1)
+            assert not (s[:, 1:] == s[:, :-1]).any()
+            d = x[b][idx, :2] - x[b][:, None, :2]
+            r2 = (d * d).sum(-1)
+            assert (np.diff(r2, axis=1) >= 0).all()
+            if b in sampled:
+                ridx, robs = orc.knn_observation(x[b])
+                np.testing.assert_array_equal(idx, ridx)
+                np.testing.assert_array_equal(obs, robs.astype(np.float32))
+    env.close()
