@@ -506,6 +506,20 @@ __device__ __forceinline__ unsigned group_min_u32(unsigned w, int S) {
 }
 
 // Lane l of (w0, w1) takes the wave-uniform 64-bit mask m.
+// Flocking-v0 predicted row's candidate bound: float32 d2 < bound covers every agent with
+// r2 < th (float32 error of d2 at |d| <= sqrt(th): 2^-23 |d| (Pi + Pj + |d|) + 2^-22 r2,
+// taken x8); -1 (no candidates) at huge coordinates (those rows go to the rim kNN)
+__device__ __forceinline__ float cand_bound(float th, float pu) {
+  float tcr = -1.f;
+  if (th > 0.f && pu < 1.0e5f) {
+    const double t = th;
+    const double dc = ldexp((static_cast<double>(pu) + 4.0) * (sqrt(t) + 1.0) + t, -20);
+    tcr = static_cast<float>(t + dc);
+    if (static_cast<double>(tcr) < t + dc) tcr = nextafterf(tcr, __builtin_inff());
+  }
+  return tcr;
+}
+
 __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m, int l) {
   w0 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m), l, static_cast<int>(w0)));
   w1 = static_cast<unsigned>(gf_writelane_i32(static_cast<int>(m >> 32), l, static_cast<int>(w1)));
@@ -956,6 +970,38 @@ void flock_step_kernel(StepArgs a) {
       const f2v qx = {qa.x, qb.x}, qy = {qa.y, qb.y};
       unsigned wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0, na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
       uint64_t band = 0;
+      // most rows predicted: their candidate test rides on the adjacency loop's d2
+      unsigned fca0 = 0, fca1 = 0, fcb0 = 0, fcb1 = 0;
+      int fp = 0, frp = 0;
+      bool fused = false;
+      if constexpr (KN > 0) fused = 2 * __popcll(predm) >= nrows;
+      if (fused) {
+        const float ftcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
+        for (int r = 0; r < nrows; ++r) {
+          const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
+          const f2v dx = xi - qx, dy = yi - qy;
+          const f2v d2 = dx * dx + dy * dy;
+          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+          band |= (Aa ^ Ma) | (Ab ^ Mb);
+          put_lane(wa0, wa1, Aa, r);
+          put_lane(wb0, wb1, Ab, r);
+          if constexpr (CTRL) {
+            const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+            const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+            band |= (Na ^ NMa) | (Nb ^ NMb);
+            put_lane(na0, na1, Na, r);
+            put_lane(nb0, nb1, Nb, r);
+          }
+          if ((predm >> r) & 1) {  // wave-uniform
+            const float tc = readlane_f(ftcr, r);
+            if (lane == fp) frp = r;
+            put_lane(fca0, fca1, __ballot(d2.x < tc), fp);
+            put_lane(fcb0, fcb1, __ballot(d2.y < tc), fp);
+            ++fp;
+          }
+        }
+      } else
       for (int r = 0; r < nrows; ++r) {
         const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
         const f2v dx = xi - qx, dy = yi - qy;
@@ -1023,16 +1069,13 @@ void flock_step_kernel(StepArgs a) {
           // row lane's candidate test: float32 d2 < tcr covers every agent with r2 < thr
           // (float32 error of d2 at |d| <= sqrt(thr): 2^-23 |d| (Pi + Pj + |d|) +
           // 2^-22 r2, taken x8); none at huge coordinates (those rows go to the rim kNN)
-          float tcr = -1.f;
-          const float th = lane < nrows ? rthr[lane] : 0.f;
-          if (th > 0.f && pu < 1.0e5f) {
-            const double t = th;
-            const double dc = ldexp((static_cast<double>(pu) + 4.0) * (sqrt(t) + 1.0) + t, -20);
-            tcr = static_cast<float>(t + dc);
-            if (static_cast<double>(tcr) < t + dc) tcr = nextafterf(tcr, __builtin_inff());
-          }
+          const float tcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
           unsigned ca0 = 0, ca1 = 0, cb0 = 0, cb1 = 0;
           int p = 0, rp = 0;
+          if (fused) {
+            ca0 = fca0; ca1 = fca1; cb0 = fcb0; cb1 = fcb1;
+            p = fp; rp = frp;
+          } else
           for (uint64_t pm = predm; pm; pm &= pm - 1, ++p) {
             const int r = __builtin_ctzll(pm);
             if (lane == p) rp = r;
