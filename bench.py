@@ -10,6 +10,13 @@ random-init swarms, float32 actions U(-1,1) resident in HBM.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py is its own launcher: the
+parent (which makes no GPU call) checks N against the GPUs it can see, spawns N fresh
+worker processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT set, relays rank 0's JSON line and exits non-zero if any worker fails. Under
+torchrun, WORLD_SIZE must equal --gpus. `--dry-host` runs the same spawn, rendezvous and
+whole-vector reward check with the CPU oracle's rewards and never loads HIP (CPU tests).
+
 At one GPU the same JSON line also carries the other single-GPU configs of
 BASELINE.json as sub-objects: "coverage_config4" (Coverage-v0, R=200, 512 envs) and
 "n8192_config5" (N=8192 x 32 envs), each with ms_per_step, roofline and cpu_baseline;
@@ -120,41 +127,60 @@ def cpu_ref_rate(n_agents, seconds, seed=0, max_steps=100000):
             return n_agents * steps / el, steps, el
 
 
-def cpu_worker(n_agents, seconds, seed):
-    """--cpu-worker: one process of the all-cores baseline (no GPU is touched)."""
+def cpu_worker(n_agents, seconds, seed, pin_core=None):
+    """--cpu-worker: one process of the CPU baseline (no GPU is touched), pinned to one
+    core first when pin_core is given (sched_setaffinity, taskset's system call)."""
+    if pin_core is not None:
+        os.sched_setaffinity(0, {pin_core})
     rate, steps, el = cpu_ref_rate(n_agents, seconds, seed)
-    print(json.dumps({"agent_steps_per_s": rate, "steps": steps, "seconds": el}), flush=True)
+    print(json.dumps({"agent_steps_per_s": rate, "steps": steps, "seconds": el,
+                      "affinity": sorted(os.sched_getaffinity(0))}), flush=True)
 
 
-def cpu_baseline_all_cores(n_agents, seconds, procs):
-    """`procs` independent single-threaded cpu_ref processes at once
-    (child processes, OMP_NUM_THREADS=1), aggregate agent-steps/s."""
+def cpu_workers(n_agents, seconds, cores):
+    """One single-threaded cpu_ref child process per core in `cores`, all at once, each
+    pinned to its core (OMP/BLAS threads 1); returns their results."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(seconds), "--n-agents", str(n_agents)]
-    ps = [subprocess.Popen(cmd + ["--seed", str(k)], stdout=subprocess.PIPE, env=env) for k in range(procs)]
-    rates = []
+    ps = [subprocess.Popen(cmd + ["--seed", str(k), "--pin-core", str(c)], stdout=subprocess.PIPE, env=env)
+          for k, c in enumerate(cores)]
+    res = []
     for p in ps:
         out, _ = p.communicate(timeout=seconds * 10 + 120)
         if p.returncode == 0:
-            rates.append(json.loads(out.decode().strip().splitlines()[-1])["agent_steps_per_s"])
-    return sum(rates), len(rates)
+            res.append(json.loads(out.decode().strip().splitlines()[-1]))
+    return res
 
 
-def flock_cpu_baseline(n_agents, seconds, procs):
-    rate, steps, el = cpu_ref_rate(n_agents, seconds)
+def flock_cpu_baseline(n_agents, seconds, procs=None):
+    """the reference's op sequence (oracle/cpu_ref.py) on one core pinned
+    (per_core), then on every core of the usable CPU share at once, one pinned
+    single-threaded process per core (value = the sum)."""
+    share = cpu_share()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    use = procs or min(share["use"], int(omp) if omp and omp.isdigit() else share["use"])
+    cores = share["cores"][:use] if use <= len(share["cores"]) else list(range(use))
+    one = cpu_workers(n_agents, seconds, cores[:1])
+    if not one:
+        return {"value": None, "unit": "agent-steps/s", "error": "CPU baseline worker failed"}
+    rate, steps, el = one[0]["agent_steps_per_s"], one[0]["steps"], one[0]["seconds"]
     out = {"value": rate, "unit": "agent-steps/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
-           "per_core": rate,
-           "sample": "oracle/cpu_ref.py step() on 1 env of N=%d for %d steps (%.1f s), 1 thread: the reference's "
-                     "own NumPy array-op sequence (flocking_relative.py:91-147), bitwise equal to it and within 15%% "
-                     "of its time (scripts/check_cpu_ref.py, profiles/r02/cpu_ref_check.json); same synthetic init "
-                     "and float32 actions as the GPU run" % (n_agents, steps, el)}
-    if procs > 1:
-        log("cpu baseline, all cores: %d processes x ~%.0fs..." % (procs, seconds / 2))
-        agg, ok = cpu_baseline_all_cores(n_agents, seconds / 2, procs)
-        out.update(value=agg, cores=ok,
-                   sample=out["sample"] + "; value = %d such processes at once (OMP_NUM_THREADS=1 each, %.0f s), "
-                                          "summed; per_core = one process alone" % (ok, seconds / 2))
+           "per_core": rate, "nproc": share["nproc"], "affinity_cpus": share["affinity"],
+           "cgroup_cpu_quota": share["cgroup_quota"], "omp_num_threads": omp,
+           "sample": "oracle/cpu_ref.py step() on 1 env of N=%d for %d steps (%.1f s), 1 thread pinned to core %d: "
+                     "the reference's own NumPy array-op sequence (flocking_relative.py:91-147), bitwise equal to it "
+                     "and within 15%% of its time (scripts/check_cpu_ref.py, profiles/r03/cpu_ref_check.json); same "
+                     "synthetic init and float32 actions as the GPU run" % (n_agents, steps, el, cores[0])}
+    if use > 1:
+        log("cpu baseline, all cores: %d pinned processes x ~%.0fs..." % (use, seconds / 2))
+        res = cpu_workers(n_agents, seconds / 2, cores)
+        out.update(value=sum(r["agent_steps_per_s"] for r in res), cores=len(res),
+                   sample=out["sample"] + "; value = %d such processes at once, one pinned per core of the usable "
+                                          "CPU share (min of nproc=%d, affinity=%d, cgroup quota=%s, "
+                                          "OMP_NUM_THREADS=%s), %.0f s, summed; per_core = one process alone"
+                                          % (len(res), share["nproc"], share["affinity"], share["cgroup_quota"],
+                                             omp, seconds / 2))
     return out
 
 
@@ -170,13 +196,15 @@ class Ranks:
         if self.g is not None:
             self.g.barrier()
 
-    def max(self, v):
-        return v if self.g is None else self.g.max(v)
+    def gather(self, v):
+        """Every rank's value, in rank order."""
+        return [float(v)] if self.g is None else self.g.allgather_f64(v)
 
 
-def timed(env, ranks, k, step):
+def timed(env, ranks, k, step, per_rank=None):
     """k steps bracketed by a barrier + device sync on both sides; returns (max-over-
-    ranks wall seconds, device ms per step from the handle's timing window)."""
+    ranks wall seconds, device ms per step from the handle's timing window). per_rank, if
+    a list, receives every rank's wall seconds."""
     ranks.barrier(env)
     env.h.timing_start(every=TIMING_EVERY)
     t0 = time.perf_counter()
@@ -186,7 +214,10 @@ def timed(env, ranks, k, step):
     el = time.perf_counter() - t0
     kernel_ms, _ = env.h.timing_stop()
     ranks.barrier(env)
-    return ranks.max(el), kernel_ms
+    every = ranks.gather(el)
+    if per_rank is not None:
+        per_rank[:] = every
+    return max(every), kernel_ms
 
 
 def flock_roofline(n, b, kernel_ms, launches_per_step):
@@ -230,25 +261,30 @@ def bench_config5(args):
 
 
 def coverage_cpu_baseline(targets, n_robots, max_nodes, seconds):
-    """The oracle's NumPy Coverage step (one core) on one env of the same workload."""
-    from oracle import coverage as oc
+    """oracle/cpu_ref_coverage.py: the reference's own CoverageEnv.step op sequence
+    (per-robot loops, np.where lookups, list-membership collision test, three R x T
+    closest_targets argmins; coverage.py:174-364, :427-432), checked bitwise against the
+    reference's recorded episodes (tests/test_oracle_coverage.py) and within 15 % of its
+    time (scripts/check_cpu_ref.py), on one env of the same workload, one thread."""
+    from oracle.cpu_ref_coverage import CpuCoverage
     rs = np.random.RandomState(0)
-    o = oc.CoverageOracle(targets, n_robots, max_nodes)
+    env = CpuCoverage(targets, n_robots, max_nodes)
     T = len(targets)
-    o.reset(rs.choice(T, n_robots, replace=False), rs.choice(T, T // 2, replace=False) + n_robots)
-    acts = rs.randint(0, 4, size=(n_robots,))
+    env.reset(rs.choice(T, n_robots, replace=False), rs.choice(T, T // 2, replace=False) + n_robots)
+    acts = rs.randint(0, 4, size=(n_robots, 1))
     steps, t0 = 0, time.perf_counter()
     while True:
-        o.step(acts)
+        env.step(acts)
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds and steps >= 3:
             break
     return {"value": n_robots * steps / el, "unit": "robot-steps/s", "cores": 1, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": "oracle/coverage.py step() (NumPy restatement, 1 thread; NOT the reference's own op sequence: "
-                      "the reference measured 12.36 ms per step at R=200 in the survey container, BASELINE.md §2, "
-                      "slower than this oracle) on 1 env, R=%d, T=%d, %d steps (%.1f s)" % (n_robots, T, steps, el)}
+            "cpu_model": cpu_model(), "ms_per_env_step": 1e3 * el / steps,
+            "sample": "oracle/cpu_ref_coverage.py step() (the reference's own loop/np.where op sequence, "
+                      "coverage.py:174-364; bitwise equal to the reference's recorded episodes and within 15%% of "
+                      "its time, profiles/r03/cpu_ref_check.json) on 1 env, R=%d, T=%d, %d steps (%.1f s), "
+                      "1 thread" % (n_robots, T, steps, el)}
 
 
 def bench_config4(args, with_greedy=False):
@@ -334,6 +370,185 @@ def bench_greedy(v, targets, R, M, B, K, args):
     return out
 
 
+# ------------------------------------------------------------------ multi-rank launch
+def visible_gpus():
+    """GPUs this process could open, counted WITHOUT initialising HIP: KFD topology nodes
+    with SIMDs whose DRM render node is accessible, capped by the *_VISIBLE_DEVICES masks.
+    None when the topology cannot be read (the workers then fail loudly at device open)."""
+    import glob
+    topo = os.environ.get("GYMFLOCK_KFD_TOPOLOGY", "/sys/class/kfd/kfd/topology")  # tests point it elsewhere
+    props = glob.glob(os.path.join(topo, "nodes", "*", "properties"))
+    if not props:
+        return None
+    n = 0
+    for path in props:
+        try:
+            with open(path) as f:
+                kv = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+        except OSError:
+            continue
+        if int(kv.get("simd_count", "0")) <= 0:
+            continue
+        minor = kv.get("drm_render_minor")
+        if minor is not None and not os.access("/dev/dri/renderD%s" % minor, os.R_OK | os.W_OK):
+            continue
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
+def _free_port_pair():
+    """A port P with P and P + 1 free on 127.0.0.1 (MASTER_PORT and the host channel)."""
+    import socket
+    for _ in range(64):
+        a = socket.socket()
+        a.bind(("127.0.0.1", 0))
+        p = a.getsockname()[1]
+        b = socket.socket()
+        try:
+            b.bind(("127.0.0.1", p + 1))
+            return p
+        except OSError:
+            continue
+        finally:
+            a.close()
+            b.close()
+    raise RuntimeError("no free port pair")
+
+
+def launch(args):
+    """--gpus N without WORLD_SIZE: spawn N workers (this script, RANK/LOCAL_RANK/
+    WORLD_SIZE/MASTER_* set), relay rank 0's JSON line; non-zero exit if N exceeds the
+    visible GPUs, if any worker fails or the run outlasts --launch-timeout. The parent
+    never touches the GPU (visible_gpus reads sysfs only)."""
+    import secrets
+    import signal
+    import subprocess
+    import threading
+    n = args.gpus
+    if not args.dry_host:
+        vis = visible_gpus()
+        if vis is not None and n > vis:
+            log("bench.py: --gpus %d but only %d GPU(s) are visible" % (n, vis))
+            return 2
+    port = _free_port_pair()
+    token = secrets.token_hex(16)
+    children = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GYMFLOCK_HOST_TOKEN=token)
+        env.pop("GYMFLOCK_HOST_PORT", None)
+        children.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                         stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                         start_new_session=True))
+    out = []
+    reader = threading.Thread(target=lambda: out.append(children[0].stdout.read()), daemon=True)
+    reader.start()
+    deadline = time.monotonic() + args.launch_timeout
+    failed = None
+    while failed is None:
+        codes = [c.poll() for c in children]
+        bad = ["rank %d exited with %d" % (r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = "; ".join(bad)
+        elif all(c == 0 for c in codes):
+            break
+        elif time.monotonic() > deadline:
+            failed = "timed out after %.0f s" % args.launch_timeout
+        else:
+            time.sleep(0.05)
+    if failed is not None:
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            for c in children:
+                if c.poll() is None:
+                    try:
+                        os.killpg(c.pid, sig)  # the worker's own session (start_new_session)
+                    except ProcessLookupError:
+                        pass
+            t_end = time.monotonic() + 10
+            while time.monotonic() < t_end and any(c.poll() is None for c in children):
+                time.sleep(0.05)
+        log("bench.py launcher: %s; the %d-rank run failed" % (failed, n))
+        return 1
+    reader.join(timeout=30)
+    lines = [ln for ln in (out[0] if out else b"").decode(errors="replace").splitlines() if ln.startswith("{")]
+    if not lines:
+        log("bench.py launcher: rank 0 printed no JSON line")
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+def dry_host(args, world, rank):
+    """--dry-host: the multi-rank path's host side with no GPU and no HIP library: the
+    host-channel rendezvous (token checked), the equal-shard check, K timed steps of the
+    CPU oracle on this rank's envs between barriers, the reward all-gather over the host
+    channel and every rank's whole-vector check. Rank 0 prints a line shaped like the
+    GPU one (n_gpus, per-rank ms, gathered_rewards_ok)."""
+    from gym_flock.hostgroup import HostGroup
+    from gym_flock.init_states import synthetic_state
+    from gym_flock.shard import HostRewardGather, check_equal_shards, check_gathered
+    from oracle import flocking as orc
+    group = HostGroup.from_env(timeout=120.0)
+    ranks = Ranks(group)
+    N, K = args.n_agents, args.steps
+    B = args.n_envs + (1 if args.dry_host_uneven and rank == world - 1 else 0)
+    check_equal_shards(group, B)
+    xs = [synthetic_state(N, rank * B + b) for b in range(B)]
+    us = [np.random.RandomState(10_000 + rank * B + b).uniform(-1, 1, size=(N, 2)).astype(np.float32)
+          for b in range(B)]
+    rew = np.zeros(B)
+
+    def step():
+        for b in range(B):
+            r = orc.step(xs[b], us[b])
+            xs[b], rew[b] = r["x"], r["reward"]
+
+    for _ in range(args.warmup):
+        step()
+    group.barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    el = time.perf_counter() - t0
+    group.barrier()
+    every = ranks.gather(el)
+    gathered = HostRewardGather(group).gather(rew)
+    if args.dry_host_corrupt and rank == 1:
+        gathered[0] += 1e-9
+    _, ok = check_gathered(group, gathered, rew)
+    group.close()
+    if rank == 0:
+        print(json.dumps({"metric": "agent-steps/sec (dry host: CPU oracle, no GPU)", "value": world * B * N * K / max(every),
+                          "unit": "agent-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+                          "ms_per_step": 1e3 * max(every) / K,
+                          "per_rank_ms_per_step": [1e3 * e / K for e in every],
+                          "gathered_rewards_ok": ok, "dry_host": True,
+                          "config": {"n_agents": N, "envs_per_gpu": B, "global_envs": world * B}}), flush=True)
+    if not ok:
+        raise SystemExit("gathered rewards differ from the ranks' local rewards")
+
+
+def cpu_share():
+    """The host CPUs the CPU baseline may use: nproc (os.cpu_count), this process's
+    affinity set, and the cgroup CPU quota; the usable share is the smallest."""
+    nproc = os.cpu_count() or 1
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(nproc))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    use = min([len(aff)] + ([quota] if quota else []))
+    return {"nproc": nproc, "affinity": len(aff), "cgroup_quota": quota, "use": use, "cores": aff[:use]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["flocking", "coverage"], default="flocking")
@@ -349,9 +564,16 @@ def main():
                     help="untimed wall time of steps before the warmup steps (reported)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0,
-                    help="processes of the all-cores CPU baseline (default: OMP_NUM_THREADS or 16, "
-                         "the box's CPU share)")
+                    help="processes of the all-cores CPU baseline (default: the usable CPU share, "
+                         "min(nproc, affinity, cgroup quota), capped by OMP_NUM_THREADS when set)")
     ap.add_argument("--cpu-worker", type=float, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--pin-core", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="seconds the --gpus N launcher waits for its workers")
+    ap.add_argument("--dry-host", action="store_true",
+                    help="multi-rank host path only (spawn, rendezvous, reward check) with the CPU oracle; no GPU")
+    ap.add_argument("--dry-host-uneven", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-host-corrupt", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-controller-line", action="store_true")
     ap.add_argument("--no-packed-line", action="store_true")
@@ -362,14 +584,21 @@ def main():
                     help="use the multi-rank path (host channel + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
     if args.cpu_worker is not None:
-        return cpu_worker(args.n_agents, args.cpu_worker, args.seed)
+        return cpu_worker(args.n_agents, args.cpu_worker, args.seed, args.pin_core)
     if args.workload == "coverage":
         print(json.dumps(dict(bench_config4(args, with_greedy=True), n_gpus=1)), flush=True)
         return
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log("bench.py: WORLD_SIZE=%d but --gpus %d: one rank per GPU is required" % (world, args.gpus))
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_host:
+        return dry_host(args, world, rank)
     multi = world > 1 or args.force_dist
     group = None
     if multi:
@@ -377,7 +606,7 @@ def main():
         group = HostGroup.from_env()
     ranks = Ranks(group)
 
-    from gym_flock.shard import RcclRewardGather, check_gathered
+    from gym_flock.shard import check_gathered, init_rccl_gather
     from gym_flock.vec import VecFlockingRelative
 
     N, B, K, W = args.n_agents, args.n_envs, args.steps, args.warmup
@@ -388,14 +617,13 @@ def main():
     env.set_actions(u)
     gather = None
     if multi:
-        uid = group.broadcast_bytes(env.h.comm_unique_id() if rank == 0 else b"")
         # RCCL prints a version banner on the process's stdout at communicator init; the
         # bench's stdout carries only the JSON line, so fd 1 points at stderr meanwhile
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            gather = RcclRewardGather(env.h, world, rank, uid)
+            gather = init_rccl_gather(group, env.h, world, rank)
         finally:
             os.dup2(saved, 1)
             os.close(saved)
@@ -410,7 +638,8 @@ def main():
     env.set_state(x_init)
     for s in range(W):
         plain(s)
-    elapsed, kernel_ms = timed(env, ranks, K, plain)
+    per_rank = []
+    elapsed, kernel_ms = timed(env, ranks, K, plain, per_rank)
 
     extra = {}
     if gather is not None:
@@ -488,6 +717,7 @@ def main():
             "warmup": W,
             "clock_warmup": warm,
             "ms_per_step": 1e3 * elapsed / K,
+            "per_rank_ms_per_step": [1e3 * e / K for e in per_rank],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -508,8 +738,7 @@ def main():
             line["n8192_config5"] = bench_config5(args)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline (cpu_ref, 1 core, ~%.0fs)..." % args.cpu_seconds)
-            procs = args.cpu_procs or min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
-            line["cpu_baseline"] = flock_cpu_baseline(N, args.cpu_seconds, procs)
+            line["cpu_baseline"] = flock_cpu_baseline(N, args.cpu_seconds, args.cpu_procs or None)
         print(json.dumps(line), flush=True)
     if group is not None:
         group.close()

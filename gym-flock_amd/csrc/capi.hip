@@ -2,12 +2,14 @@
 // stream-ordered launches, host transfers, RCCL metrics path and error reporting.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "flock_internal.h"
@@ -37,6 +39,8 @@ int fail_hip(const char* what, hipError_t e) {
 constexpr int kRewardSlots = 16;
 constexpr int kGatherBlock = 8;
 constexpr int kBlocks = kRewardSlots / kGatherBlock;
+// fe_comm_init's bound on the communicator's creation and its shard-size check
+constexpr double kCommInitTimeoutS = 300.0;
 
 }  // namespace
 
@@ -59,6 +63,8 @@ struct fe_handle {
   int nsplit = 2;                       // launches per step (fe_set_streams)
   bool s2_pending = false;              // stream2 holds work `stream` has not waited for
   bool main_dirty = true;               // `stream` holds work stream2 has not waited for
+  bool dephase = true;                  // the next split step starts the halves apart (other
+                                        // work or a single launch came before it)
   bool other_work = true;               // non-step work was enqueued since the last step:
                                         // the next step goes out as one launch (a split
                                         // step would only wait on it across streams)
@@ -213,6 +219,7 @@ int use_dev(fe_handle* h) {
   if (int rc = join_s2(h)) return rc;
   if (int rc = join_k(h)) return rc;
   h->main_dirty = true;
+  h->dephase = true;
   h->other_work = true;
   return GF_OK;
 }
@@ -419,7 +426,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     const int B = a.B, B0 = (B + 1) / 2;
     const gf::StepArgs a1 = env_range(h, a, B0, B - B0, uf64);
     hipError_t e = hipSuccess;
-    if (h->main_dirty && GF_DEPHASE && B0 >= 2) {
+    if (h->dephase && GF_DEPHASE && B0 >= 2) {
       // both streams idle (the first split step after other work): the second half
       // would start beside the first and the two would run in phase for many steps.
       // The first half's first quarter goes alone, the second half starts after it, and
@@ -429,7 +436,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
       e = gf::launch_step(env_range(h, a, 0, Bq, uf64), dyn, uf64, ctrl, h->stream);
       GF_HIP(hipEventRecord(h->ev_main, h->stream));
       GF_HIP(hipStreamWaitEvent(h->stream2, h->ev_main, 0));
-      h->main_dirty = false;
+      h->main_dirty = h->dephase = false;
       if (e == hipSuccess) e = gf::launch_step(a1, dyn, uf64, ctrl, h->stream2);
       if (e == hipSuccess) e = gf::launch_step(env_range(h, a, Bq, B0 - Bq, uf64), dyn, uf64, ctrl, h->stream);
     } else {
@@ -447,7 +454,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     return GF_OK;
   }
   if (int rc = join_s2(h)) return rc;  // a single launch covers both halves
-  h->main_dirty = true;
+  h->main_dirty = h->dephase = true;
   if (h->timing && h->nsplit > 1) h->tw_steps++;  // the window counts every step
   // a sampled launch is bracketed by two events (which also keep it from overlapping
   // its neighbours, so sampling every launch costs the stream ~7 us per step)
@@ -782,7 +789,8 @@ int fe_step(fe_handle* h, const void* u, int flags) {
     return fail(GF_EINVAL, "null action pointer");
   } else if (flags & FE_U_DEVICE) {
     // the caller may have written the actions on the handle's stream (fe_buffers.stream):
-    // the second half's stream waits for it (an event, no host sync)
+    // the second half's stream waits for it (an event, no host sync); the halves keep
+    // their phase (no de-phasing: that is for the first split step after other work)
     up = u;
     h->main_dirty = true;
   } else {
@@ -1005,8 +1013,10 @@ int fe_sync(fe_handle* h) {
   if (int rc = use_dev(h)) return rc;
   GF_HIP(hipStreamSynchronize(h->stream));
   if (h->comm_stream) GF_HIP(hipStreamSynchronize(h->comm_stream));
-  // both streams are idle now: the next step may split at once (nothing to wait on)
-  h->main_dirty = h->other_work = false;
+  // both streams are idle now: the next step may split at once. main_dirty (set by
+  // use_dev) stays: a zero-copy consumer may enqueue reads of the outputs on `stream`
+  // after this call, and the next step's second half must wait for them
+  h->other_work = false;
   return GF_OK;
 }
 
@@ -1110,25 +1120,100 @@ int fe_comm_unique_id(uint8_t id[128]) {
   return GF_OK;
 }
 
-int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
-  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(GF_EINVAL, "bad argument");
+int fe_check_shard_sizes(int nranks, const int32_t* n_envs) {
+  if (nranks < 1 || !n_envs) return fail(GF_EINVAL, "bad argument");
+  for (int r = 1; r < nranks; ++r)
+    if (n_envs[r] != n_envs[0]) {
+      std::string m = "unequal env shards over ranks (the reward all-gather needs one count per rank): n_envs =";
+      for (int q = 0; q < nranks; ++q) m += " " + std::to_string(n_envs[q]);
+      return fail(GF_ECOMM, m);
+    }
+  return GF_OK;
+}
+
+namespace {
+// A non-blocking communicator's pending work: poll its async error until it leaves
+// ncclInProgress or the deadline passes (then abort it, so no rank waits forever on a
+// peer that never joined or died).
+int comm_wait(fe_handle* h, std::chrono::steady_clock::time_point deadline, const char* what) {
+  for (;;) {
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
+    if (r != ncclSuccess) st = r;
+    if (st == ncclSuccess) return GF_OK;
+    if (st != ncclInProgress || std::chrono::steady_clock::now() > deadline) {
+      ncclCommAbort(h->comm);
+      h->comm = nullptr;
+      if (st != ncclInProgress) return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(st));
+      return fail(GF_ECOMM, std::string(what) + ": timed out (a rank did not join or stopped responding)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+}  // namespace
+
+int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[128], double timeout_s) {
+  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks || !(timeout_s > 0)) return fail(GF_EINVAL, "bad argument");
   if (h->comm) return fail(GF_ESTATE, "communicator already initialised");
   if (int rc = use_dev(h)) return rc;
+  const auto deadline = std::chrono::steady_clock::now() +
+                        std::chrono::microseconds((int64_t)(timeout_s * 1e6));
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
-  ncclResult_t r = ncclCommInitRank(&h->comm, nranks, uid, rank);
-  if (r != ncclSuccess) {
+  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+  config.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&h->comm, nranks, uid, rank, &config);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (h->comm) ncclCommAbort(h->comm);
     h->comm = nullptr;
-    return fail(GF_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    return fail(GF_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  }
+  if (int rc = comm_wait(h, deadline, "ncclCommInitRankConfig")) return rc;
+  GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
+  // every rank's shard size, before any reward all-gather relies on them being equal
+  int32_t* dsz = nullptr;
+  if (int rc = dalloc(&dsz, (size_t)nranks)) return rc;
+  std::vector<int32_t> sizes(nranks);
+  const int32_t mine = h->cfg.n_envs;
+  GF_HIP(hipMemcpyAsync(dsz + rank, &mine, 4, hipMemcpyHostToDevice, h->comm_stream));
+  r = ncclAllGather(dsz + rank, dsz, 1, ncclInt32, h->comm, h->comm_stream);
+  int rc = (r == ncclSuccess || r == ncclInProgress) ? comm_wait(h, deadline, "shard-size all-gather")
+                                                     : fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  if (rc == GF_OK) {
+    hipError_t q;
+    while ((q = hipStreamQuery(h->comm_stream)) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() > deadline) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (q == hipErrorNotReady) {
+      ncclCommAbort(h->comm);
+      h->comm = nullptr;
+      rc = fail(GF_ECOMM, "shard-size all-gather: timed out (a rank stopped responding)");
+    } else if (q != hipSuccess) {
+      rc = fail(GF_EHIP, std::string("shard-size all-gather: ") + hipGetErrorString(q));
+    } else if (hipMemcpy(sizes.data(), dsz, 4 * (size_t)nranks, hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = fail(GF_EHIP, "shard-size copy");
+    } else {
+      rc = fe_check_shard_sizes(nranks, sizes.data());
+    }
+  }
+  hipFree(dsz);
+  if (rc != GF_OK) {
+    if (h->comm) ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+    return rc;
   }
   h->nranks = nranks;
   h->rank = rank;
-  GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
   GF_HIP(hipEventCreateWithFlags(&h->step_ev, hipEventDisableTiming));
   GF_HIP(hipEventCreateWithFlags(&h->step_ev2, hipEventDisableTiming));
   for (auto& e : h->ag_ev) GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (int rc = dalloc(&h->gather, (size_t)kBlocks * nranks * kGatherBlock * h->cfg.n_envs)) return rc;
+  if (int rc2 = dalloc(&h->gather, (size_t)kBlocks * nranks * kGatherBlock * h->cfg.n_envs)) return rc2;
   return GF_OK;
+}
+
+int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
+  return fe_comm_init_timeout(h, nranks, rank, id, kCommInitTimeoutS);
 }
 
 int fe_allgather_rewards(fe_handle* h) {
@@ -1151,7 +1236,13 @@ int fe_allgather_rewards(fe_handle* h) {
     GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev2, 0));
   }
   ncclResult_t r = ncclAllGather(src, dst, (size_t)count * B, ncclFloat64, h->comm, h->comm_stream);
-  if (r != ncclSuccess) return fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  if (r == ncclInProgress) {  // the communicator is non-blocking: wait until it is enqueued
+    if (int rc = comm_wait(h, std::chrono::steady_clock::now() + std::chrono::seconds((int)kCommInitTimeoutS),
+                           "ncclAllGather"))
+      return rc;
+  } else if (r != ncclSuccess) {
+    return fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  }
   GF_HIP(hipEventRecord(h->ag_ev[blk], h->comm_stream));
   h->ag_pending[blk] = true;
   h->last_gather = blk;

@@ -721,7 +721,10 @@ int cov_sync(cov_handle* h) {
   if (!h) return cfail(GF_EINVAL, "null handle");
   if (int rc = use(h)) return rc;
   CV_HIP(hipStreamSynchronize(h->stream));
-  h->main_dirty = h->other_work = false;  // both streams idle: the next step may split
+  // both streams idle: the next step may split. main_dirty stays set (use_dev): reads of
+  // the outputs a zero-copy consumer enqueues on `stream` after this call come before
+  // the next step's second half
+  h->other_work = false;
   return check_err(h);
 }
 

@@ -100,6 +100,8 @@ SIGNATURES = {
     "fe_join": [_P],
     "fe_comm_unique_id": [_P],
     "fe_comm_init": [_P, _I, _I, _P],
+    "fe_comm_init_timeout": [_P, _I, _I, _P, ctypes.c_double],
+    "fe_check_shard_sizes": [_I, _P],
     "fe_allgather_rewards": [_P],
     "fe_get_gathered_rewards": [_P, _P],
     "fe_gathered_steps": [_P],
@@ -175,6 +177,12 @@ def load(path=None):
 def check(rc):
     if rc != GF_OK:
         raise GymFlockError(rc, load().fe_last_error().decode(errors="replace"))
+
+
+def check_shard_sizes(n_envs):
+    """fe_comm_init's shard-size rule on a list of per-rank env counts (host only)."""
+    a = np.ascontiguousarray(n_envs, dtype=np.int32)
+    check(load().fe_check_shard_sizes(len(a), a.ctypes.data_as(ctypes.c_void_p)))
 
 
 def ptr(a):
@@ -384,9 +392,12 @@ class FlockHandle:
         check(load().fe_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
         return bytes(buf)
 
-    def comm_init(self, nranks, rank, uid):
+    def comm_init(self, nranks, rank, uid, timeout=300.0):
+        """RCCL communicator for the reward all-gather: bounded by `timeout` seconds, and
+        rejected (GF_ECOMM) unless every rank holds the same number of envs."""
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
-        check(self.lib.fe_comm_init(self.h, int(nranks), int(rank), ctypes.cast(buf, ctypes.c_void_p)))
+        check(self.lib.fe_comm_init_timeout(self.h, int(nranks), int(rank), ctypes.cast(buf, ctypes.c_void_p),
+                                            float(timeout)))
         self.nranks = int(nranks)
 
     def allgather_rewards(self):

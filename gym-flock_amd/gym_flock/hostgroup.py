@@ -12,15 +12,21 @@ Topology: a star. Rank 0 listens on (MASTER_ADDR, port) and relays; every other 
 connects to it. Every operation is collective (all ranks call it in the same order).
 Launchers: torchrun (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment;
 torchrun's own store holds MASTER_PORT, so the default port is MASTER_PORT + 1, or
-GYMFLOCK_HOST_PORT), or explicit arguments.
+GYMFLOCK_HOST_PORT), bench.py's own launcher, or explicit arguments.
+
+Messages are raw bytes or fixed-format struct values (float64, int64, bool); nothing
+received is ever unpickled or evaluated. A shared token (GYMFLOCK_HOST_TOKEN, set by
+bench.py's launcher) must accompany every rank's hello, so a stray local process that
+reaches rank 0's port during the rendezvous is refused.
 """
+import hmac
 import os
-import pickle
 import socket
 import struct
 import time
 
 _HDR = struct.Struct("!Q")
+_TOKEN_LEN = 32
 
 
 def _send(sock, payload):
@@ -47,8 +53,9 @@ class HostGroup:
     """rank, world: this process's rank and the number of ranks. addr, port: rank 0's
     listening address. timeout: seconds to wait for the rendezvous and for each op."""
 
-    def __init__(self, rank, world, addr="127.0.0.1", port=29501, timeout=300.0):
+    def __init__(self, rank, world, addr="127.0.0.1", port=29501, timeout=300.0, token=b""):
         self.rank, self.world = int(rank), int(world)
+        token = (bytes(token) + bytes(_TOKEN_LEN))[:_TOKEN_LEN]
         if not (0 <= self.rank < self.world):
             raise ValueError("rank out of range")
         self.peers = {}  # rank 0: rank -> socket
@@ -67,7 +74,11 @@ class HostGroup:
                     c, _ = srv.accept()
                     c.settimeout(timeout)
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    (r,) = struct.unpack("!I", _recv_exact(c, 4))
+                    hello = _recv_exact(c, 4 + _TOKEN_LEN)
+                    (r,) = struct.unpack("!I", hello[:4])
+                    if not hmac.compare_digest(hello[4:], token):
+                        c.close()
+                        raise RuntimeError("hostgroup: a peer presented the wrong token in the rendezvous")
                     if not (0 < r < self.world) or r in self.peers:
                         c.close()
                         raise RuntimeError("hostgroup: unexpected rank %d in rendezvous" % r)
@@ -85,7 +96,7 @@ class HostGroup:
                     time.sleep(0.1)
             s.settimeout(timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            s.sendall(struct.pack("!I", self.rank))
+            s.sendall(struct.pack("!I", self.rank) + token)
             self.up = s
 
     @classmethod
@@ -95,7 +106,8 @@ class HostGroup:
         rank = int(os.environ.get("RANK", "0"))
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("GYMFLOCK_HOST_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
-        return cls(rank, world, addr, port, timeout)
+        token = bytes.fromhex(os.environ.get("GYMFLOCK_HOST_TOKEN", ""))
+        return cls(rank, world, addr, port, timeout, token)
 
     # ---------------------------------------------------------------- collectives
     def allgather_bytes(self, payload):
@@ -118,9 +130,23 @@ class HostGroup:
             off += n
         return parts
 
-    def allgather(self, obj):
-        """allgather_bytes of pickled objects (this group's own messages only)."""
-        return [pickle.loads(p) for p in self.allgather_bytes(pickle.dumps(obj))]
+    def _allgather_struct(self, fmt, value):
+        st = struct.Struct(fmt)
+        out = []
+        for p in self.allgather_bytes(st.pack(value)):
+            if len(p) != st.size:
+                raise RuntimeError("hostgroup: malformed %r message (%d bytes)" % (fmt, len(p)))
+            out.append(st.unpack(p)[0])
+        return out
+
+    def allgather_f64(self, value):
+        return self._allgather_struct("!d", float(value))
+
+    def allgather_i64(self, value):
+        return self._allgather_struct("!q", int(value))
+
+    def allgather_bool(self, value):
+        return self._allgather_struct("!?", bool(value))
 
     def barrier(self):
         self.allgather_bytes(b"")
@@ -129,7 +155,7 @@ class HostGroup:
         return self.allgather_bytes(payload if self.rank == src else b"")[src]
 
     def max(self, value):
-        return max(self.allgather(float(value)))
+        return max(self.allgather_f64(value))
 
     def close(self):
         for s in list(self.peers.values()) + ([self.up] if self.up else []):

@@ -37,9 +37,9 @@ class RcclRewardGather:
     current 8-step block (call it every 8 steps to ship each step's rewards once);
     result() returns them as (steps, world * B) in global env order."""
 
-    def __init__(self, handle, world_size, rank, unique_id):
+    def __init__(self, handle, world_size, rank, unique_id, timeout=300.0):
         self.handle = handle
-        handle.comm_init(world_size, rank, unique_id)
+        handle.comm_init(world_size, rank, unique_id, timeout)
 
     def issue(self):
         self.handle.allgather_rewards()
@@ -47,6 +47,38 @@ class RcclRewardGather:
     def result(self):
         g = self.handle.gathered_rewards()  # (world, steps, B)
         return np.concatenate(list(g), axis=1)
+
+
+def check_equal_shards(group, n_envs):
+    """Every rank's env count over the host channel; raises on every rank unless they are
+    equal (the RCCL reward all-gather ships one count per rank; fe_comm_init checks the
+    same on the device). Returns the per-rank counts."""
+    sizes = group.allgather_i64(int(n_envs))
+    if len(set(sizes)) != 1:
+        raise RuntimeError("unequal env shards over ranks: n_envs per rank = %s (the reward all-gather "
+                           "needs the same count on every rank)" % sizes)
+    return sizes
+
+
+def init_rccl_gather(group, handle, world, rank, timeout=300.0):
+    """The multi-rank path's RCCL setup, bounded by the host channel: the ranks' shard
+    sizes are compared first; rank 0's unique id goes out only once every rank has joined
+    the channel (HostGroup's rendezvous); each rank's bounded communicator init
+    (fe_comm_init_timeout) reports success over the channel, and every rank raises if any
+    rank failed, instead of leaving the others in RCCL. Returns an RcclRewardGather."""
+    check_equal_shards(group, handle.n_envs)
+    uid = group.broadcast_bytes(handle.comm_unique_id() if rank == 0 else b"")
+    err = None
+    try:
+        gather = RcclRewardGather(handle, world, rank, uid, timeout)
+    except Exception as e:  # reported to every rank below, then re-raised here
+        err, gather = e, None
+    ok = group.allgather_bool(err is None)
+    if err is not None:
+        raise err
+    if not all(ok):
+        raise RuntimeError("RCCL communicator init failed on rank(s) %s" % [r for r, v in enumerate(ok) if not v])
+    return gather
 
 
 class HostRewardGather:
@@ -67,7 +99,7 @@ def check_gathered(group, gathered, local_rewards):
     want = HostRewardGather(group).gather(local_rewards)
     got = np.asarray(gathered, dtype=np.float64).ravel()
     ok = bool(got.shape == want.shape and np.array_equal(got, want))
-    return ok, all(group.allgather(ok))
+    return ok, all(group.allgather_bool(ok))
 
 
 class GlooRewardGather:

@@ -168,7 +168,16 @@ int fe_set_dt(fe_handle* h, const double* dt);
  * step path has no exchange. Only per-env rewards are all-gathered, on a side
  * stream, so the collective never sits on the step critical path. */
 int fe_comm_unique_id(uint8_t id[128]);
+/* Creates the communicator (non-blocking RCCL init, polled), then all-gathers every
+ * rank's n_envs and fails with GF_ECOMM unless they are equal (the reward all-gather
+ * ships one count per rank). A rank that never joins, or stops responding, makes every
+ * other rank's call return GF_ECOMM after the timeout (fe_comm_init: 300 s) instead of
+ * hanging; the communicator is then aborted. */
 int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]);
+int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[128], double timeout_s);
+/* The shard-size rule fe_comm_init applies to the gathered sizes: GF_OK when every
+ * n_envs[r] (r < nranks) is equal, else GF_ECOMM naming them. Host-only (no device). */
+int fe_check_shard_sizes(int nranks, const int32_t* n_envs);
 /* Enqueue (side stream, after the latest step) an all-gather of the per-env rewards of
  * the steps since the start of the current 8-step block: one collective per 8 steps
  * carries every step's rewards. */

@@ -7,7 +7,11 @@ from the same synthetic state and float32 actions:
     FlockingRelativeEnv and of CpuFlock must be bitwise equal (same array operations);
   * time: step() and step()+controller() of both, interleaved, best of several rounds,
     one thread; CpuFlock must be within +-15 % of the reference.
-Writes the result to profiles/r02/cpu_ref_check.json.
+Coverage (config 4: R=200 robots, the map of global seed 8, max_nodes 1000): the
+reference's CoverageEnv and oracle/cpu_ref_coverage.CpuCoverage from the same starts,
+unvisited set and random actions: every step's observation, reward and done bitwise
+equal, and the step time within +-15 %.
+Writes the result to profiles/r03/cpu_ref_check.json.
 
   OMP_NUM_THREADS=1 python scripts/check_cpu_ref.py
 """
@@ -35,6 +39,42 @@ def ref_env(x, n):
     env.params_from_cfg(mg._Cfg(comm_radius=0.9, n_agents=n, v_max=5.0, dt=0.01))
     env.x = np.array(x, dtype=np.float64)
     return env
+
+
+def coverage_case(rounds=3, steps=30):
+    import importlib
+    from oracle.cpu_ref_coverage import CpuCoverage
+    mg._install_shims()
+    cov = importlib.import_module("gym_flock.envs.spatial.coverage")
+    R, M = 200, 1000
+    np.random.seed(8)
+    ref = cov.CoverageEnv(n_robots=R, nearby_starts=False, max_nodes=M)
+    ref.seed(9)
+    np.random.seed(8)
+    ref.reset()
+    T = ref.n_targets
+    ours = CpuCoverage(ref.x[R:, :2], R, M)
+    start = ref.closest_targets - R
+    ours.reset(start, np.nonzero(ref.visited[:, 0] == 0)[0])
+    rs = np.random.RandomState(7)
+    acts = [rs.randint(0, 4, size=(R, 1)) for _ in range(steps)]
+    same = True
+    for a in acts[:10]:
+        o1, r1, d1, _ = ref.step(a)
+        o2, r2, d2, _ = ours.step(a)
+        same &= bool(r1 == r2 and d1 == d2 and np.array_equal(ref.x, ours.x) and
+                     all(np.array_equal(o1[k], o2[k]) for k in ref.keys))
+    t = {"ref_step": [], "ours_step": []}
+    for _ in range(rounds):
+        for name, env in (("ref", ref), ("ours", ours)):
+            t0 = time.perf_counter()
+            for a in acts:
+                env.step(a)
+            t[name + "_step"].append((time.perf_counter() - t0) / steps)
+    best = {k: 1e3 * min(v) for k, v in t.items()}
+    ratio = best["ours_step"] / best["ref_step"]
+    return {"workload": "Coverage-v0 R=%d T=%d max_nodes %d" % (R, T, M), "bitwise_equal": bool(same), "ms": best,
+            "ratio_step": ratio, "within_15pct": bool(abs(ratio - 1) <= 0.15)}
 
 
 def main():
@@ -71,9 +111,13 @@ def main():
         ok &= case["bitwise_equal"] and case["within_15pct"]
         out["cases"].append(case)
         print(json.dumps(case))
+    case = coverage_case()
+    ok &= case["bitwise_equal"] and case["within_15pct"]
+    out["cases"].append(case)
+    print(json.dumps(case))
     out["ok"] = bool(ok)
-    os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "r02", "cpu_ref_check.json"), "w") as f:
+    os.makedirs(os.path.join(ROOT, "profiles", "r03"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "r03", "cpu_ref_check.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("ok" if ok else "FAILED")
     return 0 if ok else 1

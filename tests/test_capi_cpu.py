@@ -180,3 +180,17 @@ def test_reference_module_paths_import():
         assert callable(getattr(u, fn))
     p = np.arange(6.0).reshape(3, 2)
     assert u._get_pos_diff(p).shape == (3, 3, 2) and u._get_pos_diff(p, p[:2]).shape == (3, 2, 2)
+
+
+def test_unequal_shards_rejected_by_comm_rule():
+    """fe_comm_init all-gathers every rank's n_envs and applies fe_check_shard_sizes:
+    unequal shards (which would make ncclAllGather's counts disagree: a hang or corrupt
+    gather) are GF_ECOMM; equal ones pass. The rule itself runs on the host."""
+    from gym_flock import _native as nat
+    nat.check_shard_sizes([256] * 8)
+    nat.check_shard_sizes([3])
+    for bad in ([256, 255], [4, 4, 4, 0], [1, 2, 3, 4, 5, 6, 7, 8]):
+        with pytest.raises(nat.GymFlockError) as e:
+            nat.check_shard_sizes(bad)
+        assert e.value.code == nat.GF_ECOMM
+        assert "unequal env shards" in str(e.value)

@@ -253,9 +253,15 @@ def test_env_api_reset_matches_reference_fixture():
 def test_flocking_v0_env_api():
     import gym_flock
 
+    class Cfg:  # params_from_cfg scales r_max by sqrt(N) (:75), so reset() accepts quickly
+        def getfloat(self, k):
+            return {"comm_radius": 0.9, "v_max": 5.0, "dt": 0.01}[k]
+
+        def getint(self, k):
+            return 100
+
     env = gym_flock.make("Flocking-v0")
-    env.n_agents = 100
-    env._make_spaces()
+    env.params_from_cfg(Cfg())
     np.random.seed(3)
     obs, net = env.reset()
     assert obs.shape == (100, 28) and net.shape == (100, 100)

@@ -102,3 +102,41 @@ def test_eight_ranks_rendezvous_and_whole_vector_check():
         assert tmax == world - 0.5
         assert mine and every and not imported_torch
         np.testing.assert_array_equal(gathered, want)
+
+
+@pytest.mark.timeout(60)
+def test_rendezvous_refuses_wrong_token():
+    """A process that reaches rank 0's port with the wrong token is refused (bench.py's
+    launcher sets GYMFLOCK_HOST_TOKEN); nothing it sends is ever unpickled."""
+    import struct
+    import threading
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-flock_amd")]
+    from gym_flock.hostgroup import HostGroup
+    port = _free_port()
+    err = []
+
+    def rank0():
+        try:
+            HostGroup(0, 2, "127.0.0.1", port, timeout=20, token=b"k" * 32)
+        except Exception as e:  # noqa: BLE001
+            err.append(e)
+
+    t = threading.Thread(target=rank0)
+    t.start()
+    for _ in range(100):
+        try:
+            s = socket.create_connection(("127.0.0.1", port), timeout=5)
+            break
+        except OSError:
+            import time
+            time.sleep(0.05)
+    s.sendall(struct.pack("!I", 1) + b"x" * 32)
+    t.join(timeout=30)
+    s.close()
+    assert err and "wrong token" in str(err[0])
+
+
+def test_struct_messages_only():
+    """The group's typed gathers are fixed-format struct values (no pickle anywhere)."""
+    src = open(os.path.join(ROOT, "gym-flock_amd", "gym_flock", "hostgroup.py")).read()
+    assert "import pickle" not in src and "pickle.loads" not in src and "eval(" not in src

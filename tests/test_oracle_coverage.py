@@ -97,3 +97,25 @@ def test_flatten_and_unpack_round_trip():
     np.testing.assert_array_equal(u["senders"][:valid.sum()], obs["senders"][valid])
     np.testing.assert_array_equal(u["senders"][valid.sum():], obs["senders"] + M)
     assert u["globs"][0, 0] == obs["step"][0, 0]
+
+
+@pytest.mark.parametrize("path", EPISODES, ids=os.path.basename)
+def test_cpu_ref_coverage_matches_reference(path):
+    """oracle/cpu_ref_coverage.py (bench.py's config-4 CPU baseline, the reference's own
+    loop-and-np.where op sequence) reproduces the recorded episodes bit for bit."""
+    from oracle.cpu_ref_coverage import CpuCoverage
+    f = np.load(path)
+    R = int(f["n_robots"])
+    env = CpuCoverage(f["targets"], R, int(f["max_nodes"]))
+    np.testing.assert_array_equal(env.motion_edges[0], f["motion_senders"])
+    np.testing.assert_array_equal(env.motion_edges[1], f["motion_receivers"])
+    start = oc.closest_targets(f["x0"][:R], f["targets"], R) - R
+    obs = env.reset(start, np.nonzero(f["visited0"] == 0)[0])
+    check_obs(obs, f)
+    np.testing.assert_array_equal(env.x, f["x0"])
+    for t in range(len(f["actions"])):
+        obs, r, d, _ = env.step(np.array(f["actions"][t]).reshape(-1, 1))
+        np.testing.assert_array_equal(env.x[:R], f["xr"][t])
+        assert r == f["reward"][t] and d == f["done"][t]
+        check_obs(obs, f, t)
+        np.testing.assert_array_equal(env.visited[:, 0].astype(np.int8), f["visited"][t])
