@@ -137,13 +137,14 @@ def cpu_worker(n_agents, seconds, seed, pin_core=None):
                       "affinity": sorted(os.sched_getaffinity(0))}), flush=True)
 
 
-def cpu_workers(n_agents, seconds, cores):
-    """One single-threaded cpu_ref child process per core in `cores`, all at once, each
-    pinned to its core (OMP/BLAS threads 1); returns their results."""
+def cpu_workers(n_agents, seconds, cores, pin=True):
+    """One single-threaded cpu_ref child process per entry of `cores`, all at once (OMP/BLAS
+    threads 1), each pinned to its core when `pin`; returns their results."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(seconds), "--n-agents", str(n_agents)]
-    ps = [subprocess.Popen(cmd + ["--seed", str(k), "--pin-core", str(c)], stdout=subprocess.PIPE, env=env)
+    ps = [subprocess.Popen(cmd + ["--seed", str(k)] + (["--pin-core", str(c)] if pin else []),
+                           stdout=subprocess.PIPE, env=env)
           for k, c in enumerate(cores)]
     res = []
     for p in ps:
@@ -155,8 +156,11 @@ def cpu_workers(n_agents, seconds, cores):
 
 def flock_cpu_baseline(n_agents, seconds, procs=None):
     """the reference's op sequence (oracle/cpu_ref.py) on one core pinned
-    (per_core), then on every core of the usable CPU share at once, one pinned
-    single-threaded process per core (value = the sum)."""
+    (per_core), then on every core of the usable CPU share at once, one single-threaded
+    process per core (value = the sum). The all-cores processes are not pinned: on the
+    GPU box the cgroup grants a 16-CPU share of a 256-CPU host whose other tenants run on
+    fixed cores; 16 processes pinned to the first 16 affinity cores measured 9.1e4 against
+    2.6e5 left to the scheduler (profiles/r03)."""
     share = cpu_share()
     omp = os.environ.get("OMP_NUM_THREADS")
     use = procs or min(share["use"], int(omp) if omp and omp.isdigit() else share["use"])
@@ -173,12 +177,13 @@ def flock_cpu_baseline(n_agents, seconds, procs=None):
                      "and within 15%% of its time (scripts/check_cpu_ref.py, profiles/r03/cpu_ref_check.json); same "
                      "synthetic init and float32 actions as the GPU run" % (n_agents, steps, el, cores[0])}
     if use > 1:
-        log("cpu baseline, all cores: %d pinned processes x ~%.0fs..." % (use, seconds / 2))
-        res = cpu_workers(n_agents, seconds / 2, cores)
+        log("cpu baseline, all cores: %d processes x ~%.0fs..." % (use, seconds / 2))
+        res = cpu_workers(n_agents, seconds / 2, cores, pin=False)
         out.update(value=sum(r["agent_steps_per_s"] for r in res), cores=len(res),
-                   sample=out["sample"] + "; value = %d such processes at once, one pinned per core of the usable "
-                                          "CPU share (min of nproc=%d, affinity=%d, cgroup quota=%s, "
-                                          "OMP_NUM_THREADS=%s), %.0f s, summed; per_core = one process alone"
+                   sample=out["sample"] + "; value = %d such processes at once (unpinned, within the cgroup's "
+                                          "CPU share), one per CPU of the usable share (min of nproc=%d, "
+                                          "affinity=%d, cgroup quota=%s, OMP_NUM_THREADS=%s), %.0f s, summed; "
+                                          "per_core = one process alone, pinned"
                                           % (len(res), share["nproc"], share["affinity"], share["cgroup_quota"],
                                              omp, seconds / 2))
     return out
@@ -330,6 +335,65 @@ def bench_config4(args, with_greedy=False):
     if with_greedy:
         out["greedy_expert"] = bench_greedy(v, targets, R, M, B, K, args)
     v.close()
+    return out
+
+
+def bench_dropin(args):
+    """The drop-in single-env path existing GNN trainers call (flocking_relative.py:91-109,
+    :194-212): FlockingRelativeEnv.step(u) with host actions in and host
+    (state_values, network), reward out, one env per object, plus controller() each
+    iteration (u = env.controller(); env.step(u), the expert loop). Per-call wall time at
+    N=100 and N=1024 for each way of fetching the outputs ("getters": three synchronous
+    getters; "batched": one fe_get_outputs call and one sync into fresh numpy arrays;
+    "pooled": the same call into page-locked arrays from the env's HostPool), with the reference's op sequence (oracle/cpu_ref.py) timed
+    beside it on one core."""
+    from gym_flock.envs.flocking.flocking_relative import FlockingRelativeEnv
+    from gym_flock.init_states import synthetic_state
+    from oracle.cpu_ref import CpuFlock
+    out = {}
+    for n, iters in ((100, 400), (1024, 100)):
+        x0 = synthetic_state(n, 0)
+        u32 = np.random.RandomState(5).uniform(-1, 1, size=(n, 2)).astype(np.float32)
+        row = {}
+        for mode in ("getters", "batched", "pooled"):
+            env = FlockingRelativeEnv()
+            env.n_agents = n
+            env._make_spaces()
+            env.fetch_mode = mode
+            env.x = x0
+            env.compute_helpers()
+
+            def expert(k):
+                for _ in range(k):
+                    env.step(env.controller())
+
+            def plain(k):
+                for _ in range(k):
+                    env.step(u32)
+
+            r = {}
+            for name, fn in (("step_ms", plain), ("controller_plus_step_ms", expert)):
+                fn(20)
+                t0 = time.perf_counter()
+                fn(iters)
+                r[name] = 1e3 * (time.perf_counter() - t0) / iters
+            env.close()
+            row[mode] = r
+        cpu = CpuFlock(x0)
+        k = 200 if n <= 100 else 3
+        t0 = time.perf_counter()
+        for _ in range(k):
+            cpu.step(u32)
+        t_step = (time.perf_counter() - t0) / k
+        t0 = time.perf_counter()
+        for _ in range(k):
+            cpu.step(cpu.controller())
+        t_ctrl = (time.perf_counter() - t0) / k
+        row["cpu_ref_1core"] = {"step_ms": 1e3 * t_step, "controller_plus_step_ms": 1e3 * t_ctrl}
+        out["n%d" % n] = row
+    out["note"] = ("one env per FlockingRelativeEnv object, float32 host actions for step_ms, float64 controller() "
+                   "output for controller_plus_step_ms; outputs copied to fresh host arrays every call, as the "
+                   "reference returns them; the env default is fetch_mode='pooled'")
     return out
 
 
@@ -736,6 +800,8 @@ def main():
             line["coverage_config4"] = bench_config4(args)
             log("config 5 (N=8192 x 32)...")
             line["n8192_config5"] = bench_config5(args)
+            log("drop-in single-env path (N=100, 1024)...")
+            line["dropin"] = bench_dropin(args)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline (cpu_ref, 1 core, ~%.0fs)..." % args.cpu_seconds)
             line["cpu_baseline"] = flock_cpu_baseline(N, args.cpu_seconds, args.cpu_procs or None)

@@ -77,6 +77,7 @@ struct fe_handle {
   int ccur = 0;
   float* sv = nullptr;
   float* net = nullptr;
+  uint64_t* adj_global = nullptr;       // (B,N,Wn) the step's adjacency scratch (wide envs)
   double* reward_ring = nullptr;        // kRewardSlots x B
   int rslot = 0;
   // kNN outputs, one pair per state buffer: knn_idx[i] / knn_obs[i] belong to x[i], so
@@ -131,23 +132,18 @@ struct fe_handle {
   // step t and beside step t+1. A step that writes the state buffer x[i] (or a bits
   // buffer) an unfinished kNN reads waits for that kNN's event first; every other API
   // call joins kstream into `stream` (use_dev).
-  // After a split step the rim kNN goes out as two launches too: envs [0, B0) on
-  // kstream after `stream`'s half, [B0, B) on kstream2 after stream2's, and each half
-  // of the step after next waits only for its own. One kNN launch after both halves
-  // joined them every step (the step after next waited for it on both streams), so the
-  // halves never drifted out of phase (Flocking-v0).
-  hipStream_t kstream = nullptr, kstream2 = nullptr;
+  // The fused step's rim kNN (mode 2) is not on kstream: after a split step it goes out
+  // as two launches on the step streams themselves, envs [0, B0) behind `stream`'s half
+  // and [B0, B) behind stream2's, so each half of the next step follows its own rim by
+  // stream order and the halves keep drifting out of phase (Flocking-v0).
+  hipStream_t kstream = nullptr;
   hipEvent_t ev_kin[2] = {nullptr, nullptr};  // stream / stream2 -> kstream
   hipEvent_t ev_kjoin = nullptr;              // kstream -> stream
-  hipEvent_t ev_kjoin2 = nullptr;             // kstream2 -> stream
   bool k_pending = false;                     // kstream holds work `stream` has not waited for
-  bool k2_pending = false;                    // likewise kstream2
   int last_b0 = 0;                            // B0 of the last launch if it was split, else 0
   struct KnnReader {
-    hipEvent_t ev = nullptr;                  // the kNN launch (envs [0, B0) if split)
-    hipEvent_t ev2 = nullptr;                 // split: the launch of envs [B0, B) on kstream2
+    hipEvent_t ev = nullptr;                  // the kNN launch on kstream
     bool live = false;
-    bool split = false;
     unsigned bmask = 0;                       // bits buffers it reads
   } kread[2];                                 // by the state buffer x[i] the kNN reads
 };
@@ -172,11 +168,6 @@ int join_k(fe_handle* h) {
     GF_HIP(hipStreamWaitEvent(h->stream, h->ev_kjoin, 0));
     h->k_pending = false;
   }
-  if (h->k2_pending) {
-    GF_HIP(hipEventRecord(h->ev_kjoin2, h->kstream2));
-    GF_HIP(hipStreamWaitEvent(h->stream, h->ev_kjoin2, 0));
-    h->k2_pending = false;
-  }
   for (auto& r : h->kread) r.live = false, r.bmask = 0;
   return GF_OK;
 }
@@ -185,26 +176,15 @@ int join_k(fe_handle* h) {
 bool split_next(const fe_handle* h, int B) { return h->nsplit > 1 && B >= 2 && h->stream2 && !h->other_work; }
 
 // Before a step writes x[xw] (xw < 0: no state write) and bits buffer bw (bw < 0: none):
-// both step streams wait for the unfinished kNN launches that read them. A kNN split like
-// the step that follows (same halves) orders each half after its own launch only.
+// both step streams wait for the unfinished kNN launch (on kstream) that reads them. The
+// fused step's rim kNN runs on the step streams and needs no wait.
 int wait_knn_readers(fe_handle* h, int xw, int bw) {
-  const bool halves = split_next(h, h->cfg.n_envs);
   for (int i = 0; i < 2; ++i) {
     auto& r = h->kread[i];
     if (r.live && (i == xw || (bw >= 0 && ((r.bmask >> bw) & 1u)))) {
-      if (r.split && halves) {
-        GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
-        GF_HIP(hipStreamWaitEvent(h->stream2, r.ev2, 0));
-      } else {
-        GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
-        GF_HIP(hipStreamWaitEvent(h->stream2, r.ev, 0));
-        if (r.split) {
-          GF_HIP(hipStreamWaitEvent(h->stream, r.ev2, 0));
-          GF_HIP(hipStreamWaitEvent(h->stream2, r.ev2, 0));
-        }
-      }
+      GF_HIP(hipStreamWaitEvent(h->stream, r.ev, 0));
+      GF_HIP(hipStreamWaitEvent(h->stream2, r.ev, 0));
       r.live = false;
-      r.split = false;
       r.bmask = 0;
     }
   }
@@ -248,11 +228,10 @@ void release(fe_handle* h) {
   if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
   if (h->kstream) hipStreamSynchronize(h->kstream);
-  if (h->kstream2) hipStreamSynchronize(h->kstream2);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
                   h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
-                  h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
+                  h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1], h->adj_global};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -262,10 +241,9 @@ void release(fe_handle* h) {
   for (hipEvent_t e : h->ag_ev)
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
-                       h->ev_kjoin2, h->kread[0].ev, h->kread[1].ev, h->kread[0].ev2, h->kread[1].ev2})
+                       h->kread[0].ev, h->kread[1].ev})
     if (e) hipEventDestroy(e);
   if (h->kstream) hipStreamDestroy(h->kstream);
-  if (h->kstream2) hipStreamDestroy(h->kstream2);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->comm_stream) hipStreamDestroy(h->comm_stream);
@@ -363,6 +341,7 @@ gf::StepArgs base_args(fe_handle* h) {
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
   a.prefetch = h->prefetch;
+  a.adj_global = h->adj_global;
   a.u_scale = h->cfg.action_scalar;
   a.us_f = a.as_f;
   a.x_scale = 1.0;
@@ -398,6 +377,7 @@ gf::StepArgs env_range(const fe_handle* h, const gf::StepArgs& a, int b0, int nb
   if (a.reward) r.reward = a.reward + b0;
   if (a.dt_env) r.dt_env = a.dt_env + b0;
   if (a.adj_bits) r.adj_bits = a.adj_bits + e0 * Wn;
+  if (a.adj_global) r.adj_global = a.adj_global + e0 * Wn;
   if (a.degree_out) r.degree_out = a.degree_out + e0;
   if (a.knn_idx) {
     const size_t K = h->cfg.n_neighbors;
@@ -502,41 +482,41 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.B = h->cfg.n_envs;
   k.K = h->cfg.n_neighbors;
   k.diag = (h->diag >> 12) & 0xfc00;  // kNN kernel switches: 0x400000.. -> 0x0400.. (KnnArgs.diag)
-  if (mode == 2 && h->last_b0 > 0 && h->s2_pending && h->kstream2) {
-    // rim kNN of a split step: each half after its own half of the step (see kstream2)
-    const int B0 = h->last_b0, N = k.N, K = k.K;
-    const size_t e0 = (size_t)B0 * N;
-    gf::KnnArgs k1 = k;
-    k.B = B0;
-    k1.B = h->cfg.n_envs - B0;
-    k1.x = k.x + e0 * 4;
-    k1.idx = k.idx + e0 * K;
-    k1.obs = k.obs + e0 * 4 * K;
-    k1.r2k = k.r2k + e0;
-    k1.rimflag = k.rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
-    k.grid_cap = k1.grid_cap = GF_RIM_HALF_GRID;
-#ifdef GF_DIAG
-    if (h->diag & 0x100000) {  // experiment: each half's rim kNN in its own step stream
+  if (mode == 2) {
+    // the rim kNN of a fused step goes on the step's own streams, right behind the half
+    // that produced its rows: a kNN handle then runs two hardware queues, like a plain
+    // one, and the next step's half orders after its rim by stream order (no events)
+    if (h->last_b0 > 0 && h->s2_pending) {
+      const int B0 = h->last_b0, N = k.N, K = k.K;
+      const size_t e0 = (size_t)B0 * N;
+      gf::KnnArgs k1 = k;
+      k.B = B0;
+      k1.B = h->cfg.n_envs - B0;
+      k1.x = k.x + e0 * 4;
+      k1.idx = k.idx + e0 * K;
+      k1.obs = k.obs + e0 * 4 * K;
+      k1.r2k = k.r2k + e0;
+      k1.rimflag = k.rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
+      k.grid_cap = k1.grid_cap = GF_RIM_HALF_GRID;
       hipError_t e = gf::launch_knn(k, h->stream);
       if (e == hipSuccess) e = gf::launch_knn(k1, h->stream2);
       if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
-      h->has_knn = true;
-      return GF_OK;
+    } else {
+      if (int rc = join_s2(h)) return rc;
+      hipError_t e = gf::launch_knn(k, h->stream);
+      if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
     }
-#endif
-    GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
-    GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[0], 0));
-    GF_HIP(hipEventRecord(h->ev_kin[1], h->stream2));
-    GF_HIP(hipStreamWaitEvent(h->kstream2, h->ev_kin[1], 0));
-    hipError_t e = gf::launch_knn(k, h->kstream);
-    if (e == hipSuccess) e = gf::launch_knn(k1, h->kstream2);
-    if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
-    GF_HIP(hipEventRecord(r.ev, h->kstream));
-    GF_HIP(hipEventRecord(r.ev2, h->kstream2));
-    r.live = r.split = true;
-    h->k_pending = h->k2_pending = true;
+    r.live = false;
+    r.bmask = 0;
     h->has_knn = true;
     return GF_OK;
+  }
+  if (!h->kstream) {  // the separate kNN stream exists only once a full kNN is needed
+    hipError_t e = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      h->kstream = nullptr;
+      return fail_hip("kNN stream create", e);
+    }
   }
   // on kstream after everything on both step streams (both halves' state and bits)
   GF_HIP(hipEventRecord(h->ev_kin[0], h->stream));
@@ -549,7 +529,6 @@ int launch_knn_cur(fe_handle* h, int mode) {
   if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
   GF_HIP(hipEventRecord(r.ev, h->kstream));
   r.live = true;
-  r.split = false;
   if (mode == 1) r.bmask |= 1u << h->bits_cur;
   h->k_pending = true;
   h->has_knn = true;
@@ -606,6 +585,8 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   h->BN = B * N;
   h->R = gf::step_rows_per_block(cfg->n_agents);
   h->T = gf::step_tile(cfg->n_agents);
+  const bool global_bits = cfg->n_agents >= GF_GLOBAL_BITS_MIN_N;
+  if (global_bits) h->R = GF_GLOBAL_BITS_R;
   // tile loads issued a tile ahead: 1604 -> 1527 us at N=8192 (16 tiles); no gain at 2-8
   // tiles, where its registers cost occupancy instead
   h->prefetch = (cfg->n_agents + h->T - 1) / h->T >= 16 ? 1 : 0;
@@ -633,7 +614,8 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (rc = dalloc(&h->knn_obs[1], h->BN * 4 * cfg->n_neighbors)) ||
       (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_r2[0], h->BN)) || (rc = dalloc(&h->knn_r2[1], h->BN)))) ||
       (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_rimflag[0], B * ((N + 255) / 256))) ||
-                                (rc = dalloc(&h->knn_rimflag[1], B * ((N + 255) / 256)))))) {
+                                (rc = dalloc(&h->knn_rimflag[1], B * ((N + 255) / 256))))) ||
+      (global_bits && (rc = dalloc(&h->adj_global, h->BN * ((N + 63) / 64))))) {
     release(h);
     return rc;
   }
@@ -642,13 +624,10 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (e = hipEventCreateWithFlags(&h->ev_s2, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_main, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreate(&h->tw[0])) != hipSuccess || (e = hipEventCreate(&h->tw[1])) != hipSuccess ||
-      // the kNN stream only for handles that rank neighbours: a plain handle runs two
-      // streams, so two of them fit the process's 4 hardware queues (GPU_MAX_HW_QUEUES)
-      (cfg->n_neighbors > 0 && (e = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking)) != hipSuccess) ||
-      (cfg->n_neighbors > 0 && (e = hipStreamCreateWithFlags(&h->kstream2, hipStreamNonBlocking)) != hipSuccess) ||
-      (e = hipEventCreateWithFlags(&h->ev_kjoin2, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&h->kread[0].ev2, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&h->kread[1].ev2, hipEventDisableTiming)) != hipSuccess ||
+      // no kNN stream here: the fused step's rim kNN runs on the step streams, and a full
+      // kNN (fe_get_knn without a step, k != 7, variants) creates one on first use; so a
+      // Flocking-v0 handle, like a plain one, runs two streams and two of them fit the
+      // process's 4 hardware queues (GPU_MAX_HW_QUEUES)
       (e = hipEventCreateWithFlags(&h->ev_kin[0], hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kin[1], hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_kjoin, hipEventDisableTiming)) != hipSuccess ||
@@ -960,6 +939,41 @@ int fe_get_controls(fe_handle* h, int env, double* dst) {
   const size_t n = (size_t)h->cfg.n_agents * 2;
   const double* src = h->ctrl[h->ccur];
   return env < 0 ? d2h(h, dst, src, h->BN * 2 * 8) : d2h(h, dst, src + env * n, n * 8);
+}
+
+int fe_get_outputs(fe_handle* h, int env, float* state_values, float* network, double* rewards, int flags) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (flags != 0) return fail(GF_EINVAL, "flags must be 0");
+  if (int rc = check_env(h, env)) return rc;
+  if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (int rc = use_dev(h)) return rc;
+  const size_t N = h->cfg.n_agents;
+  const size_t nsv = env < 0 ? h->BN * 6 : N * 6, nnet = env < 0 ? h->BN * N : N * N;
+  if (rewards)
+    GF_HIP(hipMemcpyAsync(rewards, cur_reward(h), (size_t)h->cfg.n_envs * 8, hipMemcpyDeviceToHost, h->stream));
+  if (state_values)
+    GF_HIP(hipMemcpyAsync(state_values, h->sv + (env < 0 ? 0 : env * N * 6), nsv * 4, hipMemcpyDeviceToHost,
+                          h->stream));
+  if (network)
+    GF_HIP(hipMemcpyAsync(network, h->net + (env < 0 ? 0 : env * N * N), nnet * 4, hipMemcpyDeviceToHost, h->stream));
+  GF_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int fe_host_alloc(size_t bytes, void** out) {
+  if (!out || bytes == 0) return fail(GF_EINVAL, "bad argument");
+  *out = nullptr;
+  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return fail(GF_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  }
+  return GF_OK;
+}
+
+int fe_host_free(void* p) {
+  if (p) GF_HIP(hipHostFree(p));
+  return GF_OK;
 }
 
 int fe_get_rewards(fe_handle* h, double* dst) {

@@ -26,6 +26,27 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #ifndef GF_DEPHASE  // split steps: de-phase the halves at the first split step (A/B builds)
 #define GF_DEPHASE 1
 #endif
+#ifndef GF_KNN_MED3  // fused kNN: list insertion by v_med3_u32 (1) or a min/max chain (0)
+#define GF_KNN_MED3 1
+#endif
+#ifndef GF_RECIP_NR  // pair terms' 1/r2: 0 = IEEE division, 1 = rcp + Newton without the
+#define GF_RECIP_NR 0  // controller, 2 = everywhere (A/B builds; 1 and 2 measured slower)
+#endif
+#ifndef GF_KNN_LATE_GATHER  // fused kNN: the neighbour's state is loaded after the epilogue (1)
+#define GF_KNN_LATE_GATHER 0  // or before it, its latency under the epilogue's sums (0)
+#endif
+#ifndef GF_KNN_LEAN  // fused kNN: velocity sums in the reward block epilogue (1) or staged (0)
+#define GF_KNN_LEAN 0  // (A/B builds)
+#endif
+#ifndef GF_INLINE_RIM_U  // fused kNN inline rim scan: columns in flight per lane
+#define GF_INLINE_RIM_U 4
+#endif
+#ifndef GF_GLOBAL_BITS_MIN_N  // envs of at least this many agents keep the rows' adjacency
+#define GF_GLOBAL_BITS_MIN_N (1 << 30)  // bits in a global scratch (L2) instead of LDS
+#endif
+#ifndef GF_GLOBAL_BITS_R  // rows per workgroup when the bits are global
+#define GF_GLOBAL_BITS_R 16
+#endif
 #ifndef GF_KNN_SLICE_LIST  // fused kNN: keys each feature-pass slice keeps (A/B builds)
 #define GF_KNN_SLICE_LIST 7
 #endif
@@ -79,6 +100,8 @@ struct StepArgs {
   float us_f, uc_f;       // float32 copies of u_scale, u_clip
   const double* dt_env;   // (B) per-env dt of this step, or nullptr (dt)
   uint64_t* adj_bits;     // (B,N,Wn) packed adjacency or nullptr
+  uint64_t* adj_global;   // (B,N,Wn) scratch holding the rows' adjacency bits in global
+                          // memory (L2) instead of LDS (wide envs), or nullptr
   int32_t* degree_out;    // (B,N) degrees or nullptr
   // Flocking-v0 k-nearest selection fused into the feature pass (kStepFusedK neighbours):
   // rows the step can rank exactly get idx + obs; the others get idx[row*K] = -1 and
@@ -124,7 +147,7 @@ struct StatsArgs {
 // Launch-geometry helpers shared by host and tests.
 int step_rows_per_block(int N);
 int step_tile(int N);
-size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn);
+size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn, bool global_bits = false);
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
 // Whether a step of this geometry can carry the fused k-nearest selection (K ==

@@ -190,6 +190,37 @@ __device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
 }
 
 // Sorted insertion of (r2, j) into a K-list; ties go to the lower index (stable).
+// 1/r2 for the pair terms: v_rcp_f64 refined by two Newton steps (within an ulp or two
+// of the IEEE quotient, 5 float64 ops instead of the 10 of a correctly rounded
+// division); zero, denormal, huge and NaN r2 take the IEEE division, so its infinities
+// and NaNs are kept
+__device__ __forceinline__ double recip_f64(double r2) {
+  double x = __builtin_amdgcn_rcp(r2);
+  double e = fma(-r2, x, 1.0);
+  x = fma(x, e, x);
+  e = fma(-r2, x, 1.0);
+  x = fma(x, e, x);
+  if (!(r2 >= 0x1p-1000 && r2 <= 0x1p+1000)) x = 1.0 / r2;
+  return x;
+}
+
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
+  unsigned r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Insert v into the ascending list k[0..L) keeping its L smallest (the largest drops
+// off): new k[m] = median(k[m-1], k[m], v) from the top down, then k[0] = min(k[0], v):
+// one v_med3_u32 per entry, in place (a min/max exchange chain needs two per entry
+// plus the register copies the compiler adds to rotate its temporaries)
+template <int L>
+__device__ __forceinline__ void knn_list_insert(unsigned (&k)[L], unsigned v) {
+#pragma unroll
+  for (int m = L - 1; m >= 1; --m) k[m] = med3_u32(k[m - 1], k[m], v);
+  k[0] = min(k[0], v);
+}
+
 template <int K>
 __device__ __forceinline__ void knn_insert(double (&kr)[K], int (&kj)[K], double r2, int j) {
   if (r2 < kr[K - 1] || (r2 == kr[K - 1] && j < kj[K - 1])) {
@@ -314,7 +345,7 @@ __device__ __forceinline__ void step_inline_rim(const StepArgs& a, size_t env0, 
       lr[m] = __builtin_inf();
       lj[m] = INT_MAX;
     }
-    constexpr int U = UF64 ? 2 : 4;  // columns in flight per lane
+    constexpr int U = GF_INLINE_RIM_U;  // columns in flight per lane
     for (int j0 = lane; j0 < N; j0 += U * 64) {
       St p[U];
 #pragma unroll
@@ -595,7 +626,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
 // row combined, state_values (:124-129), the updated state, the controller (:194-226)
 // and, by the env's first block, the reward (instant_cost :145-147). `writer` = the
 // thread holding slice 0 of a valid row.
-template <bool DYN, bool UF64, bool CTRL, bool VAR>
+template <bool DYN, bool UF64, bool CTRL, bool VAR, bool SVACC = true>
 __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile, double* red, const St& me,
                                               double f0, double f1, double f2, double f3, double f4,
                                               double f5, double gx, double gy, double svx, double svy, int b,
@@ -617,8 +648,14 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
     }
   });
 
-  const double Svx = block_sum(svx, red);
-  const double Svy = block_sum(svy, red);
+  // SVACC: every thread summed its share of the env's velocities while staging the tiles;
+  // otherwise (the fused kNN step, whose registers are short) the reward block sums them
+  // here in the same per-thread order (j = tid, tid + kThreads, ...), so the bits agree
+  double Svx = 0, Svy = 0;
+  if constexpr (SVACC) {
+    Svx = block_sum(svx, red);
+    Svy = block_sum(svy, red);
+  }
 
   if (writer && !GF_ABLATE(a, 256)) {  // diag 256: skip the per-row outputs (timing only)
     const size_t g = env0 + i_row;
@@ -667,6 +704,23 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
   // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
   // first row block; single-tile envs read the velocities from the LDS tile
   if (a.reward && i0 == 0 && !GF_ABLATE(a, 512)) {  // diag 512: skip the reward (timing only)
+    if constexpr (!SVACC) {
+      double sx = 0, sy = 0;
+      if (N <= T) {
+        for (int t = tid; t < N; t += kThreads) {
+          sx += tile[t].vx;
+          sy += tile[t].vy;
+        }
+      } else {
+        for (int j = tid; j < N; j += kThreads) {
+          const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
+          sx += s.vx;
+          sy += s.vy;
+        }
+      }
+      Svx = block_sum(sx, red);
+      Svy = block_sum(sy, red);
+    }
     const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
     double qx = 0, qy = 0;
     if (N <= T) {
@@ -742,22 +796,24 @@ void flock_step_kernel(StepArgs a) {
   const int N = a.N, R = a.R, T = a.T;
   const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
   const int Wt = T >> 6;         // words per row of one tile
-  St* tile = reinterpret_cast<St*>(smem);                      // float64 state, T
-  St* rows = tile + T;                                         // this block's rows, R
-  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
-  uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
-  uint64_t* candb = nearb + (CTRL ? (size_t)R * Wt : 0);       // (predicted rows) x Wt kNN candidates
-  double* red = reinterpret_cast<double*>(candb + (KN ? (size_t)R * Wt : 0));
-  float* redf = reinterpret_cast<float*>(red + 4);
-  float* inv = reinterpret_cast<float*>(red + 8);
-  [[maybe_unused]] float* rthr = inv + R;                      // R kNN candidate radii^2 (0: none)
-
   // the plain step deals the reward blocks out first (195 vs 200 us at config 2; with
   // the controller it measured 1 us slower); diag 8192 forces the plain remap (A/B)
   const int L = (!CTRL && !GF_ABLATE(a, 8192)) ? xcd_remap_reward_first(blockIdx.x, gridDim.x, a.bpe)
                                             : xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / a.bpe;
   const int i0 = (L - b * a.bpe) * R;
+  St* tile = reinterpret_cast<St*>(smem);                      // float64 state, T
+  St* rows = tile + T;                                         // this block's rows, R
+  // R x Wn adjacency bits: in LDS, or (wide envs) in the global scratch at this block's
+  // rows (the same (B,N,Wn) layout as the packed output)
+  uint64_t* adj = a.adj_global ? a.adj_global + ((size_t)b * N + i0) * Wn : reinterpret_cast<uint64_t*>(rows + R);
+  uint64_t* nearb = a.adj_global ? reinterpret_cast<uint64_t*>(rows + R) : adj + (size_t)R * Wn;  // R x Wt controller bits
+  uint64_t* candb = nearb + (CTRL ? (size_t)R * Wt : 0);       // (predicted rows) x Wt kNN candidates
+  double* red = reinterpret_cast<double*>(candb + (KN ? (size_t)R * Wt : 0));
+  float* redf = reinterpret_cast<float*>(red + 4);
+  float* inv = reinterpret_cast<float*>(red + 8);
+  [[maybe_unused]] float* rthr = inv + R;                      // R kNN candidate radii^2 (0: none)
+
   const int nrows = min(R, N - i0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -802,6 +858,8 @@ void flock_step_kernel(StepArgs a) {
   const bool frow = fr < nrows;
   double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
   double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
+  // the fused kNN step leaves the velocity sums to the reward block's epilogue (4 VGPRs)
+  constexpr bool kSvAcc = CTRL || KN == 0 || !GF_KNN_LEAN;
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
   // kNN rows predicted to lack k neighbours (their k-th nearest two states back was
   // at >= 0.8 comm_radius): predm (wave-uniform) marks them, rthr[r] holds row r's
@@ -829,6 +887,7 @@ void flock_step_kernel(StepArgs a) {
 #pragma unroll
     for (int m = 0; m < KL; ++m) kk[m] = 0xFFFFFFFFu;
   }
+  [[maybe_unused]] const double qmaxd = static_cast<double>(a.knn_qmax);
   // one neighbour pair (row fr = me, tile column c): features and controller gradient.
   // The row's state is read from LDS per feature pass, so it holds no registers
   // through pass 1.
@@ -837,22 +896,31 @@ void flock_step_kernel(StepArgs a) {
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
     if constexpr (KN > 0) {
+#ifndef GF_PROBE_NO_INSERT
      if (!GF_ABLATE(a, 0x200000)) {  // diag 0x200000: no insertion (timing only)
-      const double qd = r2 * ksc;
-      const unsigned q = qd < static_cast<double>(a.knn_qmax) ? static_cast<unsigned>(qd) : a.knn_qmax;
-      unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
+#else
+     if (false) {
+#endif
+      // q = min(floor(r2 * ksc), qmax); fmin returns qmax for a NaN r2 (ranked last)
+      const unsigned q = static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
+      const unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
+      if constexpr (GF_KNN_MED3) {
+        knn_list_insert<KL>(kk, v);
+      } else {
+        unsigned w = v;
 #pragma unroll
-      for (int m = 0; m < KL; ++m) {
-        const unsigned lo = min(kk[m], v);
-        v = max(kk[m], v);
-        kk[m] = lo;
+        for (int m = 0; m < KL; ++m) {
+          const unsigned lo = min(kk[m], w);
+          w = max(kk[m], w);
+          kk[m] = lo;
+        }
       }
      }
       if (!isadj && !(CTRL && isnear)) return;  // a candidate only: no features
     }
-    // one division per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
+    // one reciprocal per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
     // reference's two divisions; far inside the float32 outputs' tolerance)
-    const double ir = 1.0 / r2, irr = ir * ir;
+    const double ir = (GF_RECIP_NR >= (CTRL ? 2 : 1)) ? recip_f64(r2) : 1.0 / r2, irr = ir * ir;
     const double q1x = dx * irr, q2x = dx * ir;
     const double q1y = dy * irr, q2y = dy * ir;
     if (isadj) {
@@ -912,8 +980,10 @@ void flock_step_kernel(StepArgs a) {
       tile[t] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
       pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
-      svx += s.vx;
-      svy += s.vy;
+      if constexpr (kSvAcc) {
+        svx += s.vx;
+        svy += s.vy;
+      }
     };
     if constexpr (PF >= 1) {
 #pragma unroll
@@ -974,7 +1044,9 @@ void flock_step_kernel(StepArgs a) {
       unsigned fca0 = 0, fca1 = 0, fcb0 = 0, fcb1 = 0;
       int fp = 0, frp = 0;
       bool fused = false;
+#ifndef GF_PROBE_NO_FUSED
       if constexpr (KN > 0) fused = 2 * __popcll(predm) >= nrows;
+#endif
       if (fused) {
         const float ftcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
         for (int r = 0; r < nrows; ++r) {
@@ -1132,7 +1204,7 @@ void flock_step_kernel(StepArgs a) {
     }
   }
   // packed output: the block's R x Wn adjacency words are one contiguous range
-  if (a.adj_bits) {
+  if (a.adj_bits && a.adj_bits != a.adj_global) {
     uint64_t* dst = a.adj_bits + (env0 + i0) * (size_t)Wn;
     for (int k = tid; k < nrows * Wn; k += kThreads) dst[k] = adj[k];
   }
@@ -1147,6 +1219,7 @@ void flock_step_kernel(StepArgs a) {
 
   [[maybe_unused]] RawState<UF64> kraw{};
   [[maybe_unused]] bool kgo = false;
+  [[maybe_unused]] int kj = 0;
   [[maybe_unused]] bool kinl = false;  // this row is ranked by its wave at the end (inline rim)
   if constexpr (KN > 0) {
    if (!GF_ABLATE(a, 1)) {  // diag 1: no merge / kNN outputs (timing only)
@@ -1203,7 +1276,8 @@ void flock_step_kernel(StepArgs a) {
         // the neighbour's state: its loads are issued here and used after the
         // epilogue, so their latency runs under the epilogue's sums
         if (!GF_ABLATE(a, 32)) {  // diag 32: no observation gather (timing only)
-          kraw = load_raw<DYN, UF64>(a, env0 + j);
+          if constexpr (!GF_KNN_LATE_GATHER) kraw = load_raw<DYN, UF64>(a, env0 + j);
+          kj = j;
           kgo = true;
         }
       }
@@ -1212,10 +1286,11 @@ void flock_step_kernel(StepArgs a) {
   }
 
   const St me = frow ? rows[fr] : St{0, 0, 0, 0};
-  step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
+  step_epilogue<DYN, UF64, CTRL, VAR, kSvAcc>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
                                       frow && fs == 0, S, tid);
   if constexpr (KN > 0) {
     if (kgo) {  // Flocking-v0 observation x_i - x_j of this lane's neighbour (flocking.py:24)
+      if constexpr (GF_KNN_LATE_GATHER) kraw = load_raw<DYN, UF64>(a, env0 + kj);
       const St o = state_from_raw<DYN, UF64>(a, kraw);
       if (fs == KN - 1 && a.knn_r2) {  // the row's k-th nearest r2: candidate radius two steps on
         const double dx = me.px - o.px, dy = me.py - o.py;
@@ -1232,7 +1307,9 @@ void flock_step_kernel(StepArgs a) {
     // agent's post-update position (recomputed from x_in and u, bit-identical to the
     // step's), with the rim kernel's ranking and outputs (knn_wave_scan, knn_write_row)
     const uint64_t todo = __ballot(kinl && fs == 0);
+#ifndef GF_PROBE_NO_INLINE_RIM
     if (todo) step_inline_rim<DYN, UF64, KN>(a, env0, todo, i_row, me);
+#endif
   }
   GF_STAMP(10);
 #if defined(GF_STAMPS) && GF_STAMPS >= 2
@@ -1599,10 +1676,10 @@ int step_tile(int N) {
   return t < kTileDefault ? t : kTileDefault;
 }
 
-size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
+size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn, bool global_bits) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
-  s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
+  s += (global_bits ? 0 : (size_t)R * Wn * 8) + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 2 : 1) + 15) / 16) * 16;
   return s;
 }
@@ -1622,7 +1699,7 @@ hipError_t max_lds_once(const void* f, std::atomic<uint64_t>& done, int bytes) {
 
 template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
-  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0);
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0, a.adj_global != nullptr);
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
   // would allow
   if (!CTRL && !VAR && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;

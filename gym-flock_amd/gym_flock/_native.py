@@ -93,6 +93,9 @@ SIGNATURES = {
     "fe_reset_synthetic": [_P, ctypes.c_uint64, ctypes.c_double],
     "fe_get_controls": [_P, _I, _P],
     "fe_get_rewards": [_P, _P],
+    "fe_get_outputs": [_P, _I, _P, _P, _P, _I],
+    "fe_host_alloc": [ctypes.c_size_t, ctypes.POINTER(_P)],
+    "fe_host_free": [_P],
     "fe_get_knn": [_P, _I, _P, _P],
     "fe_device_buffers": [_P, ctypes.POINTER(FeBuffers)],
     "fe_sync": [_P],
@@ -177,6 +180,74 @@ def load(path=None):
 def check(rc):
     if rc != GF_OK:
         raise GymFlockError(rc, load().fe_last_error().decode(errors="replace"))
+
+
+class HostPool:
+    """Page-locked host buffers (fe_host_alloc) handed out as fresh numpy arrays.
+
+    The drop-in env returns new arrays every step (the reference's step() does, and
+    callers may keep them). Copying the step's outputs into page-locked memory runs at
+    full link rate and touches no fresh pageable pages; each array here owns its buffer
+    until the array (and every view of it) is released, then the buffer returns to the
+    pool for the next step. Page-locked bytes held by live arrays are capped: past the
+    cap (a caller keeping many steps' outputs), arrays are ordinary numpy memory."""
+
+    def __init__(self, cap_bytes=256 << 20):
+        import threading
+        self.cap = int(cap_bytes)
+        self.live = 0
+        self.free = {}
+        self.lock = threading.Lock()
+
+    def array(self, shape, dtype):
+        import weakref
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dtype.itemsize
+        if nbytes == 0:
+            return np.empty(shape, dtype)
+        with self.lock:
+            lst = self.free.get(nbytes)
+            p = lst.pop() if lst else None
+            if p is None and self.live + nbytes > self.cap:
+                return np.empty(shape, dtype)
+            self.live += nbytes
+        if p is None:
+            out = ctypes.c_void_p()
+            try:
+                check(load().fe_host_alloc(nbytes, ctypes.byref(out)))
+            except GymFlockError:
+                with self.lock:
+                    self.live -= nbytes
+                return np.empty(shape, dtype)
+            p = out.value
+        buf = (ctypes.c_uint8 * nbytes).from_address(p)
+        fin = weakref.finalize(buf, self._release, p, nbytes)
+        fin.atexit = False  # the process's exit frees page-locked memory
+        return np.frombuffer(buf, dtype=dtype).reshape(shape)
+
+    def _release(self, p, nbytes):
+        with self.lock:
+            self.live -= nbytes
+            self.free.setdefault(nbytes, []).append(p)
+
+    def trim(self):
+        """Free the recycled (unused) buffers."""
+        with self.lock:
+            ps = [p for lst in self.free.values() for p in lst]
+            self.free = {}
+        for p in ps:
+            load().fe_host_free(ctypes.c_void_p(p))
+
+
+_host_pool = None
+
+
+def host_pool():
+    """The process-wide HostPool of the drop-in envs."""
+    global _host_pool
+    if _host_pool is None:
+        _host_pool = HostPool()
+    return _host_pool
 
 
 def check_shard_sizes(n_envs):
@@ -340,6 +411,19 @@ class FlockHandle:
         out = np.empty(self.n_envs)
         check(self.lib.fe_get_rewards(self.h, ptr(out)))
         return out
+
+    def outputs(self, env=None, pool=None):
+        """(state_values, network, rewards) in one call and one stream sync
+        (fe_get_outputs). With a HostPool the arrays are page-locked buffers from it
+        (fresh arrays to the caller, recycled once released)."""
+        n = self.n_agents
+        lead = (self.n_envs, n) if env is None else (n,)
+        new = pool.array if pool is not None else np.empty
+        sv = new(lead + (6,), np.float32)
+        net = new(lead + (n,), np.float32)
+        rw = np.empty(self.n_envs)
+        check(self.lib.fe_get_outputs(self.h, -1 if env is None else int(env), ptr(sv), ptr(net), ptr(rw), 0))
+        return sv, net, rw
 
     def knn(self, env=None):
         k, n = self.n_neighbors, self.n_agents

@@ -57,6 +57,11 @@ class FlockingRelativeEnv(Env):
         self.n_neighbors = 0
         self.reset_mode = "reference"
         self.reset_max_attempts = 1000
+        # how step() brings (state_values, network, reward) to the host: "pooled" = one
+        # fe_get_outputs call into page-locked arrays from the process's HostPool (fresh
+        # arrays to the caller, recycled once released); "batched" = the same call into
+        # ordinary numpy arrays; "getters" = three synchronous getters (bench.py's dropin)
+        self.fetch_mode = "pooled"
 
         self._make_spaces()
         self.fig = None
@@ -130,9 +135,14 @@ class FlockingRelativeEnv(Env):
     # ---------------------------------------------------------------- hot path
     def _fetch_obs(self):
         h = self._h
-        self.state_values = h.state_values(0)
-        self.state_network = h.network(0)
-        self._reward = float(h.rewards()[0])
+        if self.fetch_mode == "getters":
+            self.state_values = h.state_values(0)
+            self.state_network = h.network(0)
+            self._reward = float(h.rewards()[0])
+            return
+        pool = nat.host_pool() if self.fetch_mode == "pooled" else None
+        self.state_values, self.state_network, rw = h.outputs(0, pool=pool)
+        self._reward = float(rw[0])
 
     def step(self, u):
         """:91-109 — dynamics, compute_helpers and instant_cost in one device launch."""

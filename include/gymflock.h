@@ -152,7 +152,16 @@ int fe_get_network_rows(fe_handle* h, int env, int row0, int nrows, float* dst);
  * env < 0: all envs. Either pointer may be NULL. */
 int fe_get_network_packed(fe_handle* h, int env, uint64_t* bits, int32_t* degree);
 int fe_get_controls(fe_handle* h, int env, double* dst);     /* (N,2) :210-211 */
-int fe_get_rewards(fe_handle* h, double* dst);               /* (B)   :145-147 */
+int fe_get_rewards(fe_handle* h, double* dst);
+/* The step's host outputs in one call with one stream sync (the drop-in env's
+ * (state_values, network), reward tuple of step(), flocking_relative.py:109): any of
+ * state_values (N,6) / network (N,N) of `env` (env < 0: all envs) and rewards (B) may be
+ * NULL. flags: reserved, 0. Destinations from fe_host_alloc copy at full link rate. */
+int fe_get_outputs(fe_handle* h, int env, float* state_values, float* network, double* rewards, int flags);
+/* Page-locked host memory for output arrays (the drop-in env hands such buffers to the
+ * caller as fresh arrays and recycles them once released). */
+int fe_host_alloc(size_t bytes, void** out);
+int fe_host_free(void* p);               /* (B)   :145-147 */
 int fe_get_knn(fe_handle* h, int env, int32_t* idx, float* obs); /* (N,k), (N,4k) */
 int fe_device_buffers(fe_handle* h, fe_buffers* out);
 int fe_sync(fe_handle* h);

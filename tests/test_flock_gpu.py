@@ -773,3 +773,72 @@ def test_knn_bench_workload_long_run():
                 np.testing.assert_array_equal(idx, ridx)
                 np.testing.assert_array_equal(obs, robs.astype(np.float32))
     env.close()
+
+
+def test_batched_outputs_match_getters():
+    """fe_get_outputs (one call, one sync; into numpy or page-locked pool arrays) returns
+    the same state_values, network and rewards as the three getters, per env and for the
+    whole batch; the drop-in env's fetch modes give the same step() tuple."""
+    import gym_flock
+    B, n = 3, 130
+    x0 = synthetic_batch(B, n, seed0=77)
+    u = np.random.RandomState(78).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B)
+    h.set_state(x0)
+    h.step(u)
+    pool = nat.HostPool(cap_bytes=1 << 20)
+    for env in (None, 0, 2):
+        for p in (None, pool):
+            sv, net, rw = h.outputs(env, pool=p)
+            np.testing.assert_array_equal(sv, h.state_values(env))
+            np.testing.assert_array_equal(net, h.network(env))
+            np.testing.assert_array_equal(rw, h.rewards())
+    h.close()
+    outs = []
+    for mode in ("getters", "batched", "pooled"):
+        e = gym_flock.make("FlockingRelative-v0")
+        e.n_agents = n
+        e._make_spaces()
+        e.fetch_mode = mode
+        e.x = x0[0]
+        (sv, net), r, _, _ = e.step(u[0])
+        outs.append((sv, net, r))
+        e.close()
+    for sv, net, r in outs[1:]:
+        np.testing.assert_array_equal(sv, outs[0][0])
+        np.testing.assert_array_equal(net, outs[0][1])
+        assert r == outs[0][2]
+
+
+def test_host_pool_recycles_and_caps():
+    """The drop-in env's page-locked output pool: distinct buffers while arrays live, a
+    buffer comes back only once the array and every view of it are released, and past
+    the cap arrays are ordinary numpy memory."""
+    import gc
+    pool = nat.HostPool(cap_bytes=3 * 4096)
+    a = pool.array((1024,), np.float32)
+    b = pool.array((1024,), np.float32)
+    assert a.ctypes.data != b.ctypes.data and pool.live == 2 * 4096
+    pa = a.ctypes.data
+    del a
+    gc.collect()
+    c = pool.array((1024,), np.float32)
+    assert c.ctypes.data == pa
+    d = pool.array((1024,), np.float32)
+    e = pool.array((1024,), np.float32)  # over the cap: plain numpy
+    assert pool.live == 3 * 4096 and e.flags["OWNDATA"]
+    view = b[10:20]
+    pb = b.ctypes.data
+    del b
+    gc.collect()
+    assert pool.live == 3 * 4096  # the view keeps b's buffer
+    del view
+    gc.collect()
+    assert pool.live == 2 * 4096
+    f = pool.array((1024,), np.float32)
+    assert f.ctypes.data == pb
+    f[:] = 1.0
+    del c, d, e, f
+    gc.collect()
+    assert pool.live == 0
+    pool.trim()
