@@ -20,6 +20,20 @@ namespace {
 
 constexpr int kCovThreads = 256;
 
+// Phase timeline (diagnostic builds only, -DGF_STAMPS): thread 0 of each workgroup
+// records s_memrealtime (100 MHz) at: start (0), first round trip done (1), claims done
+// (2), tail writes issued (3), all writes done (4), for scripts/cov_timeline.py.
+#ifdef GF_STAMPS
+__device__ unsigned long long gf_cov_stamp_buf[4096 * 8];
+#define GF_COV_STAMP(k)                                                              \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                       \
+      gf_cov_stamp_buf[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define GF_COV_STAMP(k) ((void)0)
+#endif
+
 __device__ __forceinline__ double dist2d(double ax, double ay, double bx, double by) {
   const double dx = ax - bx, dy = ay - by;
   return sqrt(dx * dx + dy * dy);  // np.linalg.norm of a 2-vector: sqrt(dx*dx + dy*dy)
@@ -162,6 +176,7 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   if (a.actions)
     for (int k = tid; k < M; k += kCovThreads) first[k] = INT_MAX;
   if (tid == 0) *counter = 0;
+  GF_COV_STAMP(0);
   // the env's words, loaded up front so none of them costs a round trip of its own
   const bool dirty = a.dirty[b] != 0;
   const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
@@ -228,6 +243,7 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     }
   }
   __syncthreads();
+  GF_COV_STAMP(1);
 
   if (act) {
     // then, in robot order, a move succeeds unless its node is already claimed; a
@@ -294,6 +310,7 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
         if (r3.i < R) new_s[r3.i] = r3.v;
       }
       __syncthreads();
+      GF_COV_STAMP(2);
     } else {
       for (int i = tid; i < R; i += kCovThreads) new_s[i] = chosen[i];  // guess: every move succeeds
       while (true) {
@@ -358,21 +375,24 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
         atomicAdd(counter, 1);
       }
     }
-    const int qs[4] = {q4.x, q4.y, q4.z, q4.w};
-    const double2 cs[4] = {c0, c1, c2, c3};
-#pragma unroll
-    for (int ac = 0; ac < 4; ++ac) {
-      const int q = ac < nc ? qs[ac] + R : n;
-      const float d = static_cast<float>(dist2d(px, py, cs[ac].x, cs[ac].y) / a.res);
-      const int k = 4 * i + ac;
-      snd[base + k] = q;
-      snd[base + 4 * R + k] = i;
-      rcv[base + k] = i;
-      rcv[base + 4 * R + k] = q;
-      edg[base + k] = d;
-      edg[base + 4 * R + k] = d;
-    }
+    // the robot's 4 action edges in both directions: six 16-byte stores (base and 4i are
+    // multiples of 4 elements, so every group is 16-byte aligned)
+    const int4 q = make_int4(0 < nc ? q4.x + R : n, 1 < nc ? q4.y + R : n, 2 < nc ? q4.z + R : n,
+                             3 < nc ? q4.w + R : n);
+    const float4 d = make_float4(static_cast<float>(dist2d(px, py, c0.x, c0.y) / a.res),
+                                 static_cast<float>(dist2d(px, py, c1.x, c1.y) / a.res),
+                                 static_cast<float>(dist2d(px, py, c2.x, c2.y) / a.res),
+                                 static_cast<float>(dist2d(px, py, c3.x, c3.y) / a.res));
+    const int4 ii = make_int4(i, i, i, i);
+    const int k = base + 4 * i;
+    *reinterpret_cast<int4*>(snd + k) = q;
+    *reinterpret_cast<int4*>(snd + k + 4 * R) = ii;
+    *reinterpret_cast<int4*>(rcv + k) = ii;
+    *reinterpret_cast<int4*>(rcv + k + 4 * R) = q;
+    *reinterpret_cast<float4*>(edg + k) = d;
+    *reinterpret_cast<float4*>(edg + k + 4 * R) = d;
   }
+  GF_COV_STAMP(3);
   __syncthreads();
   if (tid == 0) {
     const int newly = *counter;
@@ -384,6 +404,10 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     a.done[b] = (sc0 + 1 == a.episode_length || nv == T) ? 1 : 0;
     a.dirty[b] = 0;
   }
+#ifdef GF_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GF_COV_STAMP(4);
+#endif
 }
 
 // reset (:405-424 after the random draws): robots onto their start targets, the
@@ -519,5 +543,14 @@ hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(cov_step_kernel, dim3(a.B), dim3(kCovThreads), cov_step_lds_bytes(a.R, a.M), s, a);
   return hipGetLastError();
 }
+
+#ifdef GF_STAMPS
+extern "C" __attribute__((visibility("default"))) int cov_diag_stamps(unsigned long long* dst, int n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(gf_cov_stamp_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 
 }  // namespace gf

@@ -804,10 +804,8 @@ void flock_step_kernel(StepArgs a) {
   const int i0 = (L - b * a.bpe) * R;
   St* tile = reinterpret_cast<St*>(smem);                      // float64 state, T
   St* rows = tile + T;                                         // this block's rows, R
-  // R x Wn adjacency bits: in LDS, or (wide envs) in the global scratch at this block's
-  // rows (the same (B,N,Wn) layout as the packed output)
-  uint64_t* adj = a.adj_global ? a.adj_global + ((size_t)b * N + i0) * Wn : reinterpret_cast<uint64_t*>(rows + R);
-  uint64_t* nearb = a.adj_global ? reinterpret_cast<uint64_t*>(rows + R) : adj + (size_t)R * Wn;  // R x Wt controller bits
+  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
+  uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
   uint64_t* candb = nearb + (CTRL ? (size_t)R * Wt : 0);       // (predicted rows) x Wt kNN candidates
   double* red = reinterpret_cast<double*>(candb + (KN ? (size_t)R * Wt : 0));
   float* redf = reinterpret_cast<float*>(red + 4);
@@ -1204,7 +1202,7 @@ void flock_step_kernel(StepArgs a) {
     }
   }
   // packed output: the block's R x Wn adjacency words are one contiguous range
-  if (a.adj_bits && a.adj_bits != a.adj_global) {
+  if (a.adj_bits) {
     uint64_t* dst = a.adj_bits + (env0 + i0) * (size_t)Wn;
     for (int k = tid; k < nrows * Wn; k += kThreads) dst[k] = adj[k];
   }
@@ -1655,6 +1653,314 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
   a.degree[g] = deg;
 }
 
+
+// ---------------------------------------------------------------------------------
+// Wide envs (N >= kGridMinN): a cell list instead of the all-pairs tile loop.
+//
+// The tiled step stages the whole env into LDS for every row block and compares every
+// row with every column: at N = 8192 each 16-row block re-reads 8192 agents (4.3 GB of
+// L2 -> LDS per step at config 5) and 80 % of a workgroup's life is that loop (phase
+// timeline, profiles/r03). Here flock_grid_prep_kernel (one workgroup per env) applies
+// the double-integrator update once per agent (writes x_out) and bins the agents into
+// square cells of side hc >= max(cr, sqrt(cr)) over the env's bounding box (counting
+// sort: cell_start, agent indices and float64 positions in cell order).
+// flock_grid_step_kernel decides each row's adjacency only against the agents of the
+// 3 x 3 cells around its own: every agent closer than hc lies there, since cell indices
+// of points less than hc apart differ by at most one. The decision is the reference's
+// float64 r2 = dx*dx + dy*dy < cr^2 (no FMA), so the bits are exactly the tiled step's;
+// the rows' dense network is stored as the tiled step stores it (one contiguous range
+// per block), and the feature pass walks the set bits in ascending j per word slice with
+// the neighbours' states read from x_out. Non-finite or huge coordinates make the env
+// one cell (every agent a candidate).
+struct GridLayout {
+  size_t start, idx, pos, stride;  // byte offsets of cell_start[N+1], idx[N], pos[N] (double2)
+};
+__host__ __device__ inline GridLayout grid_layout(int N) {
+  GridLayout g;
+  g.start = 64;
+  g.idx = g.start + 4 * ((size_t)N + 1);
+  g.pos = (g.idx + 4 * (size_t)N + 15) & ~(size_t)15;
+  g.stride = (g.pos + 16 * (size_t)N + 255) & ~(size_t)255;
+  return g;
+}
+struct GridHdr {
+  double ox, oy, ih;
+  int nx, ny, full;
+};
+
+constexpr int kPrepThreads = 1024;
+constexpr int kGridMaxN = 16384;  // flock_grid_prep_kernel's LDS (2N + 1 ints) fits a CU
+
+__device__ __forceinline__ int grid_cell(double v, double o, double ih, int n) {
+  const double q = floor((v - o) * ih);
+  return q < 0.0 ? 0 : (q >= static_cast<double>(n) ? n - 1 : static_cast<int>(q));
+}
+
+template <bool UF64>
+__global__ __launch_bounds__(kPrepThreads) void flock_grid_prep_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const size_t env0 = (size_t)b * N;
+  const GridLayout gl = grid_layout(N);
+  unsigned char* gb = a.grid + (size_t)b * gl.stride;
+  int* cellid = reinterpret_cast<int*>(smem);  // N
+  int* hist = cellid + N;                       // N + 1
+  __shared__ double red[4][kPrepThreads / 64];
+  __shared__ GridHdr hd;
+  __shared__ int scan_part[2 * kPrepThreads / 64];
+  // 1. the post-update state of every agent (x_out) and the bounding box
+  double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
+  for (int j = tid; j < N; j += kPrepThreads) {
+    const St s = load_state<true, UF64>(a, env0 + j);
+    double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * (env0 + j);
+    xo[0] = double2{s.px, s.py};
+    xo[1] = double2{s.vx, s.vy};
+    // fmin/fmax drop NaN; a NaN or huge coordinate shows up as a span check failure below
+    const bool ok = fabs(s.px) <= 1.0e12 && fabs(s.py) <= 1.0e12;
+    x0 = ok ? fmin(x0, s.px) : -__builtin_inf();
+    x1 = ok ? fmax(x1, s.px) : __builtin_inf();
+    y0 = fmin(y0, s.py);
+    y1 = fmax(y1, s.py);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    x0 = fmin(x0, __shfl_xor(x0, o));
+    x1 = fmax(x1, __shfl_xor(x1, o));
+    y0 = fmin(y0, __shfl_xor(y0, o));
+    y1 = fmax(y1, __shfl_xor(y1, o));
+  }
+  if (lane == 0) {
+    red[0][wid] = x0;
+    red[1][wid] = x1;
+    red[2][wid] = y0;
+    red[3][wid] = y1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kPrepThreads / 64; ++w) {
+      x0 = fmin(x0, red[0][w]);
+      x1 = fmax(x1, red[1][w]);
+      y0 = fmin(y0, red[2][w]);
+      y1 = fmax(y1, red[3][w]);
+    }
+    GridHdr h{0.0, 0.0, 0.0, 1, 1, 1};
+    const double sx = x1 - x0, sy = y1 - y0;
+    if (sx >= 0.0 && sy >= 0.0 && sx <= 1.0e12 && sy <= 1.0e12 && fabs(y0) <= 1.0e12 && fabs(y1) <= 1.0e12) {
+      // cells at least max(cr, sqrt(cr)) wide (adjacency r2 < cr^2, the controller's
+      // r2 <= cr), with a margin over the rounding of the cell index; at most N cells
+      double hc = fmax(a.cr, sqrt(a.cr)) * (1.0 + 1.0e-7) + 1.0e-290;
+      double nx = floor(sx / hc) + 1.0, ny = floor(sy / hc) + 1.0;
+      while (nx * ny > static_cast<double>(N)) {
+        hc *= 1.25;
+        nx = floor(sx / hc) + 1.0;
+        ny = floor(sy / hc) + 1.0;
+      }
+      h = GridHdr{x0, y0, 1.0 / hc, static_cast<int>(nx), static_cast<int>(ny), 0};
+    }
+    hd = h;
+    *reinterpret_cast<GridHdr*>(gb) = h;
+  }
+  __syncthreads();
+  const GridHdr h = hd;
+  const int ncell = h.nx * h.ny;
+  // 2. counting sort of the agents by cell
+  for (int c = tid; c <= ncell; c += kPrepThreads) hist[c] = 0;
+  __syncthreads();
+  for (int j = tid; j < N; j += kPrepThreads) {
+    const St s = load_state<true, UF64>(a, env0 + j);
+    const int c = h.full ? 0 : grid_cell(s.py, h.oy, h.ih, h.ny) * h.nx + grid_cell(s.px, h.ox, h.ih, h.nx);
+    cellid[j] = c;
+    atomicAdd(&hist[c], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the cell counts: each thread sums a chunk, the 16 waves scan their
+  // chunk sums with shuffles, then the wave totals
+  const int per = (ncell + 1 + kPrepThreads - 1) / kPrepThreads;
+  const int c0 = min(ncell + 1, tid * per), c1 = min(ncell + 1, c0 + per);
+  int local = 0;
+  for (int c = c0; c < c1; ++c) local += hist[c];
+  int incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) scan_part[wid] = incl;
+  __syncthreads();
+  if (wid == 0) {
+    const int wt = lane < kPrepThreads / 64 ? scan_part[lane] : 0;
+    int wi = wt;
+#pragma unroll
+    for (int o = 1; o < kPrepThreads / 64; o <<= 1) {
+      const int t = __shfl_up(wi, o);
+      if (lane >= o) wi += t;
+    }
+    if (lane < kPrepThreads / 64) scan_part[kPrepThreads / 64 + lane] = wi - wt;
+  }
+  __syncthreads();
+  int* cstart = reinterpret_cast<int*>(gb + gl.start);
+  int run = scan_part[kPrepThreads / 64 + wid] + incl - local;
+  for (int c = c0; c < c1; ++c) {
+    const int v = hist[c];
+    hist[c] = run;
+    cstart[c] = run;
+    run += v;
+  }
+  __syncthreads();
+  int* sidx = reinterpret_cast<int*>(gb + gl.idx);
+  double2* spos = reinterpret_cast<double2*>(gb + gl.pos);
+  for (int j = tid; j < N; j += kPrepThreads) {
+    const St s = load_state<true, UF64>(a, env0 + j);
+    const int q = atomicAdd(&hist[cellid[j]], 1);
+    sidx[q] = j;
+    spos[q] = double2{s.px, s.py};
+  }
+}
+
+#ifndef GF_GRID_WAVES  // waves per SIMD the cell-list step's registers allow
+#define GF_GRID_WAVES 6
+#endif
+#ifndef GF_GRID_GATHER  // neighbour states in flight per thread in its feature pass
+#define GF_GRID_GATHER 2
+#endif
+
+template <bool UF64>
+__global__ __launch_bounds__(kThreads, GF_GRID_WAVES) void flock_grid_step_kernel(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, R = a.R, Wn = (N + 63) >> 6;
+  const int L = xcd_remap_reward_first(blockIdx.x, gridDim.x, a.bpe);
+  const int b = L / a.bpe;
+  const int i0 = (L - b * a.bpe) * R;
+  const int nrows = min(R, N - i0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const size_t env0 = (size_t)b * N;
+  St* rows = reinterpret_cast<St*>(smem);                    // R
+  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);     // R x Wn
+  double* red = reinterpret_cast<double*>(adj + (size_t)R * Wn);
+  float* inv = reinterpret_cast<float*>(red + 8);            // R
+  const St* xs = reinterpret_cast<const St*>(a.x_out) + env0;  // post-update states (prep)
+  const GridLayout gl = grid_layout(N);
+  const unsigned char* gb = a.grid + (size_t)b * gl.stride;
+  const GridHdr h = *reinterpret_cast<const GridHdr*>(gb);
+  const int* cstart = reinterpret_cast<const int*>(gb + gl.start);
+  const int* sidx = reinterpret_cast<const int*>(gb + gl.idx);
+  const double2* spos = reinterpret_cast<const double2*>(gb + gl.pos);
+
+  int* rs_ = reinterpret_cast<int*>(inv + ((R + 3) & ~3));  // 3R range starts, 3R sizes, R + 1 row offsets
+  int* rn_ = rs_ + 3 * R;
+  int* pre = rn_ + 3 * R;
+  for (int k = tid; k < R * Wn; k += kThreads) adj[k] = 0ull;
+  // each row's 3 cell-row ranges (x-neighbouring cells are consecutive in cell order),
+  // looked up by 3R threads at once
+  if (tid < 3 * nrows) {
+    const int r = tid / 3, d = tid - 3 * r;
+    const St me = xs[i0 + r];
+    if (d == 0) rows[r] = me;
+    int s0 = 0, n0 = 0;
+    if (h.full) {
+      n0 = d == 0 ? N : 0;
+    } else {
+      const int cx = grid_cell(me.px, h.ox, h.ih, h.nx), cy = grid_cell(me.py, h.oy, h.ih, h.ny);
+      const int yy = cy - 1 + d;
+      if (yy >= 0 && yy < h.ny) {
+        s0 = cstart[yy * h.nx + max(cx - 1, 0)];
+        n0 = cstart[yy * h.nx + min(cx + 1, h.nx - 1) + 1] - s0;
+      }
+    }
+    rs_[tid] = s0;
+    rn_[tid] = n0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int r = 0; r < nrows; ++r) {
+      pre[r] = run;
+      run += rn_[3 * r] + rn_[3 * r + 1] + rn_[3 * r + 2];
+    }
+    pre[nrows] = run;
+  }
+  __syncthreads();
+  // adjacency: every (row, candidate) pair of the block, flattened over its threads (the
+  // candidates' loads are independent), decided in float64 as the reference does
+  const int total = pre[nrows];
+  for (int f = tid; f < total; f += kThreads) {
+    int r = 0;
+    for (int step = 32; step >= 1; step >>= 1)
+      if (r + step <= nrows - 1 && pre[r + step] <= f) r += step;
+    int k = f - pre[r];
+    const int n0 = rn_[3 * r], n1 = rn_[3 * r + 1];
+    const int q = k < n0 ? rs_[3 * r] + k : (k < n0 + n1 ? rs_[3 * r + 1] + (k - n0) : rs_[3 * r + 2] + (k - n0 - n1));
+    const int j = sidx[q];
+    const double2 p = spos[q];
+    const St me = rows[r];
+    const double dx = me.px - p.x, dy = me.py - p.y;
+    const double r2 = dx * dx + dy * dy;
+    if (r2 < a.cr2 && j != i0 + r)
+      atomicOr(reinterpret_cast<unsigned long long*>(adj + (size_t)r * Wn + (j >> 6)), 1ull << (j & 63));
+  }
+  __syncthreads();
+  // degrees -> 1/deg, stores, features: the tiled step's mapping (S slices per row)
+  const int S = kThreads / R;
+  const int fr = tid / S, fs = tid - fr * S;
+  const bool frow = fr < nrows;
+  const int wpt = (Wn + S - 1) / S;
+  const int wb = fs * wpt, we = min(Wn, wb + wpt);
+  {
+    int deg = 0;
+    if (frow)
+      for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
+    with_slices(S, [&](auto Sc) { deg = group_sum_c<decltype(Sc)::value>(deg); });
+    if (frow && fs == 0) inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
+  }
+  __syncthreads();
+  if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
+  double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0;
+  const St me = frow ? rows[fr] : St{0, 0, 0, 0};
+  if (frow) {
+    for (int w = wb; w < we; ++w) {
+      uint64_t m = adj[(size_t)fr * Wn + w];
+      while (m) {
+        // up to G neighbours' states in flight
+        constexpr int G = GF_GRID_GATHER;
+        int js[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          js[q] = -1;
+          if (m) {
+            js[q] = (w << 6) + __builtin_ctzll(m);
+            m &= m - 1;
+          }
+        }
+        St os[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q)
+          if (js[q] >= 0) os[q] = xs[js[q]];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          if (js[q] < 0) continue;
+          const St o = os[q];
+          const double dx = me.px - o.px, dy = me.py - o.py;
+          const double r2 = dx * dx + dy * dy;
+          const double ir = 1.0 / r2, irr = ir * ir;
+          f0 += me.vx - o.vx;
+          f1 += dx * irr;
+          f2 += dx * ir;
+          f3 += me.vy - o.vy;
+          f4 += dy * irr;
+          f5 += dy * ir;
+        }
+      }
+    }
+  }
+  // per-row outputs and the reward from the post-update states (x_out already written)
+  StepArgs e = a;
+  e.x_in = a.x_out;
+  e.T = 0;
+  step_epilogue<false, UF64, false, false, false>(e, nullptr, red, me, f0, f1, f2, f3, f4, f5, 0.0, 0.0, 0.0,
+                                                  0.0, b, i0, i0 + fr, frow && fs == 0, S, tid);
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- host
@@ -1676,10 +1982,10 @@ int step_tile(int N) {
   return t < kTileDefault ? t : kTileDefault;
 }
 
-size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn, bool global_bits) {
+size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
-  s += (global_bits ? 0 : (size_t)R * Wn * 8) + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
+  s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 2 : 1) + 15) / 16) * 16;
   return s;
 }
@@ -1699,7 +2005,7 @@ hipError_t max_lds_once(const void* f, std::atomic<uint64_t>& done, int bytes) {
 
 template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
-  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0, a.adj_global != nullptr);
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0);
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
   // would allow
   if (!CTRL && !VAR && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
@@ -1732,7 +2038,40 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   return launch_step_tiled<DYN, UF64, CTRL, false>(a, s);
 }
 
+
+size_t grid_bytes_per_env(int N) { return grid_layout(N).stride; }
+
+template <bool UF64>
+static hipError_t launch_step_grid_t(const StepArgs& a, hipStream_t s) {
+  const size_t prep_lds = (2 * (size_t)a.N + 1) * sizeof(int);
+  static std::atomic<uint64_t> attr_p{0};
+  // its static LDS (~5 KiB) plus the dynamic cell arrays must fit the 160 KiB of a CU:
+  // the attribute covers N <= kGridMaxN
+  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_grid_prep_kernel<UF64>), attr_p,
+                                        (int)((2 * (size_t)kGridMaxN + 1) * sizeof(int)));
+      e != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(flock_grid_prep_kernel<UF64>, dim3(a.B), dim3(kPrepThreads), prep_lds, s, a);
+  if (const hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  const size_t Wn = (a.N + 63) / 64;
+  const size_t lds = (size_t)a.R * sizeof(St) + (size_t)a.R * Wn * 8 + 8 * sizeof(double) +
+                     (((size_t)a.R + 3) & ~(size_t)3) * 4 + (7 * (size_t)a.R + 1) * 4;
+  static std::atomic<uint64_t> attr_s{0};
+  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_grid_step_kernel<UF64>), attr_s,
+                                        160 * 1024);
+      e != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(flock_grid_step_kernel<UF64>, dim3(a.B * a.bpe), dim3(kThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+bool step_grid_ok(const StepArgs& a, bool dyn, bool ctrl) {
+  return a.grid && dyn && !ctrl && !a.knn_idx && !a.variant && !a.adj_bits && !a.degree_out && a.N <= kGridMaxN &&
+         kThreads % a.R == 0 && kThreads / a.R <= 64;
+}
+
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s) {
+  if (step_grid_ok(a, dyn, ctrl)) return u_f64 ? launch_step_grid_t<true>(a, s) : launch_step_grid_t<false>(a, s);
   if (dyn) {
     if (u_f64) return ctrl ? launch_step_t<true, true, true>(a, s) : launch_step_t<true, true, false>(a, s);
     return ctrl ? launch_step_t<true, false, true>(a, s) : launch_step_t<true, false, false>(a, s);

@@ -12,7 +12,8 @@ from gym_flock.init_states import synthetic_batch  # noqa: E402
 N = int(os.environ.get("N", 1024))
 B = int(os.environ.get("B", 256))
 STEPS = int(os.environ.get("STEPS", 5))
-h = nat.FlockHandle(N, B)
+KNN = os.environ.get("KNN") == "1"  # the Flocking-v0 step (fused 7-NN) instead of the plain one
+h = nat.FlockHandle(N, B, n_neighbors=7 if KNN else 0)
 # one launch per step (fe_set_streams(1)) so each counter row is a whole step's bytes;
 # the split launches of the default write the same bytes in two halves
 h.set_streams(1)
@@ -21,7 +22,7 @@ h.set_actions(np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.
 if os.environ.get("DIAG"):  # ablation switches: diagnostic build only (GYMFLOCK_LIB=build/lib_diag/...)
     h.diag_switches(int(os.environ["DIAG"], 0))
 for _ in range(STEPS):
-    h.step(None, nat.FE_U_RESIDENT)
+    h.step(None, nat.FE_U_RESIDENT | (nat.FE_WITH_KNN if KNN else 0))
 if os.environ.get("FILL"):
     h.diag_fill(os.environ["FILL"] == "nt", STEPS)
 h.sync()
