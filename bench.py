@@ -96,14 +96,15 @@ def step_bytes(n):
     return 4 * n * n + 96 * n + 8
 
 
-def load_traffic(n_agents, n_envs):
-    """Per-step HBM bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE,
-    gfx950 correction) for this workload, committed under profiles/; None if absent."""
+def load_traffic(key):
+    """Per-step HBM bytes measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    correction) for the workload `key` ("1024x256", "8192x32", "knn7_1024x256",
+    "coverage_r200x512"), committed in profiles/pmc_traffic.json; None if absent."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get("%dx%d" % (n_agents, n_envs))
+        e = d.get(key)
         return None if e is None else float(e["bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         return None
@@ -225,12 +226,12 @@ def timed(env, ranks, k, step, per_rank=None):
     return max(every), kernel_ms
 
 
-def flock_roofline(n, b, kernel_ms, launches_per_step):
+def flock_roofline(n, b, kernel_ms, launches_per_step, kernel="flock_step_kernel<DYN,f32 u>"):
     bytes_step = b * step_bytes(n)
     achieved = bytes_step / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(n, b),
-            "kernel": "flock_step_kernel<DYN,f32 u>", "region_ms_per_step": kernel_ms,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("%dx%d" % (n, b)),
+            "kernel": kernel, "region_ms_per_step": kernel_ms,
             "algorithmic_bytes_per_step": bytes_step, "launches_per_step": launches_per_step,
             "timing": "device time per step of the whole timed region (HIP events on the handle's stream, the "
                       "end event after it joins the second): each step is two concurrent half-batch launches "
@@ -253,7 +254,8 @@ def bench_config5(args):
     out = {"metric": "agent-steps/sec, FlockingRelative N=8192", "value": N * B * K / el, "unit": "agent-steps/s",
            "steps": K, "warmup": W, "clock_warmup": warm, "ms_per_step": 1e3 * el / K,
            "config": {"workload": "FlockingRelative-v0 step(), N=8192 agents x 32 envs (BASELINE.json configs[4])"},
-           "roofline": flock_roofline(N, B, kms, 2)}
+           "roofline": flock_roofline(N, B, kms, 2, kernel="flock_grid_prep_kernel + flock_grid_step_kernel "
+                                                          "(cell-list step for N >= 4096)")}
     if not args.no_cpu_baseline:
         log("cpu baseline N=8192 (cpu_ref, 1 step)...")
         rate, steps, sec = cpu_ref_rate(N, 1.0, max_steps=1)
@@ -326,10 +328,13 @@ def bench_config4(args, with_greedy=False):
            "config": {"workload": "Coverage-v0 step(), R=200 robots, T=%d targets, max_nodes %d, %d envs "
                                   "(BASELINE.json configs[3])" % (len(targets), M, B)},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "cov_step_kernel",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("coverage_r200x512"),
+                        "kernel": "cov_step_kernel",
                         "region_ms_per_step": kernel_ms, "algorithmic_bytes_per_step": B * per_env,
                         "note": "latency-limited, not bandwidth-limited: one workgroup per env, two dependent "
-                                "global round trips and the claim resolution per step (DESIGN.md)"}}
+                                "global round trips and the claim resolution per step (DESIGN.md); traffic from "
+                                "PMC with the FETCH_SIZE x2 correction, which the guide calibrates for wide "
+                                "coalesced reads only (these are scattered 4-64 B reads)"}}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = coverage_cpu_baseline(targets, R, M, min(args.cpu_seconds, 8.0))
     if with_greedy:
@@ -724,8 +729,15 @@ def main():
         for _ in range(min(W, 5)):
             env.step(expert=True, controller=True)
         ec, cms = timed(env, ranks, K, lambda s: env.step(expert=True, controller=True))
+        cb = B * (step_bytes(N) + N * 8 * 2)  # + the controller's output (read back as the next u)
+        cach = cb / (cms * 1e-3) / 1e9 if cms > 0 else 0.0
         extra["step_with_controller"] = {"value": world * B * N * K / ec, "unit": "agent-steps/s",
-                                         "ms_per_step": 1e3 * ec / K, "region_ms_per_step": cms}
+                                         "ms_per_step": 1e3 * ec / K, "region_ms_per_step": cms,
+                                         "algorithmic_bytes_per_step": cb,
+                                         "roofline": {"bound": "hbm", "achieved": cach, "peak": HBM_PEAK_GBS,
+                                                      "unit": "GB/s", "frac": cach / HBM_PEAK_GBS,
+                                                      "traffic": load_traffic("ctrl_1024x256"),
+                                                      "kernel": "flock_step_kernel<DYN,f64 u,CTRL>"}}
 
     # packed output mode: adjacency bits + degree instead of the dense rows
     if not args.no_packed_line:
@@ -735,10 +747,13 @@ def main():
         ep, pk_ms = timed(env, ranks, K, lambda s: env.step(resident=True, network="packed"))
         wn = (N + 63) // 64
         pk_bytes = B * (8 * N * wn + 4 * N + 96 * N + 8)
+        pach = pk_bytes / (pk_ms * 1e-3) / 1e9 if pk_ms > 0 else 0.0
         extra["packed_network"] = {
             "value": world * B * N * K / ep, "unit": "agent-steps/s", "ms_per_step": 1e3 * ep / K,
             "region_ms_per_step": pk_ms, "algorithmic_bytes_per_step": pk_bytes,
-            "achieved_GBs": pk_bytes / (pk_ms * 1e-3) / 1e9 if pk_ms > 0 else None,
+            "roofline": {"bound": "hbm", "achieved": pach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": pach / HBM_PEAK_GBS, "traffic": load_traffic("packed_1024x256"),
+                         "kernel": "flock_step_kernel<DYN,f32 u> (packed output)"},
             "note": "adjacency as bits (N*ceil(N/64)*8 B) + int32 degree per env instead of the dense "
                     "float32 network; the pair work, not HBM, bounds this mode"}
 
@@ -760,12 +775,14 @@ def main():
         # the step's bytes + per agent idx (7 x int32), obs (28 x float32) and the k-th
         # nearest r2 (float32) written, the history r2 read
         kb = B * (step_bytes(N) + N * (7 * 4 + 28 * 4 + 4 + 4))
+        kach = kb / (kk_ms * 1e-3) / 1e9 if kk_ms > 0 else 0.0
         extra["flocking_v0_knn7"] = {
             "value": world * B * N * K / ek, "unit": "agent-steps/s", "ms_per_step": 1e3 * ek / K,
             "region_ms_per_step": kk_ms, "ratio_to_plain_step": ek / elapsed,
             "algorithmic_bytes_per_step": kb,
-            "achieved_GBs": kb / (kk_ms * 1e-3) / 1e9 if kk_ms > 0 else None,
-            "frac_of_hbm_peak": kb / (kk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if kk_ms > 0 else None,
+            "roofline": {"bound": "hbm", "achieved": kach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": kach / HBM_PEAK_GBS, "traffic": load_traffic("knn7_1024x256"),
+                         "kernel": "flock_step_kernel<DYN,f32 u,KN=7> (+ rim flock_knn_kernel on the step streams)"},
             "note": "Flocking-v0 step: FlockingRelative step + 7-NN observation (idx + obs), from the "
                     "synthetic init under the same random actions"}
         envk.close()

@@ -635,6 +635,7 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     return fail_hip("event create", e);
   }
   if ((e = hipMemsetAsync(h->reward_ring, 0, sizeof(double) * kRewardSlots * B, h->stream)) != hipSuccess ||
+      (h->grid && (e = hipMemsetAsync(h->grid, 0, B * gf::grid_bytes_per_env((int)N), h->stream)) != hipSuccess) ||
       (e = clear_knn_history(h)) != hipSuccess ||
       (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
     release(h);

@@ -1655,173 +1655,187 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
 
 
 // ---------------------------------------------------------------------------------
-// Wide envs (N >= kGridMinN): a cell list instead of the all-pairs tile loop.
+// Wide envs (N >= kGridMinN): a hashed cell list instead of the all-pairs tile loop.
 //
 // The tiled step stages the whole env into LDS for every row block and compares every
 // row with every column: at N = 8192 each 16-row block re-reads 8192 agents (4.3 GB of
 // L2 -> LDS per step at config 5) and 80 % of a workgroup's life is that loop (phase
-// timeline, profiles/r03). Here flock_grid_prep_kernel (one workgroup per env) applies
-// the double-integrator update once per agent (writes x_out) and bins the agents into
-// square cells of side hc >= max(cr, sqrt(cr)) over the env's bounding box (counting
-// sort: cell_start, agent indices and float64 positions in cell order).
-// flock_grid_step_kernel decides each row's adjacency only against the agents of the
-// 3 x 3 cells around its own: every agent closer than hc lies there, since cell indices
-// of points less than hc apart differ by at most one. The decision is the reference's
-// float64 r2 = dx*dx + dy*dy < cr^2 (no FMA), so the bits are exactly the tiled step's;
-// the rows' dense network is stored as the tiled step stores it (one contiguous range
-// per block), and the feature pass walks the set bits in ascending j per word slice with
-// the neighbours' states read from x_out. Non-finite or huge coordinates make the env
-// one cell (every agent a candidate).
+// timeline, profiles/r03). Here, per step and env:
+//  * flock_grid_bin_kernel (one thread per agent): the double-integrator update (writes
+//    x_out), the agent's cell (cx, cy) = floor(p / hc), hc = max(cr, sqrt(cr)) plus a
+//    rounding margin, hashed into NB >= N buckets; its rank in the bucket by a global
+//    atomic. Non-finite or huge coordinates mark the env "full" (every agent is a
+//    candidate of every row).
+//  * flock_grid_scan_kernel (one workgroup per env): exclusive scan of the bucket counts
+//    (zeroed for the next step); flock_grid_scatter_kernel puts every agent (index and
+//    state) at its bucket's start + rank; flock_grid_order_kernel writes each bucket's
+//    agents again, ordered by index (one wave per bucket), so the candidates' order, and
+//    with it every sum, is deterministic.
+//  * flock_grid_step_kernel: each row's candidates are the agents of the buckets of the
+//    3 x 3 cells around its own (every agent closer than hc lies there; a bucket shared by
+//    two of those cells is read once; hash collisions only add candidates). Adjacency is
+//    the reference's float64 r2 = dx*dx + dy*dy < cr^2 (no FMA), so the bits are exactly
+//    the tiled step's; a wave takes a row, its lanes the candidates, and the features are
+//    summed per lane then across the wave (fixed order: deterministic). The rows' dense
+//    network is stored as the tiled step stores it (one contiguous range per block).
+constexpr int kGridMaxN = 16384;  // ranks and bucket counts of the cell-list step stay small
+constexpr int kScanThreads = 256;  // small workgroups: they slip in beside a running step
+constexpr int kScanMaxPer = 65;    // (NB + 1) / kScanThreads rounded up, NB <= 16384
+
 struct GridLayout {
-  size_t start, idx, pos, stride;  // byte offsets of cell_start[N+1], idx[N], pos[N] (double2)
+  size_t cnt, start, bin, rank, idx, st, idx2, st2, stride;  // byte offsets; NB buckets (+1: overflow)
+  int NB;
 };
 __host__ __device__ inline GridLayout grid_layout(int N) {
   GridLayout g;
-  g.start = 64;
-  g.idx = g.start + 4 * ((size_t)N + 1);
-  g.pos = (g.idx + 4 * (size_t)N + 15) & ~(size_t)15;
-  g.stride = (g.pos + 16 * (size_t)N + 255) & ~(size_t)255;
+  int nb = 64;
+  while (nb < N) nb <<= 1;
+  g.NB = nb;
+  g.cnt = 64;                                        // int cnt[NB + 1] (zero between steps)
+  g.start = g.cnt + 4 * ((size_t)nb + 1);            // int start[NB + 2]
+  g.bin = g.start + 4 * ((size_t)nb + 2);            // int bin[N]
+  g.rank = g.bin + 4 * (size_t)N;                    // int rank[N]
+  g.idx = g.rank + 4 * (size_t)N;                    // int idx[N] (bucket order)
+  g.st = (g.idx + 4 * (size_t)N + 31) & ~(size_t)31; // St st[N] (bucket order)
+  g.idx2 = g.st + 32 * (size_t)N;                    // int idx2[N] (bucket order, by index)
+  g.st2 = (g.idx2 + 4 * (size_t)N + 31) & ~(size_t)31;  // St st2[N]
+  g.stride = (g.st2 + 32 * (size_t)N + 255) & ~(size_t)255;
   return g;
 }
-struct GridHdr {
-  double ox, oy, ih;
-  int nx, ny, full;
-};
 
-constexpr int kPrepThreads = 1024;
-constexpr int kGridMaxN = 16384;  // flock_grid_prep_kernel's LDS (2N + 1 ints) fits a CU
-
-__device__ __forceinline__ int grid_cell(double v, double o, double ih, int n) {
-  const double q = floor((v - o) * ih);
-  return q < 0.0 ? 0 : (q >= static_cast<double>(n) ? n - 1 : static_cast<int>(q));
+__device__ __forceinline__ double grid_inv_cell(const StepArgs& a) {
+  return 1.0 / (fmax(a.cr, sqrt(a.cr)) * (1.0 + 1.0e-7) + 1.0e-290);
+}
+__device__ __forceinline__ int grid_hash(long long cx, long long cy, int nb) {
+  const unsigned long long h = static_cast<unsigned long long>(cx) * 0x9E3779B97F4A7C15ull ^
+                               static_cast<unsigned long long>(cy) * 0xC2B2AE3D27D4EB4Full;
+  return static_cast<int>((h ^ (h >> 29)) & static_cast<unsigned long long>(nb - 1));
 }
 
 template <bool UF64>
-__global__ __launch_bounds__(kPrepThreads) void flock_grid_prep_kernel(StepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = a.N, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const size_t env0 = (size_t)b * N;
+__global__ __launch_bounds__(kThreads) void flock_grid_bin_kernel(StepArgs a) {
+  const int N = a.N;
+  const size_t g = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g >= (size_t)a.B * N) return;
+  const int b = static_cast<int>(g / N), j = static_cast<int>(g - (size_t)b * N);
   const GridLayout gl = grid_layout(N);
   unsigned char* gb = a.grid + (size_t)b * gl.stride;
-  int* cellid = reinterpret_cast<int*>(smem);  // N
-  int* hist = cellid + N;                       // N + 1
-  __shared__ double red[4][kPrepThreads / 64];
-  __shared__ GridHdr hd;
-  __shared__ int scan_part[2 * kPrepThreads / 64];
-  // 1. the post-update state of every agent (x_out) and the bounding box
-  double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
-  for (int j = tid; j < N; j += kPrepThreads) {
-    const St s = load_state<true, UF64>(a, env0 + j);
-    double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * (env0 + j);
-    xo[0] = double2{s.px, s.py};
-    xo[1] = double2{s.vx, s.vy};
-    // fmin/fmax drop NaN; a NaN or huge coordinate shows up as a span check failure below
-    const bool ok = fabs(s.px) <= 1.0e12 && fabs(s.py) <= 1.0e12;
-    x0 = ok ? fmin(x0, s.px) : -__builtin_inf();
-    x1 = ok ? fmax(x1, s.px) : __builtin_inf();
-    y0 = fmin(y0, s.py);
-    y1 = fmax(y1, s.py);
+  const St s = load_state<true, UF64>(a, g);
+  double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
+  xo[0] = double2{s.px, s.py};
+  xo[1] = double2{s.vx, s.vy};
+  const double ih = grid_inv_cell(a);
+  int bk = gl.NB;  // overflow bucket
+  if (fabs(s.px) <= 1.0e12 && fabs(s.py) <= 1.0e12) {
+    bk = grid_hash(static_cast<long long>(floor(s.px * ih)), static_cast<long long>(floor(s.py * ih)), gl.NB);
+  } else {
+    atomicOr(reinterpret_cast<int*>(gb), 1);  // the env is "full" (flag word 0, see the sort)
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    x0 = fmin(x0, __shfl_xor(x0, o));
-    x1 = fmax(x1, __shfl_xor(x1, o));
-    y0 = fmin(y0, __shfl_xor(y0, o));
-    y1 = fmax(y1, __shfl_xor(y1, o));
-  }
-  if (lane == 0) {
-    red[0][wid] = x0;
-    red[1][wid] = x1;
-    red[2][wid] = y0;
-    red[3][wid] = y1;
-  }
-  __syncthreads();
+  int* cnt = reinterpret_cast<int*>(gb + gl.cnt);
+  reinterpret_cast<int*>(gb + gl.bin)[j] = bk;
+  reinterpret_cast<int*>(gb + gl.rank)[j] = atomicAdd(&cnt[bk], 1);
+}
+
+// exclusive scan of the env's bucket counts into start[0..NB+1] (and the counts zeroed
+// for the next step); this step's "full" flag for the step kernel (word 1), word 0 re-armed
+__global__ __launch_bounds__(kScanThreads) void flock_grid_scan_kernel(StepArgs a) {
+  const int N = a.N, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const GridLayout gl = grid_layout(N);
+  unsigned char* gb = a.grid + (size_t)b * gl.stride;
+  int* cnt = reinterpret_cast<int*>(gb + gl.cnt);
+  int* start = reinterpret_cast<int*>(gb + gl.start);
+  const int nbk = gl.NB + 1;
+  __shared__ int wsum[2][kScanThreads / 64];
   if (tid == 0) {
-    for (int w = 1; w < kPrepThreads / 64; ++w) {
-      x0 = fmin(x0, red[0][w]);
-      x1 = fmax(x1, red[1][w]);
-      y0 = fmin(y0, red[2][w]);
-      y1 = fmax(y1, red[3][w]);
-    }
-    GridHdr h{0.0, 0.0, 0.0, 1, 1, 1};
-    const double sx = x1 - x0, sy = y1 - y0;
-    if (sx >= 0.0 && sy >= 0.0 && sx <= 1.0e12 && sy <= 1.0e12 && fabs(y0) <= 1.0e12 && fabs(y1) <= 1.0e12) {
-      // cells at least max(cr, sqrt(cr)) wide (adjacency r2 < cr^2, the controller's
-      // r2 <= cr), with a margin over the rounding of the cell index; at most N cells
-      double hc = fmax(a.cr, sqrt(a.cr)) * (1.0 + 1.0e-7) + 1.0e-290;
-      double nx = floor(sx / hc) + 1.0, ny = floor(sy / hc) + 1.0;
-      while (nx * ny > static_cast<double>(N)) {
-        hc *= 1.25;
-        nx = floor(sx / hc) + 1.0;
-        ny = floor(sy / hc) + 1.0;
-      }
-      h = GridHdr{x0, y0, 1.0 / hc, static_cast<int>(nx), static_cast<int>(ny), 0};
-    }
-    hd = h;
-    *reinterpret_cast<GridHdr*>(gb) = h;
+    reinterpret_cast<int*>(gb)[1] = reinterpret_cast<int*>(gb)[0];
+    reinterpret_cast<int*>(gb)[0] = 0;
   }
-  __syncthreads();
-  const GridHdr h = hd;
-  const int ncell = h.nx * h.ny;
-  // 2. counting sort of the agents by cell
-  for (int c = tid; c <= ncell; c += kPrepThreads) hist[c] = 0;
-  __syncthreads();
-  for (int j = tid; j < N; j += kPrepThreads) {
-    const St s = load_state<true, UF64>(a, env0 + j);
-    const int c = h.full ? 0 : grid_cell(s.py, h.oy, h.ih, h.ny) * h.nx + grid_cell(s.px, h.ox, h.ih, h.nx);
-    cellid[j] = c;
-    atomicAdd(&hist[c], 1);
-  }
-  __syncthreads();
-  // exclusive scan of the cell counts: each thread sums a chunk, the 16 waves scan their
-  // chunk sums with shuffles, then the wave totals
-  const int per = (ncell + 1 + kPrepThreads - 1) / kPrepThreads;
-  const int c0 = min(ncell + 1, tid * per), c1 = min(ncell + 1, c0 + per);
+  const int per = (nbk + kScanThreads - 1) / kScanThreads;
+  const int c0 = min(nbk, tid * per), c1 = min(nbk, c0 + per);
+  int v[kScanMaxPer];
   int local = 0;
-  for (int c = c0; c < c1; ++c) local += hist[c];
+#pragma unroll
+  for (int k = 0; k < kScanMaxPer; ++k) {
+    v[k] = c0 + k < c1 ? cnt[c0 + k] : 0;
+    local += v[k];
+  }
   int incl = local;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int t = __shfl_up(incl, o);
     if (lane >= o) incl += t;
   }
-  if (lane == 63) scan_part[wid] = incl;
+  if (lane == 63) wsum[0][wid] = incl;
   __syncthreads();
   if (wid == 0) {
-    const int wt = lane < kPrepThreads / 64 ? scan_part[lane] : 0;
+    const int wt = lane < kScanThreads / 64 ? wsum[0][lane] : 0;
     int wi = wt;
 #pragma unroll
-    for (int o = 1; o < kPrepThreads / 64; o <<= 1) {
+    for (int o = 1; o < kScanThreads / 64; o <<= 1) {
       const int t = __shfl_up(wi, o);
       if (lane >= o) wi += t;
     }
-    if (lane < kPrepThreads / 64) scan_part[kPrepThreads / 64 + lane] = wi - wt;
+    if (lane < kScanThreads / 64) wsum[1][lane] = wi - wt;
   }
   __syncthreads();
-  int* cstart = reinterpret_cast<int*>(gb + gl.start);
-  int run = scan_part[kPrepThreads / 64 + wid] + incl - local;
-  for (int c = c0; c < c1; ++c) {
-    const int v = hist[c];
-    hist[c] = run;
-    cstart[c] = run;
-    run += v;
+  int run = wsum[1][wid] + incl - local;
+#pragma unroll
+  for (int k = 0; k < kScanMaxPer; ++k) {
+    if (c0 + k < c1) {
+      start[c0 + k] = run;
+      cnt[c0 + k] = 0;
+      run += v[k];
+    }
   }
-  __syncthreads();
-  int* sidx = reinterpret_cast<int*>(gb + gl.idx);
-  double2* spos = reinterpret_cast<double2*>(gb + gl.pos);
-  for (int j = tid; j < N; j += kPrepThreads) {
-    const St s = load_state<true, UF64>(a, env0 + j);
-    const int q = atomicAdd(&hist[cellid[j]], 1);
-    sidx[q] = j;
-    spos[q] = double2{s.px, s.py};
+  if (c1 == nbk && c0 < c1) start[nbk] = run;
+}
+
+// every agent to its slot: start of its bucket + its rank there
+__global__ __launch_bounds__(kThreads) void flock_grid_scatter_kernel(StepArgs a) {
+  const int N = a.N;
+  const size_t g = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g >= (size_t)a.B * N) return;
+  const int b = static_cast<int>(g / N), j = static_cast<int>(g - (size_t)b * N);
+  const GridLayout gl = grid_layout(N);
+  unsigned char* gb = a.grid + (size_t)b * gl.stride;
+  const int q = reinterpret_cast<const int*>(gb + gl.start)[reinterpret_cast<const int*>(gb + gl.bin)[j]] +
+                reinterpret_cast<const int*>(gb + gl.rank)[j];
+  reinterpret_cast<int*>(gb + gl.idx)[q] = j;
+  reinterpret_cast<St*>(gb + gl.st)[q] = reinterpret_cast<const St*>(a.x_out)[g];
+}
+
+// each bucket's agents by index (the atomics of the binning ranked them in any order),
+// into the second pair of arrays: one wave per bucket, each lane takes entries l, l+64,
+// ... and counts the bucket's smaller indices (agent indices are distinct)
+__global__ __launch_bounds__(kThreads) void flock_grid_order_kernel(StepArgs a) {
+  const int N = a.N;
+  const GridLayout gl = grid_layout(N);
+  const int nbk = gl.NB + 1;
+  const int lane = threadIdx.x & 63;
+  const size_t wv = ((size_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const size_t nwv = ((size_t)gridDim.x * kThreads) >> 6;
+  for (size_t g = wv; g < (size_t)a.B * nbk; g += nwv) {
+    const int b = static_cast<int>(g / nbk), c = static_cast<int>(g - (size_t)b * nbk);
+    const unsigned char* gb = a.grid + (size_t)b * gl.stride;
+    const int* start = reinterpret_cast<const int*>(gb + gl.start);
+    const int q0 = start[c], n = start[c + 1] - q0;
+    if (n == 0) continue;
+    const int* idx = reinterpret_cast<const int*>(gb + gl.idx) + q0;
+    const St* st = reinterpret_cast<const St*>(gb + gl.st) + q0;
+    int* idx2 = reinterpret_cast<int*>(a.grid + (size_t)b * gl.stride + gl.idx2) + q0;
+    St* st2 = reinterpret_cast<St*>(a.grid + (size_t)b * gl.stride + gl.st2) + q0;
+    for (int k = lane; k < n; k += 64) {
+      const int key = idx[k];
+      int rk = 0;
+      for (int m = 0; m < n; ++m) rk += idx[m] < key ? 1 : 0;
+      idx2[rk] = key;
+      st2[rk] = st[k];
+    }
   }
 }
 
 #ifndef GF_GRID_WAVES  // waves per SIMD the cell-list step's registers allow
-#define GF_GRID_WAVES 6
-#endif
-#ifndef GF_GRID_GATHER  // neighbour states in flight per thread in its feature pass
-#define GF_GRID_GATHER 2
+#define GF_GRID_WAVES 8
 #endif
 
 template <bool UF64>
@@ -1835,130 +1849,126 @@ __global__ __launch_bounds__(kThreads, GF_GRID_WAVES) void flock_grid_step_kerne
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const size_t env0 = (size_t)b * N;
-  St* rows = reinterpret_cast<St*>(smem);                    // R
-  uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);     // R x Wn
-  double* red = reinterpret_cast<double*>(adj + (size_t)R * Wn);
-  float* inv = reinterpret_cast<float*>(red + 8);            // R
-  const St* xs = reinterpret_cast<const St*>(a.x_out) + env0;  // post-update states (prep)
+  uint64_t* adj = reinterpret_cast<uint64_t*>(smem);                    // R x Wn
+  double* fsum = reinterpret_cast<double*>(adj + (size_t)R * Wn);       // R x 6 feature sums
+  double* red = fsum + 6 * R;                                           // 8
+  float* inv = reinterpret_cast<float*>(red + 8);                       // R
+  int* seg = reinterpret_cast<int*>(inv + ((R + 3) & ~3));              // R x 9 x (start, count)
+  const St* xs = reinterpret_cast<const St*>(a.x_out) + env0;           // post-update states
   const GridLayout gl = grid_layout(N);
   const unsigned char* gb = a.grid + (size_t)b * gl.stride;
-  const GridHdr h = *reinterpret_cast<const GridHdr*>(gb);
-  const int* cstart = reinterpret_cast<const int*>(gb + gl.start);
-  const int* sidx = reinterpret_cast<const int*>(gb + gl.idx);
-  const double2* spos = reinterpret_cast<const double2*>(gb + gl.pos);
+  const bool full = reinterpret_cast<const int*>(gb)[1] != 0;
+  const int* start = reinterpret_cast<const int*>(gb + gl.start);
+  const int* sidx = reinterpret_cast<const int*>(gb + gl.idx2);
+  const St* sst = reinterpret_cast<const St*>(gb + gl.st2);
 
-  int* rs_ = reinterpret_cast<int*>(inv + ((R + 3) & ~3));  // 3R range starts, 3R sizes, R + 1 row offsets
-  int* rn_ = rs_ + 3 * R;
-  int* pre = rn_ + 3 * R;
   for (int k = tid; k < R * Wn; k += kThreads) adj[k] = 0ull;
-  // each row's 3 cell-row ranges (x-neighbouring cells are consecutive in cell order),
-  // looked up by 3R threads at once
-  if (tid < 3 * nrows) {
-    const int r = tid / 3, d = tid - 3 * r;
-    const St me = xs[i0 + r];
-    if (d == 0) rows[r] = me;
+  // the 9 cells' buckets of every row, looked up by 9R threads at once; a bucket that
+  // an earlier cell of the same row already names is left out
+  for (int t = tid; t < 9 * nrows; t += kThreads) {
+    const int r = t / 9, d = t - 9 * r;
     int s0 = 0, n0 = 0;
-    if (h.full) {
+    if (full) {
       n0 = d == 0 ? N : 0;
     } else {
-      const int cx = grid_cell(me.px, h.ox, h.ih, h.nx), cy = grid_cell(me.py, h.oy, h.ih, h.ny);
-      const int yy = cy - 1 + d;
-      if (yy >= 0 && yy < h.ny) {
-        s0 = cstart[yy * h.nx + max(cx - 1, 0)];
-        n0 = cstart[yy * h.nx + min(cx + 1, h.nx - 1) + 1] - s0;
+      const St me = xs[i0 + r];
+      const double ih = grid_inv_cell(a);
+      const long long cx = static_cast<long long>(floor(me.px * ih)), cy = static_cast<long long>(floor(me.py * ih));
+      int bk[9];
+#pragma unroll
+      for (int e = 0; e < 9; ++e) bk[e] = grid_hash(cx + e % 3 - 1, cy + e / 3 - 1, gl.NB);
+      bool dup = false;
+#pragma unroll
+      for (int e = 0; e < 9; ++e) dup |= e < d && bk[e] == bk[d];
+      if (!dup) {
+        s0 = start[bk[d]];
+        n0 = start[bk[d] + 1] - s0;
       }
     }
-    rs_[tid] = s0;
-    rn_[tid] = n0;
+    seg[2 * t] = s0;
+    seg[2 * t + 1] = n0;
   }
   __syncthreads();
-  if (tid == 0) {
-    int run = 0;
-    for (int r = 0; r < nrows; ++r) {
-      pre[r] = run;
-      run += rn_[3 * r] + rn_[3 * r + 1] + rn_[3 * r + 2];
+  // adjacency and features: wave w takes rows w, w+4, ...; lane l the candidates l, l+64,
+  // ... of the row's segments (in bucket order), float64 decisions as the reference's
+  for (int r = wid; r < nrows; r += 4) {
+    const St me = xs[i0 + r];
+    const int* sg = seg + 18 * r;
+    int cum[10];
+    cum[0] = 0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) cum[e + 1] = cum[e] + sg[2 * e + 1];
+    const int tot = cum[9], self = i0 + r;
+    uint64_t* arow = adj + (size_t)r * Wn;
+    double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0;
+    int sgs[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) sgs[e] = sg[2 * e] - cum[e];
+    for (int k = lane; k < tot; k += 64) {
+      int q = 0;
+#pragma unroll
+      for (int e = 0; e < 9; ++e) q = (k >= cum[e] && k < cum[e + 1]) ? sgs[e] + k : q;
+      const int j = sidx[q];
+      const St o = sst[q];
+      const double dx = me.px - o.px, dy = me.py - o.py;
+      const double r2 = dx * dx + dy * dy;
+      if (r2 < a.cr2 && j != self) {
+        atomicOr(reinterpret_cast<unsigned long long*>(arow + (j >> 6)), 1ull << (j & 63));
+        const double ir = 1.0 / r2, irr = ir * ir;
+        f0 += me.vx - o.vx;
+        f1 += dx * irr;
+        f2 += dx * ir;
+        f3 += me.vy - o.vy;
+        f4 += dy * irr;
+        f5 += dy * ir;
+      }
     }
-    pre[nrows] = run;
+    f0 = wave_sum(f0);
+    f1 = wave_sum(f1);
+    f2 = wave_sum(f2);
+    f3 = wave_sum(f3);
+    f4 = wave_sum(f4);
+    f5 = wave_sum(f5);
+    if (lane == 0) {
+      double* fs = fsum + 6 * r;
+      fs[0] = f0, fs[1] = f1, fs[2] = f2, fs[3] = f3, fs[4] = f4, fs[5] = f5;
+    }
   }
   __syncthreads();
-  // adjacency: every (row, candidate) pair of the block, flattened over its threads (the
-  // candidates' loads are independent), decided in float64 as the reference does
-  const int total = pre[nrows];
-  for (int f = tid; f < total; f += kThreads) {
-    int r = 0;
-    for (int step = 32; step >= 1; step >>= 1)
-      if (r + step <= nrows - 1 && pre[r + step] <= f) r += step;
-    int k = f - pre[r];
-    const int n0 = rn_[3 * r], n1 = rn_[3 * r + 1];
-    const int q = k < n0 ? rs_[3 * r] + k : (k < n0 + n1 ? rs_[3 * r + 1] + (k - n0) : rs_[3 * r + 2] + (k - n0 - n1));
-    const int j = sidx[q];
-    const double2 p = spos[q];
-    const St me = rows[r];
-    const double dx = me.px - p.x, dy = me.py - p.y;
-    const double r2 = dx * dx + dy * dy;
-    if (r2 < a.cr2 && j != i0 + r)
-      atomicOr(reinterpret_cast<unsigned long long*>(adj + (size_t)r * Wn + (j >> 6)), 1ull << (j & 63));
-  }
-  __syncthreads();
-  // degrees -> 1/deg, stores, features: the tiled step's mapping (S slices per row)
+  // degrees -> 1/deg (S slices per row), then the rows' dense network
   const int S = kThreads / R;
-  const int fr = tid / S, fs = tid - fr * S;
+  const int fr = tid / S, fs_ = tid - fr * S;
   const bool frow = fr < nrows;
-  const int wpt = (Wn + S - 1) / S;
-  const int wb = fs * wpt, we = min(Wn, wb + wpt);
   {
+    const int wpt = (Wn + S - 1) / S;
+    const int wb = fs_ * wpt, we = min(Wn, wb + wpt);
     int deg = 0;
     if (frow)
       for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
     with_slices(S, [&](auto Sc) { deg = group_sum_c<decltype(Sc)::value>(deg); });
-    if (frow && fs == 0) inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
+    if (frow && fs_ == 0) inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
   }
   __syncthreads();
   if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
-  double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0;
-  const St me = frow ? rows[fr] : St{0, 0, 0, 0};
-  if (frow) {
-    for (int w = wb; w < we; ++w) {
-      uint64_t m = adj[(size_t)fr * Wn + w];
-      while (m) {
-        // up to G neighbours' states in flight
-        constexpr int G = GF_GRID_GATHER;
-        int js[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          js[q] = -1;
-          if (m) {
-            js[q] = (w << 6) + __builtin_ctzll(m);
-            m &= m - 1;
-          }
-        }
-        St os[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q)
-          if (js[q] >= 0) os[q] = xs[js[q]];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          if (js[q] < 0) continue;
-          const St o = os[q];
-          const double dx = me.px - o.px, dy = me.py - o.py;
-          const double r2 = dx * dx + dy * dy;
-          const double ir = 1.0 / r2, irr = ir * ir;
-          f0 += me.vx - o.vx;
-          f1 += dx * irr;
-          f2 += dx * ir;
-          f3 += me.vy - o.vy;
-          f4 += dy * irr;
-          f5 += dy * ir;
-        }
-      }
+  if (a.state_values && tid < 6 * nrows) a.state_values[(env0 + i0) * 6 + tid] = static_cast<float>(fsum[tid]);
+  // the reward (instant_cost :145-147) by the env's first block, from the post-update
+  // velocities in the tiled step's summation order (the same bits)
+  if (a.reward && i0 == 0) {
+    double sx = 0, sy = 0;
+    for (int j = tid; j < N; j += kThreads) {
+      sx += xs[j].vx;
+      sy += xs[j].vy;
     }
+    const double mx = block_sum(sx, red) / static_cast<double>(N), my = block_sum(sy, red) / static_cast<double>(N);
+    double qx = 0, qy = 0;
+    for (int j = tid; j < N; j += kThreads) {
+      const double ex = xs[j].vx - mx, ey = xs[j].vy - my;
+      qx += ex * ex;
+      qy += ey * ey;
+    }
+    const double Qx = block_sum(qx, red), Qy = block_sum(qy, red);
+    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
   }
-  // per-row outputs and the reward from the post-update states (x_out already written)
-  StepArgs e = a;
-  e.x_in = a.x_out;
-  e.T = 0;
-  step_epilogue<false, UF64, false, false, false>(e, nullptr, red, me, f0, f1, f2, f3, f4, f5, 0.0, 0.0, 0.0,
-                                                  0.0, b, i0, i0 + fr, frow && fs == 0, S, tid);
 }
 
 }  // namespace
@@ -2043,19 +2053,14 @@ size_t grid_bytes_per_env(int N) { return grid_layout(N).stride; }
 
 template <bool UF64>
 static hipError_t launch_step_grid_t(const StepArgs& a, hipStream_t s) {
-  const size_t prep_lds = (2 * (size_t)a.N + 1) * sizeof(int);
-  static std::atomic<uint64_t> attr_p{0};
-  // its static LDS (~5 KiB) plus the dynamic cell arrays must fit the 160 KiB of a CU:
-  // the attribute covers N <= kGridMaxN
-  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_grid_prep_kernel<UF64>), attr_p,
-                                        (int)((2 * (size_t)kGridMaxN + 1) * sizeof(int)));
-      e != hipSuccess)
-    return e;
-  hipLaunchKernelGGL(flock_grid_prep_kernel<UF64>, dim3(a.B), dim3(kPrepThreads), prep_lds, s, a);
-  if (const hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  const size_t Wn = (a.N + 63) / 64;
-  const size_t lds = (size_t)a.R * sizeof(St) + (size_t)a.R * Wn * 8 + 8 * sizeof(double) +
-                     (((size_t)a.R + 3) & ~(size_t)3) * 4 + (7 * (size_t)a.R + 1) * 4;
+  const size_t BN = (size_t)a.B * a.N;
+  hipLaunchKernelGGL(flock_grid_bin_kernel<UF64>, dim3((BN + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(flock_grid_scan_kernel, dim3(a.B), dim3(kScanThreads), 0, s, a);
+  hipLaunchKernelGGL(flock_grid_scatter_kernel, dim3((BN + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a);
+  const size_t nbk = (size_t)a.B * (grid_layout(a.N).NB + 1);  // one wave per bucket, at most 8 per CU slot
+  hipLaunchKernelGGL(flock_grid_order_kernel, dim3(std::min<size_t>((nbk + 3) / 4, 8192)), dim3(kThreads), 0, s, a);
+  const size_t Wn = (a.N + 63) / 64, R = a.R;
+  const size_t lds = R * Wn * 8 + 6 * R * 8 + 8 * sizeof(double) + ((R + 3) & ~(size_t)3) * 4 + 18 * R * 4;
   static std::atomic<uint64_t> attr_s{0};
   if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_grid_step_kernel<UF64>), attr_s,
                                         160 * 1024);

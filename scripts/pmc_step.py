@@ -21,8 +21,16 @@ h.set_state(synthetic_batch(B, N))
 h.set_actions(np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
 if os.environ.get("DIAG"):  # ablation switches: diagnostic build only (GYMFLOCK_LIB=build/lib_diag/...)
     h.diag_switches(int(os.environ["DIAG"], 0))
+# MODE: "plain" (default), "ctrl" (closed loop: step + fused controller), "packed"
+MODE = os.environ.get("MODE", "plain")
+flags = nat.FE_U_RESIDENT | (nat.FE_WITH_KNN if KNN else 0)
+if MODE == "ctrl":
+    h.controller()
+    flags = nat.FE_U_EXPERT | nat.FE_WITH_CONTROLLER
+elif MODE == "packed":
+    flags |= nat.FE_PACKED_NETWORK
 for _ in range(STEPS):
-    h.step(None, nat.FE_U_RESIDENT | (nat.FE_WITH_KNN if KNN else 0))
+    h.step(None, flags)
 if os.environ.get("FILL"):
     h.diag_fill(os.environ["FILL"] == "nt", STEPS)
 h.sync()

@@ -6,7 +6,7 @@ O=gpurun_out/r03s5; mkdir -p $O; export TMPDIR=/tmp
 set -o pipefail
 timeout -k 10 600 python -u -m pytest tests/test_grid_step_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_grid.log 2>&1 || { tail -40 $O/pytest_grid.log; exit 1; }
 tail -1 $O/pytest_grid.log
-ROUNDS=2 timeout -k 10 600 bash scripts/ab_n8192_libs.sh old tree > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+ROUNDS=3 timeout -k 10 600 bash scripts/ab_n8192_libs.sh old tree > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
 cat $O/ab.txt
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof8192 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --n-agents 8192 --n-envs 32 --steps 20 --warmup 3 --no-cpu-baseline --no-controller-line --no-packed-line --no-knn-line > $GRAFT_REPO_ROOT/$O/prof8192.log 2>&1 || { tail $GRAFT_REPO_ROOT/$O/prof8192.log; exit 1; }
