@@ -254,8 +254,7 @@ def bench_config5(args):
     out = {"metric": "agent-steps/sec, FlockingRelative N=8192", "value": N * B * K / el, "unit": "agent-steps/s",
            "steps": K, "warmup": W, "clock_warmup": warm, "ms_per_step": 1e3 * el / K,
            "config": {"workload": "FlockingRelative-v0 step(), N=8192 agents x 32 envs (BASELINE.json configs[4])"},
-           "roofline": flock_roofline(N, B, kms, 2, kernel="flock_grid_prep_kernel + flock_grid_step_kernel "
-                                                          "(cell-list step for N >= 4096)")}
+           "roofline": flock_roofline(N, B, kms, 2, kernel="flock_step_kernel<DYN,f32 u,PF> (tiles prefetched one ahead)")}
     if not args.no_cpu_baseline:
         log("cpu baseline N=8192 (cpu_ref, 1 step)...")
         rate, steps, sec = cpu_ref_rate(N, 1.0, max_steps=1)

@@ -77,7 +77,6 @@ struct fe_handle {
   int ccur = 0;
   float* sv = nullptr;
   float* net = nullptr;
-  unsigned char* grid = nullptr;        // (B, grid_bytes_per_env) cell lists (wide envs)
   double* reward_ring = nullptr;        // kRewardSlots x B
   int rslot = 0;
   // kNN outputs, one pair per state buffer: knn_idx[i] / knn_obs[i] belong to x[i], so
@@ -231,7 +230,7 @@ void release(fe_handle* h) {
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
                   h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
-                  h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1], h->grid};
+                  h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -341,7 +340,6 @@ gf::StepArgs base_args(fe_handle* h) {
   a.centralized = h->cfg.centralized;
   a.diag = h->diag;
   a.prefetch = h->prefetch;
-  a.grid = h->grid;
   a.u_scale = h->cfg.action_scalar;
   a.us_f = a.as_f;
   a.x_scale = 1.0;
@@ -377,7 +375,6 @@ gf::StepArgs env_range(const fe_handle* h, const gf::StepArgs& a, int b0, int nb
   if (a.reward) r.reward = a.reward + b0;
   if (a.dt_env) r.dt_env = a.dt_env + b0;
   if (a.adj_bits) r.adj_bits = a.adj_bits + e0 * Wn;
-  if (a.grid) r.grid = a.grid + (size_t)b0 * gf::grid_bytes_per_env(N);
   if (a.degree_out) r.degree_out = a.degree_out + e0;
   if (a.knn_idx) {
     const size_t K = h->cfg.n_neighbors;
@@ -612,8 +609,7 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
       (rc = dalloc(&h->knn_obs[1], h->BN * 4 * cfg->n_neighbors)) ||
       (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_r2[0], h->BN)) || (rc = dalloc(&h->knn_r2[1], h->BN)))) ||
       (cfg->n_neighbors > 0 && ((rc = dalloc(&h->knn_rimflag[0], B * ((N + 255) / 256))) ||
-                                (rc = dalloc(&h->knn_rimflag[1], B * ((N + 255) / 256))))) ||
-      ((int)N >= gf::kGridMinN && (int)N <= 16384 && (rc = dalloc(&h->grid, B * gf::grid_bytes_per_env((int)N))))) {
+                                (rc = dalloc(&h->knn_rimflag[1], B * ((N + 255) / 256)))))) {
     release(h);
     return rc;
   }
@@ -635,7 +631,6 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
     return fail_hip("event create", e);
   }
   if ((e = hipMemsetAsync(h->reward_ring, 0, sizeof(double) * kRewardSlots * B, h->stream)) != hipSuccess ||
-      (h->grid && (e = hipMemsetAsync(h->grid, 0, B * gf::grid_bytes_per_env((int)N), h->stream)) != hipSuccess) ||
       (e = clear_knn_history(h)) != hipSuccess ||
       (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
     release(h);

@@ -41,9 +41,6 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #ifndef GF_INLINE_RIM_U  // fused kNN inline rim scan: columns in flight per lane
 #define GF_INLINE_RIM_U 4
 #endif
-#ifndef GF_GRID_MIN_N  // envs of at least this many agents take the cell-list step
-#define GF_GRID_MIN_N 4096
-#endif
 #ifndef GF_KNN_SLICE_LIST  // fused kNN: keys each feature-pass slice keeps (A/B builds)
 #define GF_KNN_SLICE_LIST 7
 #endif
@@ -97,8 +94,6 @@ struct StepArgs {
   float us_f, uc_f;       // float32 copies of u_scale, u_clip
   const double* dt_env;   // (B) per-env dt of this step, or nullptr (dt)
   uint64_t* adj_bits;     // (B,N,Wn) packed adjacency or nullptr
-  unsigned char* grid;    // (B x grid_bytes_per_env(N)) cell lists of the wide-env step, or
-                          // nullptr: the tiled all-pairs step
   int32_t* degree_out;    // (B,N) degrees or nullptr
   // Flocking-v0 k-nearest selection fused into the feature pass (kStepFusedK neighbours):
   // rows the step can rank exactly get idx + obs; the others get idx[row*K] = -1 and
@@ -147,11 +142,7 @@ int step_tile(int N);
 size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn);
 
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s);
-// Wide envs (N >= kGridMinN): the plain step through per-env cell lists (two launches:
-// flock_grid_prep_kernel, flock_grid_step_kernel); launch_step takes that path itself
-// when StepArgs.grid is set and the step is a plain one.
-constexpr int kGridMinN = GF_GRID_MIN_N;
-size_t grid_bytes_per_env(int N);
+
 // Whether a step of this geometry can carry the fused k-nearest selection (K ==
 // kStepFusedK, no variant, no tile prefetch, at least K word-slices per row).
 bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch);

@@ -1654,323 +1654,6 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------------
-// Wide envs (N >= kGridMinN): a hashed cell list instead of the all-pairs tile loop.
-//
-// The tiled step stages the whole env into LDS for every row block and compares every
-// row with every column: at N = 8192 each 16-row block re-reads 8192 agents (4.3 GB of
-// L2 -> LDS per step at config 5) and 80 % of a workgroup's life is that loop (phase
-// timeline, profiles/r03). Here, per step and env:
-//  * flock_grid_bin_kernel (one thread per agent): the double-integrator update (writes
-//    x_out), the agent's cell (cx, cy) = floor(p / hc), hc = max(cr, sqrt(cr)) plus a
-//    rounding margin, hashed into NB >= N buckets; its rank in the bucket by a global
-//    atomic. Non-finite or huge coordinates mark the env "full" (every agent is a
-//    candidate of every row).
-//  * flock_grid_scan_kernel (one workgroup per env): exclusive scan of the bucket counts
-//    (zeroed for the next step); flock_grid_scatter_kernel puts every agent (index and
-//    state) at its bucket's start + rank; flock_grid_order_kernel writes each bucket's
-//    agents again, ordered by index (one wave per bucket), so the candidates' order, and
-//    with it every sum, is deterministic.
-//  * flock_grid_step_kernel: each row's candidates are the agents of the buckets of the
-//    3 x 3 cells around its own (every agent closer than hc lies there; a bucket shared by
-//    two of those cells is read once; hash collisions only add candidates). Adjacency is
-//    the reference's float64 r2 = dx*dx + dy*dy < cr^2 (no FMA), so the bits are exactly
-//    the tiled step's; a wave takes a row, its lanes the candidates, and the features are
-//    summed per lane then across the wave (fixed order: deterministic). The rows' dense
-//    network is stored as the tiled step stores it (one contiguous range per block).
-constexpr int kGridMaxN = 16384;  // ranks and bucket counts of the cell-list step stay small
-constexpr int kScanThreads = 256;  // small workgroups: they slip in beside a running step
-constexpr int kScanMaxPer = 65;    // (NB + 1) / kScanThreads rounded up, NB <= 16384
-
-struct GridLayout {
-  size_t cnt, start, bin, rank, idx, st, idx2, st2, stride;  // byte offsets; NB buckets (+1: overflow)
-  int NB;
-};
-__host__ __device__ inline GridLayout grid_layout(int N) {
-  GridLayout g;
-  int nb = 64;
-  while (nb < N) nb <<= 1;
-  g.NB = nb;
-  g.cnt = 64;                                        // int cnt[NB + 1] (zero between steps)
-  g.start = g.cnt + 4 * ((size_t)nb + 1);            // int start[NB + 2]
-  g.bin = g.start + 4 * ((size_t)nb + 2);            // int bin[N]
-  g.rank = g.bin + 4 * (size_t)N;                    // int rank[N]
-  g.idx = g.rank + 4 * (size_t)N;                    // int idx[N] (bucket order)
-  g.st = (g.idx + 4 * (size_t)N + 31) & ~(size_t)31; // St st[N] (bucket order)
-  g.idx2 = g.st + 32 * (size_t)N;                    // int idx2[N] (bucket order, by index)
-  g.st2 = (g.idx2 + 4 * (size_t)N + 31) & ~(size_t)31;  // St st2[N]
-  g.stride = (g.st2 + 32 * (size_t)N + 255) & ~(size_t)255;
-  return g;
-}
-
-__device__ __forceinline__ double grid_inv_cell(const StepArgs& a) {
-  return 1.0 / (fmax(a.cr, sqrt(a.cr)) * (1.0 + 1.0e-7) + 1.0e-290);
-}
-__device__ __forceinline__ int grid_hash(long long cx, long long cy, int nb) {
-  const unsigned long long h = static_cast<unsigned long long>(cx) * 0x9E3779B97F4A7C15ull ^
-                               static_cast<unsigned long long>(cy) * 0xC2B2AE3D27D4EB4Full;
-  return static_cast<int>((h ^ (h >> 29)) & static_cast<unsigned long long>(nb - 1));
-}
-
-template <bool UF64>
-__global__ __launch_bounds__(kThreads) void flock_grid_bin_kernel(StepArgs a) {
-  const int N = a.N;
-  const size_t g = (size_t)blockIdx.x * kThreads + threadIdx.x;
-  if (g >= (size_t)a.B * N) return;
-  const int b = static_cast<int>(g / N), j = static_cast<int>(g - (size_t)b * N);
-  const GridLayout gl = grid_layout(N);
-  unsigned char* gb = a.grid + (size_t)b * gl.stride;
-  const St s = load_state<true, UF64>(a, g);
-  double2* xo = reinterpret_cast<double2*>(a.x_out) + 2 * g;
-  xo[0] = double2{s.px, s.py};
-  xo[1] = double2{s.vx, s.vy};
-  const double ih = grid_inv_cell(a);
-  int bk = gl.NB;  // overflow bucket
-  if (fabs(s.px) <= 1.0e12 && fabs(s.py) <= 1.0e12) {
-    bk = grid_hash(static_cast<long long>(floor(s.px * ih)), static_cast<long long>(floor(s.py * ih)), gl.NB);
-  } else {
-    atomicOr(reinterpret_cast<int*>(gb), 1);  // the env is "full" (flag word 0, see the sort)
-  }
-  int* cnt = reinterpret_cast<int*>(gb + gl.cnt);
-  reinterpret_cast<int*>(gb + gl.bin)[j] = bk;
-  reinterpret_cast<int*>(gb + gl.rank)[j] = atomicAdd(&cnt[bk], 1);
-}
-
-// exclusive scan of the env's bucket counts into start[0..NB+1] (and the counts zeroed
-// for the next step); this step's "full" flag for the step kernel (word 1), word 0 re-armed
-__global__ __launch_bounds__(kScanThreads) void flock_grid_scan_kernel(StepArgs a) {
-  const int N = a.N, b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const GridLayout gl = grid_layout(N);
-  unsigned char* gb = a.grid + (size_t)b * gl.stride;
-  int* cnt = reinterpret_cast<int*>(gb + gl.cnt);
-  int* start = reinterpret_cast<int*>(gb + gl.start);
-  const int nbk = gl.NB + 1;
-  __shared__ int wsum[2][kScanThreads / 64];
-  if (tid == 0) {
-    reinterpret_cast<int*>(gb)[1] = reinterpret_cast<int*>(gb)[0];
-    reinterpret_cast<int*>(gb)[0] = 0;
-  }
-  const int per = (nbk + kScanThreads - 1) / kScanThreads;
-  const int c0 = min(nbk, tid * per), c1 = min(nbk, c0 + per);
-  int v[kScanMaxPer];
-  int local = 0;
-#pragma unroll
-  for (int k = 0; k < kScanMaxPer; ++k) {
-    v[k] = c0 + k < c1 ? cnt[c0 + k] : 0;
-    local += v[k];
-  }
-  int incl = local;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(incl, o);
-    if (lane >= o) incl += t;
-  }
-  if (lane == 63) wsum[0][wid] = incl;
-  __syncthreads();
-  if (wid == 0) {
-    const int wt = lane < kScanThreads / 64 ? wsum[0][lane] : 0;
-    int wi = wt;
-#pragma unroll
-    for (int o = 1; o < kScanThreads / 64; o <<= 1) {
-      const int t = __shfl_up(wi, o);
-      if (lane >= o) wi += t;
-    }
-    if (lane < kScanThreads / 64) wsum[1][lane] = wi - wt;
-  }
-  __syncthreads();
-  int run = wsum[1][wid] + incl - local;
-#pragma unroll
-  for (int k = 0; k < kScanMaxPer; ++k) {
-    if (c0 + k < c1) {
-      start[c0 + k] = run;
-      cnt[c0 + k] = 0;
-      run += v[k];
-    }
-  }
-  if (c1 == nbk && c0 < c1) start[nbk] = run;
-}
-
-// every agent to its slot: start of its bucket + its rank there
-__global__ __launch_bounds__(kThreads) void flock_grid_scatter_kernel(StepArgs a) {
-  const int N = a.N;
-  const size_t g = (size_t)blockIdx.x * kThreads + threadIdx.x;
-  if (g >= (size_t)a.B * N) return;
-  const int b = static_cast<int>(g / N), j = static_cast<int>(g - (size_t)b * N);
-  const GridLayout gl = grid_layout(N);
-  unsigned char* gb = a.grid + (size_t)b * gl.stride;
-  const int q = reinterpret_cast<const int*>(gb + gl.start)[reinterpret_cast<const int*>(gb + gl.bin)[j]] +
-                reinterpret_cast<const int*>(gb + gl.rank)[j];
-  reinterpret_cast<int*>(gb + gl.idx)[q] = j;
-  reinterpret_cast<St*>(gb + gl.st)[q] = reinterpret_cast<const St*>(a.x_out)[g];
-}
-
-// each bucket's agents by index (the atomics of the binning ranked them in any order),
-// into the second pair of arrays: one wave per bucket, each lane takes entries l, l+64,
-// ... and counts the bucket's smaller indices (agent indices are distinct)
-__global__ __launch_bounds__(kThreads) void flock_grid_order_kernel(StepArgs a) {
-  const int N = a.N;
-  const GridLayout gl = grid_layout(N);
-  const int nbk = gl.NB + 1;
-  const int lane = threadIdx.x & 63;
-  const size_t wv = ((size_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
-  const size_t nwv = ((size_t)gridDim.x * kThreads) >> 6;
-  for (size_t g = wv; g < (size_t)a.B * nbk; g += nwv) {
-    const int b = static_cast<int>(g / nbk), c = static_cast<int>(g - (size_t)b * nbk);
-    const unsigned char* gb = a.grid + (size_t)b * gl.stride;
-    const int* start = reinterpret_cast<const int*>(gb + gl.start);
-    const int q0 = start[c], n = start[c + 1] - q0;
-    if (n == 0) continue;
-    const int* idx = reinterpret_cast<const int*>(gb + gl.idx) + q0;
-    const St* st = reinterpret_cast<const St*>(gb + gl.st) + q0;
-    int* idx2 = reinterpret_cast<int*>(a.grid + (size_t)b * gl.stride + gl.idx2) + q0;
-    St* st2 = reinterpret_cast<St*>(a.grid + (size_t)b * gl.stride + gl.st2) + q0;
-    for (int k = lane; k < n; k += 64) {
-      const int key = idx[k];
-      int rk = 0;
-      for (int m = 0; m < n; ++m) rk += idx[m] < key ? 1 : 0;
-      idx2[rk] = key;
-      st2[rk] = st[k];
-    }
-  }
-}
-
-#ifndef GF_GRID_WAVES  // waves per SIMD the cell-list step's registers allow
-#define GF_GRID_WAVES 8
-#endif
-
-template <bool UF64>
-__global__ __launch_bounds__(kThreads, GF_GRID_WAVES) void flock_grid_step_kernel(StepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = a.N, R = a.R, Wn = (N + 63) >> 6;
-  const int L = xcd_remap_reward_first(blockIdx.x, gridDim.x, a.bpe);
-  const int b = L / a.bpe;
-  const int i0 = (L - b * a.bpe) * R;
-  const int nrows = min(R, N - i0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const size_t env0 = (size_t)b * N;
-  uint64_t* adj = reinterpret_cast<uint64_t*>(smem);                    // R x Wn
-  double* fsum = reinterpret_cast<double*>(adj + (size_t)R * Wn);       // R x 6 feature sums
-  double* red = fsum + 6 * R;                                           // 8
-  float* inv = reinterpret_cast<float*>(red + 8);                       // R
-  int* seg = reinterpret_cast<int*>(inv + ((R + 3) & ~3));              // R x 9 x (start, count)
-  const St* xs = reinterpret_cast<const St*>(a.x_out) + env0;           // post-update states
-  const GridLayout gl = grid_layout(N);
-  const unsigned char* gb = a.grid + (size_t)b * gl.stride;
-  const bool full = reinterpret_cast<const int*>(gb)[1] != 0;
-  const int* start = reinterpret_cast<const int*>(gb + gl.start);
-  const int* sidx = reinterpret_cast<const int*>(gb + gl.idx2);
-  const St* sst = reinterpret_cast<const St*>(gb + gl.st2);
-
-  for (int k = tid; k < R * Wn; k += kThreads) adj[k] = 0ull;
-  // the 9 cells' buckets of every row, looked up by 9R threads at once; a bucket that
-  // an earlier cell of the same row already names is left out
-  for (int t = tid; t < 9 * nrows; t += kThreads) {
-    const int r = t / 9, d = t - 9 * r;
-    int s0 = 0, n0 = 0;
-    if (full) {
-      n0 = d == 0 ? N : 0;
-    } else {
-      const St me = xs[i0 + r];
-      const double ih = grid_inv_cell(a);
-      const long long cx = static_cast<long long>(floor(me.px * ih)), cy = static_cast<long long>(floor(me.py * ih));
-      int bk[9];
-#pragma unroll
-      for (int e = 0; e < 9; ++e) bk[e] = grid_hash(cx + e % 3 - 1, cy + e / 3 - 1, gl.NB);
-      bool dup = false;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) dup |= e < d && bk[e] == bk[d];
-      if (!dup) {
-        s0 = start[bk[d]];
-        n0 = start[bk[d] + 1] - s0;
-      }
-    }
-    seg[2 * t] = s0;
-    seg[2 * t + 1] = n0;
-  }
-  __syncthreads();
-  // adjacency and features: wave w takes rows w, w+4, ...; lane l the candidates l, l+64,
-  // ... of the row's segments (in bucket order), float64 decisions as the reference's
-  for (int r = wid; r < nrows; r += 4) {
-    const St me = xs[i0 + r];
-    const int* sg = seg + 18 * r;
-    int cum[10];
-    cum[0] = 0;
-#pragma unroll
-    for (int e = 0; e < 9; ++e) cum[e + 1] = cum[e] + sg[2 * e + 1];
-    const int tot = cum[9], self = i0 + r;
-    uint64_t* arow = adj + (size_t)r * Wn;
-    double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0;
-    int sgs[9];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) sgs[e] = sg[2 * e] - cum[e];
-    for (int k = lane; k < tot; k += 64) {
-      int q = 0;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) q = (k >= cum[e] && k < cum[e + 1]) ? sgs[e] + k : q;
-      const int j = sidx[q];
-      const St o = sst[q];
-      const double dx = me.px - o.px, dy = me.py - o.py;
-      const double r2 = dx * dx + dy * dy;
-      if (r2 < a.cr2 && j != self) {
-        atomicOr(reinterpret_cast<unsigned long long*>(arow + (j >> 6)), 1ull << (j & 63));
-        const double ir = 1.0 / r2, irr = ir * ir;
-        f0 += me.vx - o.vx;
-        f1 += dx * irr;
-        f2 += dx * ir;
-        f3 += me.vy - o.vy;
-        f4 += dy * irr;
-        f5 += dy * ir;
-      }
-    }
-    f0 = wave_sum(f0);
-    f1 = wave_sum(f1);
-    f2 = wave_sum(f2);
-    f3 = wave_sum(f3);
-    f4 = wave_sum(f4);
-    f5 = wave_sum(f5);
-    if (lane == 0) {
-      double* fs = fsum + 6 * r;
-      fs[0] = f0, fs[1] = f1, fs[2] = f2, fs[3] = f3, fs[4] = f4, fs[5] = f5;
-    }
-  }
-  __syncthreads();
-  // degrees -> 1/deg (S slices per row), then the rows' dense network
-  const int S = kThreads / R;
-  const int fr = tid / S, fs_ = tid - fr * S;
-  const bool frow = fr < nrows;
-  {
-    const int wpt = (Wn + S - 1) / S;
-    const int wb = fs_ * wpt, we = min(Wn, wb + wpt);
-    int deg = 0;
-    if (frow)
-      for (int w = wb; w < we; ++w) deg += __popcll(adj[(size_t)fr * Wn + w]);
-    with_slices(S, [&](auto Sc) { deg = group_sum_c<decltype(Sc)::value>(deg); });
-    if (frow && fs_ == 0) inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
-  }
-  __syncthreads();
-  if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
-  if (a.state_values && tid < 6 * nrows) a.state_values[(env0 + i0) * 6 + tid] = static_cast<float>(fsum[tid]);
-  // the reward (instant_cost :145-147) by the env's first block, from the post-update
-  // velocities in the tiled step's summation order (the same bits)
-  if (a.reward && i0 == 0) {
-    double sx = 0, sy = 0;
-    for (int j = tid; j < N; j += kThreads) {
-      sx += xs[j].vx;
-      sy += xs[j].vy;
-    }
-    const double mx = block_sum(sx, red) / static_cast<double>(N), my = block_sum(sy, red) / static_cast<double>(N);
-    double qx = 0, qy = 0;
-    for (int j = tid; j < N; j += kThreads) {
-      const double ex = xs[j].vx - mx, ey = xs[j].vy - my;
-      qx += ex * ex;
-      qy += ey * ey;
-    }
-    const double Qx = block_sum(qx, red), Qy = block_sum(qy, red);
-    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
-  }
-}
-
 }  // namespace
 
 // ----------------------------------------------------------------------------- host
@@ -2049,34 +1732,7 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
 }
 
 
-size_t grid_bytes_per_env(int N) { return grid_layout(N).stride; }
-
-template <bool UF64>
-static hipError_t launch_step_grid_t(const StepArgs& a, hipStream_t s) {
-  const size_t BN = (size_t)a.B * a.N;
-  hipLaunchKernelGGL(flock_grid_bin_kernel<UF64>, dim3((BN + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL(flock_grid_scan_kernel, dim3(a.B), dim3(kScanThreads), 0, s, a);
-  hipLaunchKernelGGL(flock_grid_scatter_kernel, dim3((BN + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a);
-  const size_t nbk = (size_t)a.B * (grid_layout(a.N).NB + 1);  // one wave per bucket, at most 8 per CU slot
-  hipLaunchKernelGGL(flock_grid_order_kernel, dim3(std::min<size_t>((nbk + 3) / 4, 8192)), dim3(kThreads), 0, s, a);
-  const size_t Wn = (a.N + 63) / 64, R = a.R;
-  const size_t lds = R * Wn * 8 + 6 * R * 8 + 8 * sizeof(double) + ((R + 3) & ~(size_t)3) * 4 + 18 * R * 4;
-  static std::atomic<uint64_t> attr_s{0};
-  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_grid_step_kernel<UF64>), attr_s,
-                                        160 * 1024);
-      e != hipSuccess)
-    return e;
-  hipLaunchKernelGGL(flock_grid_step_kernel<UF64>, dim3(a.B * a.bpe), dim3(kThreads), lds, s, a);
-  return hipGetLastError();
-}
-
-bool step_grid_ok(const StepArgs& a, bool dyn, bool ctrl) {
-  return a.grid && dyn && !ctrl && !a.knn_idx && !a.variant && !a.adj_bits && !a.degree_out && a.N <= kGridMaxN &&
-         kThreads % a.R == 0 && kThreads / a.R <= 64;
-}
-
 hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipStream_t s) {
-  if (step_grid_ok(a, dyn, ctrl)) return u_f64 ? launch_step_grid_t<true>(a, s) : launch_step_grid_t<false>(a, s);
   if (dyn) {
     if (u_f64) return ctrl ? launch_step_t<true, true, true>(a, s) : launch_step_t<true, true, false>(a, s);
     return ctrl ? launch_step_t<true, false, true>(a, s) : launch_step_t<true, false, false>(a, s);

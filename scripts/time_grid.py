@@ -16,6 +16,8 @@ N, B = int(os.environ.get("N", 8192)), int(os.environ.get("B", 32))
 K = int(os.environ.get("K", 20))
 env = VecFlockingRelative(B, N)
 env.h.set_streams(int(os.environ.get("STREAMS", 2)))
+if os.environ.get("DIAG"):  # ablation switches (diagnostic build: GYMFLOCK_LIB=build/lib_diag/...)
+    env.h.diag_switches(int(os.environ["DIAG"], 0))
 x0 = env.reset(seed=0)
 env.set_actions(np.random.RandomState(1234).uniform(-1, 1, size=(B, N, 2)).astype(np.float32))
 t0 = time.perf_counter()
@@ -32,5 +34,6 @@ for _ in range(K):
     env.step(resident=True)
 env.sync()
 el = time.perf_counter() - t0
-print("N=%d B=%d streams=%s: %.1f us/step" % (N, B, os.environ.get("STREAMS", 2), 1e6 * el / K))
+print("N=%d B=%d streams=%s diag=%s: %.1f us/step" % (N, B, os.environ.get("STREAMS", 2), os.environ.get("DIAG", "0"),
+                                                     1e6 * el / K))
 env.close()

@@ -1,11 +1,12 @@
-"""Parity of the wide-env cell-list step (flock_grid_prep_kernel + flock_grid_step_kernel,
-taken by plain steps at N >= 4096) against the CPU oracle and against the tiled
-all-pairs kernel (which steps with the fused controller still take).
+"""Wide envs (N = 4096, 8192: many LDS tiles, the prefetching tiled kernel) against the
+CPU oracle on awkward layouts: a far outlier, a coordinate beyond any float32 band
+(every pair decided in float64), 600 coincident agents plus a pile jittered below 1e-9,
+all agents on one line; float32 and float64 actions; and the plain step at config 5's
+full size with sampled rows (tests/test_flock_gpu.py covers config 5 with the fused
+controller).
 
 Tolerances as tests/test_flock_gpu.py: state and network bit-exact, state_values
-|d| <= 1e-5 |ref| + 1e-9, reward rtol 1e-12. Against the tiled kernel on the same input:
-network and reward bit-exact (same decisions, same reward summation order),
-state_values within 1e-12 (the feature sums run in another order)."""
+|d| <= 1e-5 |ref| + 1e-9, reward rtol 1e-12."""
 import numpy as np
 import pytest
 
@@ -35,7 +36,7 @@ def check_env(h, b, x0, u, rows=None):
 
 
 @pytest.mark.parametrize("u64", [False, True])
-def test_grid_step_vs_oracle_n4096(u64):
+def test_wide_step_vs_oracle_n4096(u64):
     n, B = 4096, 3
     x0 = synthetic_batch(B, n, seed0=900)
     u = np.random.RandomState(901).uniform(-1, 1, size=(B, n, 2))
@@ -52,20 +53,20 @@ def _edge_states(n):
     rs = np.random.RandomState(902)
     base = synthetic_batch(1, n, seed0=903)[0]
     far = base.copy()
-    far[7, :2] = [1.0e4, -3.0e4]            # a far outlier: the span needs bigger cells
+    far[7, :2] = [1.0e4, -3.0e4]            # a far outlier
     huge = base.copy()
-    huge[11, 0] = 5.0e13                    # beyond the grid's range: the env is one cell
+    huge[11, 0] = 5.0e13                    # past the float32 prefilter's range: float64 pairs
     pile = base.copy()
-    pile[:600, :2] = pile[0, :2]            # 600 coincident agents (one crowded cell)
+    pile[:600, :2] = pile[0, :2]            # 600 coincident agents
     pile[600:900, :2] = pile[600, :2] + rs.uniform(-1e-9, 1e-9, size=(300, 2))
     line = base.copy()
-    line[:, 1] = 0.0                        # all agents on a line (a one-row grid)
+    line[:, 1] = 0.0                        # all agents on a line
     line[:, 0] = np.linspace(-50, 50, n)
     return {"far": far, "huge": huge, "pile": pile, "line": line}
 
 
 @pytest.mark.parametrize("case", ["far", "huge", "pile", "line"])
-def test_grid_step_edge_layouts(case):
+def test_wide_step_edge_layouts(case):
     n = 4096
     x0 = _edge_states(n)[case]
     u = np.random.RandomState(904).uniform(-1, 1, size=(1, n, 2)).astype(np.float32)
@@ -81,36 +82,8 @@ def test_grid_step_edge_layouts(case):
     h.close()
 
 
-def test_grid_step_matches_tiled_kernel_n8192():
-    """4 envs x N=8192 (split into two launches per step): the cell-list step's network
-    equals the tiled kernel's bit for bit over the whole batch (the tiled kernel runs
-    when the step also asks for the controller), its reward too, and sampled rows match
-    the oracle; three consecutive steps keep the state chain bit-exact."""
-    n, B = 8192, 4
-    x0 = synthetic_batch(B, n, seed0=905)
-    rs = np.random.RandomState(906)
-    us = [rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32) for _ in range(3)]
-    hg, ht = nat.FlockHandle(n, B), nat.FlockHandle(n, B)
-    hg.set_state(x0)
-    ht.set_state(x0)
-    x = x0.copy()
-    for t in range(3):
-        hg.step(us[t])
-        ht.step(us[t], nat.FE_WITH_CONTROLLER)
-        for b in range(B):
-            x[b] = orc.integrate(x[b], us[t][b])
-        np.testing.assert_array_equal(hg.get_state(), x)
-        np.testing.assert_array_equal(ht.get_state(), x)
-    np.testing.assert_array_equal(hg.rewards(), ht.rewards())
-    for b in range(B):
-        np.testing.assert_array_equal(hg.network(b), ht.network(b))
-        np.testing.assert_allclose(hg.state_values(b), ht.state_values(b), rtol=1e-12, atol=1e-12)
-    hg.close()
-    ht.close()
-
-
-def test_grid_step_config5_sampled_oracle():
-    """BASELINE.json configs[4] (32 envs x N=8192) through the cell-list step: every env's
+def test_plain_step_config5_sampled_oracle():
+    """BASELINE.json configs[4] (32 envs x N=8192), the bench's plain step: every env's
     state bit-exact and reward (rtol 1e-12); sampled rows of 3 envs against the oracle."""
     n, B = 8192, 32
     x0 = synthetic_batch(B, n, seed0=907)
