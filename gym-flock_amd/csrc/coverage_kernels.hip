@@ -19,6 +19,9 @@ namespace gf {
 namespace {
 
 constexpr int kCovThreads = 256;
+#ifndef GF_COV_TAGGED  // claim rounds tagged (no table clearing) or cleared (A/B builds)
+#define GF_COV_TAGGED 0
+#endif
 
 // Phase timeline (diagnostic builds only, -DGF_STAMPS): thread 0 of each workgroup
 // records s_memrealtime (100 MHz) at: start (0), first round trip done (1), claims done
@@ -274,19 +277,30 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
           r.fr = r.mv && !(claim[r.n >> 5] & (1u << (r.n & 31)));  // not a stayer's node
           r.v = r.n;  // guess: every move succeeds
         };
-        // branch-free rounds: a robot that does not move adds INT_MAX (no-op) and clears
-        // its own node, which no mover's test reads (movers onto it are blocked by its
-        // stay claim; robots past R sit on node 0, a robot slot no target uses)
+        // branch-free rounds: a robot that does not move adds INT_MAX (no-op).
+#if GF_COV_TAGGED
+        // Claims carry the round: (tag << 9) | robot, the tag falling by one per round, so
+        // atomicMin keeps this round's first claimer over any earlier round's, and an
+        // entry with another tag is no claim this round (no table clearing between rounds)
+        int tag = 1 << 12;
+        auto put = [&](const Rb& r) { atomicMin(&first[r.v], r.mv ? (tag << 9) | r.i : INT_MAX); };
+        auto eval = [&](Rb& r, int e) {
+          const int f = (e >> 9) == tag ? (e & 511) : INT_MAX;
+#else
+        // A mover's claim sits on its chosen node or its own; both are cleared between
+        // rounds (a non-mover's own node: no mover's test reads it, since movers onto it
+        // are blocked by its stay claim; robots past R sit on node 0, a slot no target uses)
         auto put = [&](const Rb& r) { atomicMin(&first[r.v], r.mv ? r.i : INT_MAX); };
+        auto clear = [&](const Rb& r) {
+          first[r.n] = INT_MAX;
+          first[r.c] = INT_MAX;
+        };
         auto eval = [&](Rb& r, int f) {
+#endif
           const int v = (r.fr && f >= r.i) ? r.n : r.c;  // r.fr implies r.mv
           const bool ch = v != r.v;
           r.v = v;
           return ch;
-        };
-        auto clear = [&](const Rb& r) {  // a mover's claim sits on its chosen node or its own
-          first[r.n] = INT_MAX;
-          first[r.c] = INT_MAX;
         };
         Rb r0, r1, r2, r3;
         init(r0, tid);
@@ -300,9 +314,13 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
           // all four evaluated (no short circuit)
           const int changed = int(eval(r0, f0)) | int(eval(r1, f1)) | int(eval(r2, f2)) | int(eval(r3, f3));
           if (!__any(changed)) break;
+#if GF_COV_TAGGED
+          --tag;  // at most R + 1 <= 257 rounds: the tag stays positive
+#else
           lds_fence();
           clear(r0), clear(r1), clear(r2), clear(r3);
           lds_fence();
+#endif
         }
         if (r0.i < R) new_s[r0.i] = r0.v;
         if (r1.i < R) new_s[r1.i] = r1.v;

@@ -28,7 +28,7 @@ if MODE == "ctrl":
     h.controller()
     flags = nat.FE_U_EXPERT | nat.FE_WITH_CONTROLLER
 elif MODE == "packed":
-    flags |= nat.FE_PACKED_NETWORK
+    flags |= nat.FE_PACKED_NETWORK | nat.FE_NO_NETWORK  # as bench.py network="packed"
 for _ in range(STEPS):
     h.step(None, flags)
 if os.environ.get("FILL"):
