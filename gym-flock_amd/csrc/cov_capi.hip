@@ -118,7 +118,7 @@ void cov_release(cov_handle* h) {
   gf::CovArgs& a = h->a;
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
-                  a.receivers, a.obs_step, a.axy, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT,
+                  a.receivers, a.obs_step, a.axy, a.nrec, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT,
                   h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
                   h->goff};
   for (void* p : bufs)
@@ -314,7 +314,7 @@ int cov_create(const cov_config* cfg, cov_handle** out) {
       (rc = calloc_dev(&a.step_counter, B)) || (rc = calloc_dev(&a.dirty, B)) || (rc = calloc_dev(&h->actions, B * R)) ||
       (rc = calloc_dev(&a.reward, B)) || (rc = calloc_dev(&a.done, B)) || (rc = calloc_dev(&a.nodes, B * M * 3)) ||
       (rc = calloc_dev(&a.edges, B * E)) || (rc = calloc_dev(&a.senders, B * E)) || (rc = calloc_dev(&a.receivers, B * E)) ||
-      (rc = calloc_dev(&a.obs_step, B)) || (rc = calloc_dev(&a.axy, B * Tm * 8)) || (rc = calloc_dev(&h->err, 1)) || (rc = calloc_dev(&h->start, B * R)) ||
+      (rc = calloc_dev(&a.obs_step, B)) || (rc = calloc_dev(&a.axy, B * Tm * 8)) || (rc = calloc_dev(&a.nrec, B * Tm * 16)) || (rc = calloc_dev(&h->err, 1)) || (rc = calloc_dev(&h->start, B * R)) ||
       (rc = calloc_dev(&h->visited0, B * Tm)) || (rc = calloc_dev(&h->envsel, B))) {
     cov_release(h);
     return rc;

@@ -31,6 +31,9 @@ struct CovArgs {
   int32_t* receivers;     // (B,4M)
   int64_t* obs_step;      // (B)
   double* axy;            // (B,Tmax,4,2) coordinates of each node's 4 action targets
+  float* nrec;            // (B,Tmax,16) per node, 64 B: its 4 action targets (global, padded
+                          // with itself; int4), the 4 action-edge features of a robot on it
+                          // (float4), its position (double2), 16 B pad
   int* err;               // device error bits: 1 degree > 4, 2 edges overflow, 4 bad action
 };
 

@@ -19,6 +19,12 @@ namespace gf {
 namespace {
 
 constexpr int kCovThreads = 256;
+#ifndef GF_COV_STEP_NT  // R <= 256: threads per env workgroup (A/B builds: 64 or 128 hold
+#define GF_COV_STEP_NT 256  // 4 or 2 robots per lane; one wave measured 8.9 vs 7.3 us)
+#endif
+#ifndef GF_COV_LDS_ORDER  // claim rounds: compiler-only ordering of the wave's LDS operations
+#define GF_COV_LDS_ORDER 1
+#endif
 #ifndef GF_COV_TAGGED  // claim rounds tagged (no table clearing) or cleared (A/B builds)
 #define GF_COV_TAGGED 0
 #endif
@@ -125,6 +131,26 @@ __global__ __launch_bounds__(kCovThreads) void cov_graph_kernel(CovArgs a, const
     const int q = ac < cnt[t] ? nbr[4 * t + ac] : t;
     axy[k] = make_double2(tg[2 * q], tg[2 * q + 1]);
   }
+  // per node, the record a robot moving onto it needs (one 64-byte line): its 4 action
+  // targets, the 4 action-edge features from its position (get_action_edges :206-232 with
+  // the robot on the node, exactly as the step's full pass computes them) and the position
+  float4* rec = reinterpret_cast<float4*>(a.nrec) + (size_t)b * Tm * 4;
+  for (int t = tid; t < T; t += kCovThreads) {
+    const int c = cnt[t], n = t + R;
+    const double px = tg[2 * t], py = tg[2 * t + 1];
+    int q[4];
+    float d[4];
+    for (int k = 0; k < 4; ++k) {
+      const int j = k < c ? nbr[4 * t + k] : t;
+      q[k] = k < c ? j + R : n;
+      d[k] = static_cast<float>(dist2d(px, py, tg[2 * j], tg[2 * j + 1]) / a.res);
+    }
+    const double2 xy = make_double2(px, py);
+    rec[4 * t] = make_float4(__int_as_float(q[0]), __int_as_float(q[1]), __int_as_float(q[2]), __int_as_float(q[3]));
+    rec[4 * t + 1] = make_float4(d[0], d[1], d[2], d[3]);
+    rec[4 * t + 2] = *reinterpret_cast<const float4*>(&xy);
+    rec[4 * t + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (tid == 0) {
     a.n_motion[b] = n_motion;
     a.dirty[b] = 1;  // a new graph: the next pass recomputes nodes and action edges
@@ -146,7 +172,9 @@ __device__ __forceinline__ int action_node(const int32_t* nbr, const int32_t* cn
 // node's position, visited flag, neighbours and their coordinates (cov_graph_kernel's
 // table) together, and rewrites its 8 tail edges; a robot that stayed keeps its edges.
 // After an external placement, a new graph or a reset, everything is recomputed.
-__global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
+  constexpr int RPT = kCovThreads / NT;  // robots per thread when R <= kCovThreads
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = a.env0 + blockIdx.x;
   const int R = a.R, M = a.M, Tm = a.Tmax, E = 4 * M;
@@ -172,33 +200,31 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
   float* edg = a.edges + (size_t)b * E;
   const int base = E - 8 * R;  // action edges: [base, base+4R) target->robot, then robot->target
 
-  for (int k = tid; k < W; k += kCovThreads) {
+  for (int k = tid; k < W; k += NT) {
     claim[k] = 0u;
     seen[k] = 0u;
   }
   if (a.actions)
-    for (int k = tid; k < M; k += kCovThreads) first[k] = INT_MAX;
+    for (int k = tid; k < M; k += NT) first[k] = INT_MAX;
   if (tid == 0) *counter = 0;
   GF_COV_STAMP(0);
-  // the env's words, loaded up front so none of them costs a round trip of its own
-  const bool dirty = a.dirty[b] != 0;
-  const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
-  const bool full = dirty || !a.actions;  // recompute every robot's action edges
   const int32_t* act = a.actions ? a.actions + (size_t)b * R : nullptr;
-  // One robot per thread (R <= kCovThreads): the data of the node a robot will end on
+  // One robot per thread (R <= NT): the data of the node a robot will end on
   // (if it moves: the chosen node; in a full pass: its node) is loaded right after the
   // chosen node is known, so that round trip runs under the claim resolution.
   const bool one = R <= kCovThreads;
-  int pn = -1;  // node whose data is in the registers below
-  double ptx = 0, pty = 0;
-  uint8_t pwas = 0;
-  int4 pq4 = make_int4(0, 0, 0, 0);
-  int pnc = 0;
-  double2 pc0{}, pc1{}, pc2{}, pc3{};
-  auto load_node = [&](int t, double& x, double& y, uint8_t& was, int4& q4, int& nc, double2& c0, double2& c1,
-                       double2& c2, double2& c3) {
-    x = tg[2 * t];
-    y = tg[2 * t + 1];
+  const float4* rec = reinterpret_cast<const float4*>(a.nrec) + (size_t)b * Tm * 4;
+  // per robot slot: the chosen node's record (n = -1: none)
+  struct Pf {
+    int n;
+    float4 r0, r1, r2;
+    uint8_t was;
+  };
+  Pf pf[RPT];
+  // a robot that stays in a full pass keeps its own position (xr, which after an external
+  // placement need not be its node's): its edges come from the coordinate table
+  auto load_node = [&](int t, uint8_t& was, int4& q4, int& nc, double2& c0, double2& c1, double2& c2,
+                       double2& c3) {
     was = vis[t];
     q4 = *reinterpret_cast<const int4*>(nbr + 4 * t);
     nc = cnt[t];
@@ -207,12 +233,35 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     c2 = axy[4 * t + 2];
     c3 = axy[4 * t + 3];
   };
-  for (int i = tid; i < R; i += kCovThreads) {
-    int c = cur[i];
-    int ai = act ? act[i] : 0;
-    // the 4 action targets offered at the robot's node: the tail of the last observation
-    // (read whether or not the env is dirty, so it is not a dependent load)
-    const int4 offer = act ? *reinterpret_cast<const int4*>(snd + base + 4 * i) : make_int4(0, 0, 0, 0);
+  // robot i's loads: the node, the action and the 4 action targets offered at the node, i.e.
+  // the tail of the last observation, read whether or not the env is dirty so that it is
+  // not a dependent load
+  struct Ld {
+    int c, ai;
+    int4 offer;
+  };
+  auto load = [&](int i) {
+    Ld l;
+    l.c = cur[i];
+    l.ai = act ? act[i] : 0;
+    l.offer = act ? *reinterpret_cast<const int4*>(snd + base + 4 * i) : make_int4(0, 0, 0, 0);
+    return l;
+  };
+  Ld ld[RPT];  // R <= kCovThreads: every slot's loads issued first, before the env's words
+  if (one) {
+#pragma unroll
+    for (int j = 0; j < RPT; ++j)
+      if (tid + j * NT < R) ld[j] = load(tid + j * NT);
+  }
+  // the env's words, loaded up front so none of them costs a round trip of its own
+  const bool dirty = a.dirty[b] != 0;
+  const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
+  const bool full = dirty || !a.actions;  // recompute every robot's action edges
+  // robot i: its node c and the node n its action points at (claiming c if n == c)
+  auto pick = [&](int i, const Ld& l, int& c) {
+    c = l.c;
+    int ai = l.ai;
+    const int4 offer = l.offer;
     if (dirty) {
       // closest_targets (:427-432): the robots were placed externally
       const double px = xr[2 * i], py = xr[2 * i + 1];
@@ -240,9 +289,34 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       chosen[i] = n;
       if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
     }
-    if (one && (n != c || full)) {
-      pn = n;
-      load_node(n - R, ptx, pty, pwas, pq4, pnc, pc0, pc1, pc2, pc3);
+    return n;
+  };
+  if (one) {
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      pf[j].n = -1;
+      const int i = tid + j * NT;
+      if (i < R) {
+        int c;
+        const int n = pick(i, ld[j], c);
+        if (n != c) pf[j].n = n;
+      }
+    }
+    // then every slot's record: no wait for one slot's record before the next slot
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int t = pf[j].n - R;
+      if (t >= 0) {
+        pf[j].r0 = rec[4 * t];
+        pf[j].r1 = rec[4 * t + 1];
+        pf[j].r2 = rec[4 * t + 2];
+        pf[j].was = vis[t];
+      }
+    }
+  } else {
+    for (int i = tid; i < R; i += NT) {
+      int c;
+      pick(i, load(i), c);
     }
   }
   __syncthreads();
@@ -262,7 +336,14 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       if (tid < 64) {
         // wait for this wave's LDS operations only (a fence would also wait for the
         // node prefetch still in flight from global memory)
-        auto lds_fence = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+        // GF_COV_LDS_ORDER: a wave's LDS instructions execute in issue order, so only the
+        // compiler must keep them in order (the reads' results are waited for as used)
+        auto lds_fence = [] {
+          if (GF_COV_LDS_ORDER)
+            asm volatile("" ::: "memory");
+          else
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
         // four named robots, not an array: an array indexed in a loop stays in scratch
         struct Rb {
           int i, c, n, v;
@@ -330,14 +411,14 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       __syncthreads();
       GF_COV_STAMP(2);
     } else {
-      for (int i = tid; i < R; i += kCovThreads) new_s[i] = chosen[i];  // guess: every move succeeds
+      for (int i = tid; i < R; i += NT) new_s[i] = chosen[i];  // guess: every move succeeds
       while (true) {
         __syncthreads();
-        for (int i = tid; i < R; i += kCovThreads)
+        for (int i = tid; i < R; i += NT)
           if (chosen[i] != cur_s[i]) atomicMin(&first[new_s[i]], i);
         __syncthreads();
         int changed = 0;
-        for (int i = tid; i < R; i += kCovThreads) {
+        for (int i = tid; i < R; i += NT) {
           const int c = cur_s[i], n = chosen[i];
           if (n == c) continue;
           const bool ok = !(claim[n >> 5] & (1u << (n & 31))) && first[n] >= i;
@@ -348,7 +429,7 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
           }
         }
         if (!__syncthreads_or(changed)) break;
-        for (int i = tid; i < R; i += kCovThreads)
+        for (int i = tid; i < R; i += NT)
           if (chosen[i] != cur_s[i]) {
             first[chosen[i]] = INT_MAX;
             first[cur_s[i]] = INT_MAX;
@@ -356,34 +437,42 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
       }
     }
   } else {
-    for (int i = tid; i < R; i += kCovThreads) new_s[i] = cur_s[i];
+    for (int i = tid; i < R; i += NT) new_s[i] = cur_s[i];
     __syncthreads();
   }
 
   // move (:198), visit (:265-266, :359) and the observation tail (:259-323)
   float* nodes = a.nodes + (size_t)b * M * 3;
-  for (int i = tid; i < R; i += kCovThreads) {
+  auto finish = [&](int i, const Pf* p) {
     const int n = new_s[i];
     const int t = n - R;
     const bool moved = n != cur_s[i];
     cur[i] = n;
-    if (!moved && !full) continue;  // same node, same position: its edges stand
-    double px, py;
+    if (!moved && !full) return;  // same node, same position: its edges stand
     uint8_t was;
-    int4 q4;
-    int nc;
-    double2 c0, c1, c2, c3;
-    if (n == pn) {
-      px = ptx, py = pty, was = pwas, q4 = pq4, nc = pnc, c0 = pc0, c1 = pc1, c2 = pc2, c3 = pc3;
-    } else {  // R > kCovThreads, or a blocked robot in a full pass
-      load_node(t, px, py, was, q4, nc, c0, c1, c2, c3);
-    }
-    if (moved) {
-      xr[2 * i] = px;
-      xr[2 * i + 1] = py;
+    int4 q;
+    float4 d;
+    if (moved) {  // on its node's position: the node's record holds its edges
+      float4 r0, r1, r2;
+      if (p && n == p->n) {
+        r0 = p->r0, r1 = p->r1, r2 = p->r2, was = p->was;
+      } else {  // R > kCovThreads
+        r0 = rec[4 * t], r1 = rec[4 * t + 1], r2 = rec[4 * t + 2], was = vis[t];
+      }
+      q = make_int4(__float_as_int(r0.x), __float_as_int(r0.y), __float_as_int(r0.z), __float_as_int(r0.w));
+      d = r1;
+      *reinterpret_cast<float4*>(xr + 2 * i) = r2;
     } else {  // a robot that does not move keeps its position (:198)
-      px = xr[2 * i];
-      py = xr[2 * i + 1];
+      int4 q4;
+      int nc;
+      double2 c0, c1, c2, c3;
+      load_node(t, was, q4, nc, c0, c1, c2, c3);
+      const double px = xr[2 * i], py = xr[2 * i + 1];
+      q = make_int4(0 < nc ? q4.x + R : n, 1 < nc ? q4.y + R : n, 2 < nc ? q4.z + R : n, 3 < nc ? q4.w + R : n);
+      d = make_float4(static_cast<float>(dist2d(px, py, c0.x, c0.y) / a.res),
+                      static_cast<float>(dist2d(px, py, c1.x, c1.y) / a.res),
+                      static_cast<float>(dist2d(px, py, c2.x, c2.y) / a.res),
+                      static_cast<float>(dist2d(px, py, c3.x, c3.y) / a.res));
     }
     if (!was) {
       const unsigned old = atomicOr(&seen[n >> 5], 1u << (n & 31));
@@ -395,12 +484,6 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     }
     // the robot's 4 action edges in both directions: six 16-byte stores (base and 4i are
     // multiples of 4 elements, so every group is 16-byte aligned)
-    const int4 q = make_int4(0 < nc ? q4.x + R : n, 1 < nc ? q4.y + R : n, 2 < nc ? q4.z + R : n,
-                             3 < nc ? q4.w + R : n);
-    const float4 d = make_float4(static_cast<float>(dist2d(px, py, c0.x, c0.y) / a.res),
-                                 static_cast<float>(dist2d(px, py, c1.x, c1.y) / a.res),
-                                 static_cast<float>(dist2d(px, py, c2.x, c2.y) / a.res),
-                                 static_cast<float>(dist2d(px, py, c3.x, c3.y) / a.res));
     const int4 ii = make_int4(i, i, i, i);
     const int k = base + 4 * i;
     *reinterpret_cast<int4*>(snd + k) = q;
@@ -409,6 +492,13 @@ __global__ __launch_bounds__(kCovThreads) void cov_step_kernel(CovArgs a) {
     *reinterpret_cast<int4*>(rcv + k + 4 * R) = q;
     *reinterpret_cast<float4*>(edg + k) = d;
     *reinterpret_cast<float4*>(edg + k + 4 * R) = d;
+  };
+  if (one) {
+#pragma unroll
+    for (int j = 0; j < RPT; ++j)
+      if (tid + j * NT < R) finish(tid + j * NT, &pf[j]);
+  } else {
+    for (int i = tid; i < R; i += NT) finish(i, nullptr);
   }
   GF_COV_STAMP(3);
   __syncthreads();
@@ -558,7 +648,12 @@ hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_
 }
 
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(cov_step_kernel, dim3(a.B), dim3(kCovThreads), cov_step_lds_bytes(a.R, a.M), s, a);
+  if (a.R <= kCovThreads && GF_COV_STEP_NT != kCovThreads)
+    hipLaunchKernelGGL(cov_step_kernel<GF_COV_STEP_NT>, dim3(a.B), dim3(GF_COV_STEP_NT), cov_step_lds_bytes(a.R, a.M),
+                       s, a);
+  else
+    hipLaunchKernelGGL(cov_step_kernel<kCovThreads>, dim3(a.B), dim3(kCovThreads), cov_step_lds_bytes(a.R, a.M), s,
+                       a);
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ v.set_targets(targets)
 if os.environ.get("STREAMS"):  # launches per step (cov_set_streams: 1 or 2)
     v.h.set_streams(int(os.environ["STREAMS"]))
 rs = np.random.RandomState(7)
-walls, kern = [], []
+walls, kern, enq = [], [], []
 for rnd in range(int(os.environ.get("ROUNDS", "5"))):
     v.reset(seed=rnd)
     v.set_actions(rs.randint(0, 4, size=(B, R)))
@@ -32,9 +32,10 @@ for rnd in range(int(os.environ.get("ROUNDS", "5"))):
     t0 = time.perf_counter()
     for _ in range(K):
         v.step(resident=True)
+    enq.append(1e6 * (time.perf_counter() - t0) / K)  # host time to enqueue a step
     v.sync()
     walls.append(1e6 * (time.perf_counter() - t0) / K)
     kern.append(1e3 * v.h.timing_stop()[0])
-print("%-8s wall median %6.2f us/step (min %6.2f)  kernel median %6.2f us" %
-      (tag, np.median(walls), np.min(walls), np.median(kern)))
+print("%-8s wall median %6.2f us/step (min %6.2f)  kernel median %6.2f us  enqueue %6.2f us/step" %
+      (tag, np.median(walls), np.min(walls), np.median(kern), np.median(enq)))
 v.close()
