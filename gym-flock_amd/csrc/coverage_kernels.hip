@@ -25,6 +25,9 @@ constexpr int kCovThreads = 256;
 #ifndef GF_COV_LDS_ORDER  // claim rounds: compiler-only ordering of the wave's LDS operations
 #define GF_COV_LDS_ORDER 1
 #endif
+#ifndef GF_COV_SKIP_CONST  // steps skip the tail's constant robot-index stores (A/B: 0)
+#define GF_COV_SKIP_CONST 1
+#endif
 #ifndef GF_COV_TAGGED  // claim rounds tagged (no table clearing) or cleared (A/B builds)
 #define GF_COV_TAGGED 0
 #endif
@@ -447,8 +450,8 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     const int n = new_s[i];
     const int t = n - R;
     const bool moved = n != cur_s[i];
-    cur[i] = n;
     if (!moved && !full) return;  // same node, same position: its edges stand
+    cur[i] = n;
     uint8_t was;
     int4 q;
     float4 d;
@@ -484,12 +487,16 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     }
     // the robot's 4 action edges in both directions: six 16-byte stores (base and 4i are
     // multiples of 4 elements, so every group is 16-byte aligned)
-    const int4 ii = make_int4(i, i, i, i);
+    // (the robot's own index never changes: written by full passes only, so a step leaves
+    // fewer dirty lines for the end-of-kernel L2 writeback)
     const int k = base + 4 * i;
     *reinterpret_cast<int4*>(snd + k) = q;
-    *reinterpret_cast<int4*>(snd + k + 4 * R) = ii;
-    *reinterpret_cast<int4*>(rcv + k) = ii;
     *reinterpret_cast<int4*>(rcv + k + 4 * R) = q;
+    if (full || !GF_COV_SKIP_CONST) {
+      const int4 ii = make_int4(i, i, i, i);
+      *reinterpret_cast<int4*>(snd + k + 4 * R) = ii;
+      *reinterpret_cast<int4*>(rcv + k) = ii;
+    }
     *reinterpret_cast<float4*>(edg + k) = d;
     *reinterpret_cast<float4*>(edg + k + 4 * R) = d;
   };

@@ -20,12 +20,14 @@
     }                                                                          \
   } while (0)
 
-struct Big {  // kernel arguments about the size of the Coverage step's
-  void* p[32];
+template <int NP>
+struct Big {  // kernel arguments of 8 NP + 8 bytes (NP = 32: about the Coverage step's)
+  void* p[NP];
   int spin;
 };
 
-__global__ void touch(Big a) {
+template <int NP>
+__global__ void touch(Big<NP> a) {
   if (threadIdx.x == 0) {
     long t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < a.spin) {
@@ -35,6 +37,29 @@ __global__ void touch(Big a) {
 }
 
 using clk = std::chrono::steady_clock;
+
+template <int NP>
+void sweep(int* p, hipStream_t s1, hipStream_t s2, int spin) {
+  Big<NP> a{};
+  a.p[0] = p;
+  a.spin = spin;
+  const int K = 2000, G = 256;
+  auto issue = [&] {
+    hipLaunchKernelGGL(touch<NP>, dim3(G), dim3(256), 0, s1, a);
+    hipLaunchKernelGGL(touch<NP>, dim3(G), dim3(256), 0, s2, a);
+  };
+  for (int k = 0; k < 50; ++k) issue();
+  CK(hipDeviceSynchronize());
+  auto t0 = clk::now();
+  for (int k = 0; k < K; ++k) issue();
+  auto t1 = clk::now();
+  CK(hipDeviceSynchronize());
+  auto t2 = clk::now();
+  printf("args %4d B  spin %3d  2 x hipLaunchKernel: enqueue %6.2f us/iter  wall %6.2f us/iter\n", (int)sizeof(a), spin,
+         std::chrono::duration<double, std::micro>(t1 - t0).count() / K,
+         std::chrono::duration<double, std::micro>(t2 - t0).count() / K);
+  fflush(stdout);
+}
 
 int main() {
   int* p;
@@ -46,9 +71,18 @@ int main() {
   hipEvent_t fork, join;
   CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  for (int rep = 0; rep < 2; ++rep)
+    for (int spin : {0, 100}) {
+      sweep<32>(p, s1, s2, spin);
+      sweep<1>(p, s1, s2, spin);
+      sweep<15>(p, s1, s2, spin);
+      sweep<7>(p, s1, s2, spin);
+      sweep<32>(p, s1, s2, spin);
+      sweep<1>(p, s1, s2, spin);
+    }
   const int K = 2000, G = 256;
   for (int spin : {0, 300}) {
-    Big a{};
+    Big<32> a{};
     a.p[0] = p;
     a.spin = spin;
     // (a) two launches per iteration
@@ -59,8 +93,8 @@ int main() {
         CK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
         CK(hipEventRecord(fork, cs));
         CK(hipStreamWaitEvent(s2, fork, 0));
-        hipLaunchKernelGGL(touch, dim3(G), dim3(256), 0, cs, a);
-        hipLaunchKernelGGL(touch, dim3(G), dim3(256), 0, s2, a);
+        hipLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, cs, a);
+        hipLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, s2, a);
         CK(hipEventRecord(join, s2));
         CK(hipStreamWaitEvent(cs, join, 0));
         CK(hipStreamEndCapture(cs, &g));
@@ -68,13 +102,13 @@ int main() {
       }
       auto issue = [&] {
         if (mode == 0) {
-          hipLaunchKernelGGL(touch, dim3(G), dim3(256), 0, s1, a);
-          hipLaunchKernelGGL(touch, dim3(G), dim3(256), 0, s2, a);
+          hipLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, s1, a);
+          hipLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, s2, a);
         } else if (mode == 1) {
           CK(hipGraphLaunch(ge, cs));
         } else {
-          hipExtLaunchKernelGGL(touch, dim3(G), dim3(256), 0, s1, nullptr, nullptr, 0, a);
-          hipExtLaunchKernelGGL(touch, dim3(G), dim3(256), 0, s2, nullptr, nullptr, 0, a);
+          hipExtLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, s1, nullptr, nullptr, 0, a);
+          hipExtLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, s2, nullptr, nullptr, 0, a);
         }
       };
       for (int k = 0; k < 50; ++k) issue();
