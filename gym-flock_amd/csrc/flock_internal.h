@@ -41,9 +41,19 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #ifndef GF_INLINE_RIM_U  // fused kNN inline rim scan: columns in flight per lane
 #define GF_INLINE_RIM_U 4
 #endif
+#ifndef GF_P1_FMA  // pass 1: float32 d2 as one fused multiply-add (the band covers its
+#define GF_P1_FMA 1   // rounding, which is smaller than the unfused form's); 0 = unfused (A/B)
+#endif
+#ifndef GF_P1_LDSROW  // pass 1: each row's float32 position read as an LDS broadcast (1) or
+#define GF_P1_LDSROW 1  // by two v_readlane (0; A/B builds)
+#endif
+#ifndef GF_STORE_TABLE  // network rows: float4 per nibble from a per-row 16-entry LDS table
+#define GF_STORE_TABLE 1  // (2 VALU per float4) or bit extraction (8 VALU; A/B builds: 0)
+#endif
 #ifndef GF_KNN_SLICE_LIST  // fused kNN: keys each feature-pass slice keeps (A/B builds)
 #define GF_KNN_SLICE_LIST 7
 #endif
+constexpr int kStoreTab = 16;      // network rows: float4 table entries per wave (one per nibble)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
 constexpr int kKnnRimGrid = 256;
 #ifndef GF_RIM_HALF_GRID  // rim kNN workgroups per half-batch launch (A/B builds)

@@ -454,6 +454,15 @@ __device__ __forceinline__ float2 pos32(const St& s) {
   return make_float2(static_cast<float>(p.x), static_cast<float>(p.y));
 }
 
+// pass 1's float32 squared distance of a row (xi, yi) to a wave's two columns
+__device__ __forceinline__ f2v d2_f32(float xi, float yi, f2v qx, f2v qy) {
+  const f2v dx = xi - qx, dy = yi - qy;
+  if constexpr (GF_P1_FMA)
+    return __builtin_elementwise_fma(dx, dx, dy * dy);
+  else
+    return dx * dx + dy * dy;
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -560,7 +569,7 @@ __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m,
 // stores (1 KiB per wave instruction); the block's rows are one contiguous range
 // starting at global row grow0.
 __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint64_t* adj, const float* inv,
-                                                   int Wn, size_t grow0, int nrows, int wid, int lane) {
+                                                   f4v* stab, int Wn, size_t grow0, int nrows, int wid, int lane) {
   const int N = a.N;
   const bool vec4 = (N & 3) == 0;
   // wave w writes the contiguous rows [w*R/4, (w+1)*R/4): the 4 waves' concurrent
@@ -586,7 +595,24 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
       for (int q = lane; q < (N >> 2); q += 64) r4[q] = f4v{iv, 0.f, iv, 0.f};
       continue;
     }
-    if (fast) {
+    if (fast && GF_STORE_TABLE) {
+      // the row's 16 float4 values by nibble in the wave's LDS table (a wave's LDS
+      // operations run in order: the previous row's reads precede this write, and this
+      // write the reads below), then per float4 one bit-field extract and one address
+      f4v* tab = stab + wid * kStoreTab;
+      if (lane < kStoreTab)
+        tab[lane] = f4v{(lane & 1) ? iv : 0.0f, (lane & 2) ? iv : 0.0f, (lane & 4) ? iv : 0.0f, (lane & 8) ? iv : 0.0f};
+      const unsigned* wr = bits32 + (size_t)r * 2 * Wn + wsel;
+      f4v* dst = reinterpret_cast<f4v*>(rowp) + lane;
+#pragma unroll 1
+      for (int c = 0; c < (N >> 8); c += 4) {
+        unsigned w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = wr[8 * (c + k)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[64 * (c + k)] = tab[__builtin_amdgcn_ubfe(w[k], o0, 4)];
+      }
+    } else if (fast) {
       const int ivb = __float_as_int(iv);
       const unsigned* wr = bits32 + (size_t)r * 2 * Wn + wsel;
       f4v* dst = reinterpret_cast<f4v*>(rowp) + lane;
@@ -751,7 +777,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 // kStepLdsPlainFloor), 6 with the controller (79 VGPRs, 23.2 KiB of LDS: 6 per CU);
 // variants are not capped (their extra state would spill).
 #ifndef GF_STEP_WAVES_PLAIN
-#define GF_STEP_WAVES_PLAIN 7
+#define GF_STEP_WAVES_PLAIN 6
 #endif
 #ifndef GF_STEP_WAVES_PF
 #define GF_STEP_WAVES_PF 4
@@ -802,7 +828,9 @@ void flock_step_kernel(StepArgs a) {
                                             : xcd_remap(blockIdx.x, gridDim.x);
   const int b = L / a.bpe;
   const int i0 = (L - b * a.bpe) * R;
-  St* tile = reinterpret_cast<St*>(smem);                      // float64 state, T
+  f4v* stab = reinterpret_cast<f4v*>(smem);                    // 4 x 16 network-row table entries
+  float2* rxy = reinterpret_cast<float2*>(stab + 4 * kStoreTab);  // R rows' float32 positions
+  St* tile = reinterpret_cast<St*>(smem + 4 * kStoreTab * 16 + ((R * 8 + 31) & ~31));  // float64 state, T
   St* rows = tile + T;                                         // this block's rows, R
   uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
   uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
@@ -997,6 +1025,9 @@ void flock_step_kernel(StepArgs a) {
         const St ri = rows[lane];
         rx32 = static_cast<float>(ri.px);
         ry32 = static_cast<float>(ri.py);
+        if (wid == 0) rxy[lane] = make_float2(rx32, ry32);
+      } else if (!CTRL && KN == 0 && wid == 0 && lane < ((nrows + 3) & ~3)) {
+        rxy[lane] = make_float2(-1.0e18f, -1.0e18f);  // pass 1's padding rows (far away)
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
       if constexpr (KN > 0) {
@@ -1026,6 +1057,11 @@ void flock_step_kernel(StepArgs a) {
     }
     ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
     bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
+    // row r's float32 position: an LDS broadcast (no VALU) or two v_readlane
+    auto row_pos = [&](int r) {
+      if constexpr (GF_P1_LDSROW) return rxy[r];
+      else return make_float2(readlane_f(rx32, r), readlane_f(ry32, r));
+    };
     for (int cp = GF_ABLATE(a, 8) ? npair : wid; cp < npair; cp += 4) {
       const int ca = cp << 1;
       const bool has_b = ca + 1 < nch;
@@ -1048,9 +1084,8 @@ void flock_step_kernel(StepArgs a) {
       if (fused) {
         const float ftcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
         for (int r = 0; r < nrows; ++r) {
-          const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-          const f2v dx = xi - qx, dy = yi - qy;
-          const f2v d2 = dx * dx + dy * dy;
+          const float2 pr = row_pos(r);
+          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
           const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
           const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
           band |= (Aa ^ Ma) | (Ab ^ Mb);
@@ -1071,31 +1106,57 @@ void flock_step_kernel(StepArgs a) {
             ++fp;
           }
         }
-      } else
-      for (int r = 0; r < nrows; ++r) {
-        const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-        const f2v dx = xi - qx, dy = yi - qy;
-        const f2v d2 = dx * dx + dy * dy;
-        const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
-        const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
-        band |= (Aa ^ Ma) | (Ab ^ Mb);
-        put_lane(wa0, wa1, Aa, r);
-        put_lane(wb0, wb1, Ab, r);
-        if constexpr (CTRL) {
-          const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
-          const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
-          band |= (Na ^ NMa) | (Nb ^ NMb);
-          put_lane(na0, na1, Na, r);
-          put_lane(nb0, nb1, Nb, r);
+      } else {
+        auto row1 = [&](int r, float2 pr) {
+          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
+          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+          band |= (Aa ^ Ma) | (Ab ^ Mb);
+          put_lane(wa0, wa1, Aa, r);
+          put_lane(wb0, wb1, Ab, r);
+          if constexpr (CTRL) {
+            const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+            const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+            band |= (Na ^ NMa) | (Nb ^ NMb);
+            put_lane(na0, na1, Na, r);
+            put_lane(nb0, nb1, Nb, r);
+          }
+        };
+        if constexpr (GF_P1_LDSROW && !CTRL && KN == 0) {  // (the others' budgets would spill)
+          // rows in pairs, their two LDS reads issued together (the compiler will not
+          // unroll a loop of ballots by a runtime count); rows past nrows sit far away
+          // in rxy: no bits, no band, and their lanes store nothing
+          const int nr4 = (nrows + 3) & ~3;
+          for (int r = 0; r < nr4; r += 2) {
+            const float2 p0 = rxy[r], p1 = rxy[r + 1];
+            row1(r, p0);
+            row1(r + 1, p1);
+          }
+        } else {
+          for (int r = 0; r < nrows; ++r) {
+            const float2 pr = row_pos(r);
+            const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
+            const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+            const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+            band |= (Aa ^ Ma) | (Ab ^ Mb);
+            put_lane(wa0, wa1, Aa, r);
+            put_lane(wb0, wb1, Ab, r);
+            if constexpr (CTRL) {
+              const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+              const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+              band |= (Na ^ NMa) | (Nb ^ NMb);
+              put_lane(na0, na1, Na, r);
+              put_lane(nb0, nb1, Nb, r);
+            }
+          }
         }
       }
       if (band) {  // rare: some pair is within the float32 error band of a threshold
         const St oa = va ? tile[jta] : St{1.0e300, 1.0e300, 0, 0};
         const St ob = vb ? tile[jtb] : St{1.0e300, 1.0e300, 0, 0};
         for (int r = 0; r < nrows; ++r) {
-          const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r);
-          const f2v dx = xi - qx, dy = yi - qy;
-          const f2v d2 = dx * dx + dy * dy;
+          const float2 pr = row_pos(r);
+          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
           const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
           const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
           uint64_t Na = 0, Nb = 0, NMa = 0, NMb = 0;
@@ -1149,9 +1210,9 @@ void flock_step_kernel(StepArgs a) {
           for (uint64_t pm = predm; pm; pm &= pm - 1, ++p) {
             const int r = __builtin_ctzll(pm);
             if (lane == p) rp = r;
-            const float xi = readlane_f(rx32, r), yi = readlane_f(ry32, r), tc = readlane_f(tcr, r);
-            const f2v dx = xi - qx, dy = yi - qy;
-            const f2v d2 = dx * dx + dy * dy;
+            const float2 pr = row_pos(r);
+            const float tc = readlane_f(tcr, r);
+            const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
             put_lane(ca0, ca1, __ballot(d2.x < tc), p);
             put_lane(cb0, cb1, __ballot(d2.y < tc), p);
           }
@@ -1209,7 +1270,7 @@ void flock_step_kernel(StepArgs a) {
   __syncthreads();
   GF_STAMP(7);
 
-  if (a.network) store_network_rows(a, adj, inv, Wn, env0 + i0, nrows, wid, lane);
+  if (a.network) store_network_rows(a, adj, inv, stab, Wn, env0 + i0, nrows, wid, lane);
 
   GF_STAMP(8);
   feature_pass(jl, nchl);
@@ -1680,6 +1741,7 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 2 : 1) + 15) / 16) * 16;
+  s += 4 * kStoreTab * 16 + (((size_t)R * 8 + 31) & ~size_t(31));  // row table, rows' float32 positions
   return s;
 }
 

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Pass 1 FMA + LDS-broadcast rows, network rows from an LDS nibble table: full GPU suite,
+# then the bench A/B against HEAD's library.
+set -e
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/s16_pytest.txt 2>&1 || { tail -30 gpurun_out/s16_pytest.txt; exit 1; }
+tail -2 gpurun_out/s16_pytest.txt
+ROUNDS=2 bash scripts/ab_bench.sh > gpurun_out/s16_ab.txt 2>&1
+cat gpurun_out/s16_ab.txt
