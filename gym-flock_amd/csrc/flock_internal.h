@@ -30,7 +30,7 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #define GF_KNN_MED3 1
 #endif
 #ifndef GF_RECIP_NR  // pair terms' 1/r2: 0 = IEEE division, 1 = rcp + Newton without the
-#define GF_RECIP_NR 0  // controller, 2 = everywhere (A/B builds; 1 and 2 measured slower)
+#define GF_RECIP_NR 1  // controller, 2 = everywhere (A/B builds)
 #endif
 #ifndef GF_KNN_LATE_GATHER  // fused kNN: the neighbour's state is loaded after the epilogue (1)
 #define GF_KNN_LATE_GATHER 0  // or before it, its latency under the epilogue's sums (0)

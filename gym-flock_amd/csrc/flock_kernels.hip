@@ -190,18 +190,16 @@ __device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
 }
 
 // Sorted insertion of (r2, j) into a K-list; ties go to the lower index (stable).
-// 1/r2 for the pair terms: v_rcp_f64 refined by two Newton steps (within an ulp or two
-// of the IEEE quotient, 5 float64 ops instead of the 10 of a correctly rounded
-// division); zero, denormal, huge and NaN r2 take the IEEE division, so its infinities
-// and NaNs are kept
+// 1/r2 for the feature pair terms (float32 outputs) without the controller: v_rcp_f64
+// refined by one Newton step (about 2^-50 relative, 3 float64 ops instead of the 10 of a
+// correctly rounded division; GF_RECIP_NR). The controller keeps the IEEE division.
 __device__ __forceinline__ double recip_f64(double r2) {
-  double x = __builtin_amdgcn_rcp(r2);
-  double e = fma(-r2, x, 1.0);
-  x = fma(x, e, x);
-  e = fma(-r2, x, 1.0);
-  x = fma(x, e, x);
-  if (!(r2 >= 0x1p-1000 && r2 <= 0x1p+1000)) x = 1.0 / r2;
-  return x;
+  // one Newton step on v_rcp_f64; outside [2^-1000, 2^1000] (zero, denormals, huge,
+  // inf, NaN) the raw v_rcp_f64 value, chosen without a branch
+  const double x0 = __builtin_amdgcn_rcp(r2);
+  const double e = fma(-r2, x0, 1.0);
+  const double x1 = fma(x0, e, x0);
+  return (r2 >= 0x1p-1000 && r2 <= 0x1p+1000) ? x1 : x0;
 }
 
 __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
