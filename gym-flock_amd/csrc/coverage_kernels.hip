@@ -655,13 +655,15 @@ hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_
 }
 
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {
-  if (a.R <= kCovThreads && GF_COV_STEP_NT != kCovThreads)
-    hipLaunchKernelGGL(cov_step_kernel<GF_COV_STEP_NT>, dim3(a.B), dim3(GF_COV_STEP_NT), cov_step_lds_bytes(a.R, a.M),
-                       s, a);
-  else
-    hipLaunchKernelGGL(cov_step_kernel<kCovThreads>, dim3(a.B), dim3(kCovThreads), cov_step_lds_bytes(a.R, a.M), s,
-                       a);
-  return hipGetLastError();
+  // hipLaunchKernel with the argument pointer: the step is host-bound at two launches
+  // per step, and the hipLaunchKernelGGL wrapper's repacking measured ~0.15 us more per
+  // launch (scripts/graphprobe.hip)
+  void* args[] = {const_cast<CovArgs*>(&a)};
+  const bool narrow = a.R <= kCovThreads && GF_COV_STEP_NT != kCovThreads;
+  const void* f = narrow ? reinterpret_cast<const void*>(&cov_step_kernel<GF_COV_STEP_NT>)
+                         : reinterpret_cast<const void*>(&cov_step_kernel<kCovThreads>);
+  return hipLaunchKernel(f, dim3(a.B), dim3(narrow ? GF_COV_STEP_NT : kCovThreads), args,
+                         cov_step_lds_bytes(a.R, a.M), s);
 }
 
 #ifdef GF_STAMPS

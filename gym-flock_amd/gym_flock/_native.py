@@ -6,6 +6,7 @@ __graft_entry__.build()); if it is missing or no GPU is present, every call that
 needs it raises — there is no CPU fallback in the product path.
 """
 import ctypes
+import functools
 import os
 
 import numpy as np
@@ -510,6 +511,8 @@ class CoverageHandle:
         h = ctypes.c_void_p()
         check(self.lib.cov_create(ctypes.byref(self.cfg), ctypes.byref(h)))
         self.h = h
+        # the resident-action step with its arguments bound: a step is ~7 us, host-bound
+        self._step_resident = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_RESIDENT)
 
     def close(self):
         if getattr(self, "h", None):
@@ -542,7 +545,9 @@ class CoverageHandle:
 
     def step(self, actions=None, resident=False):
         if resident:
-            check(self.lib.cov_step(self.h, None, COV_ACTIONS_RESIDENT))
+            rc = self._step_resident()
+            if rc:
+                check(rc)
             return
         a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
         check(self.lib.cov_step(self.h, ptr(a), 0))

@@ -166,6 +166,11 @@ class VecCoverage:
         return start, visited
 
     def step(self, actions=None, resident=False):
+        if resident:
+            rc = self.h._step_resident()
+            if rc:
+                nat.check(rc)
+            return
         self.h.step(actions, resident)
 
     def set_actions(self, actions):

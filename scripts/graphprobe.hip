@@ -61,6 +61,41 @@ void sweep(int* p, hipStream_t s1, hipStream_t s2, int spin) {
   fflush(stdout);
 }
 
+// two launches per iteration through each C launch API, arguments of 264 bytes
+void api_sweep(int* p, hipStream_t s1, hipStream_t s2, int spin) {
+  Big<32> a{};
+  a.p[0] = p;
+  a.spin = spin;
+  hipFunction_t f;
+  CK(hipGetFuncBySymbol(&f, reinterpret_cast<const void*>(&touch<32>)));
+  void* args[] = {&a};
+  const int K = 2000, G = 256;
+  for (int mode = 0; mode < 3; ++mode) {
+    auto issue = [&] {
+      for (hipStream_t s : {s1, s2}) {
+        if (mode == 0)
+          hipLaunchKernelGGL(touch<32>, dim3(G), dim3(256), 0, s, a);
+        else if (mode == 1)
+          CK(hipLaunchKernel(reinterpret_cast<const void*>(&touch<32>), dim3(G), dim3(256), args, 0, s));
+        else
+          CK(hipModuleLaunchKernel(f, G, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+      }
+    };
+    for (int k = 0; k < 50; ++k) issue();
+    CK(hipDeviceSynchronize());
+    auto t0 = clk::now();
+    for (int k = 0; k < K; ++k) issue();
+    auto t1 = clk::now();
+    CK(hipDeviceSynchronize());
+    auto t2 = clk::now();
+    printf("spin %3d  %-28s enqueue %6.2f us/iter  wall %6.2f us/iter\n", spin,
+           mode == 0 ? "2 x hipLaunchKernelGGL" : mode == 1 ? "2 x hipLaunchKernel" : "2 x hipModuleLaunchKernel",
+           std::chrono::duration<double, std::micro>(t1 - t0).count() / K,
+           std::chrono::duration<double, std::micro>(t2 - t0).count() / K);
+    fflush(stdout);
+  }
+}
+
 int main() {
   int* p;
   CK(hipMalloc(&p, 1 << 20));
@@ -71,6 +106,9 @@ int main() {
   hipEvent_t fork, join;
   CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  for (int rep = 0; rep < 3; ++rep)
+    for (int spin : {0, 100}) api_sweep(p, s1, s2, spin);
+  if (getenv("API_ONLY")) return 0;
   for (int rep = 0; rep < 2; ++rep)
     for (int spin : {0, 100}) {
       sweep<32>(p, s1, s2, spin);

@@ -116,14 +116,20 @@ def test_external_robot_positions_recompute_closest():
     start = np.arange(R) * (T // R)
     h.reset(start[None], np.ones((1, M - R), np.uint8))
     o.reset(start, [])
-    xr = f["targets"][start] + np.random.RandomState(1).uniform(-2.0, 2.0, size=(R, 2))
-    h.set_robot_positions(0, xr)
-    o.xr = xr.copy()
-    a = np.random.RandomState(2).randint(0, 4, size=R)
-    h.step(a[None])
-    obs, rr, dd = o.step(a)
-    assert_obs(h.obs(0), {k + "0": val for k, val in obs.items()})
-    np.testing.assert_array_equal(h.robots(0)[0], o.xr)
+    rs = np.random.RandomState(2)
+    # two placements, each followed by steps: the full pass after a placement (blocked
+    # robots keep their off-node positions and edges) and the node-record steps after it
+    for place in range(2):
+        xr = f["targets"][start] + np.random.RandomState(1 + place).uniform(-2.0, 2.0, size=(R, 2))
+        h.set_robot_positions(0, xr)
+        o.xr = xr.copy()
+        for t in range(8):
+            a = rs.randint(0, 4, size=R)
+            h.step(a[None])
+            obs, rr, dd = o.step(a)
+            assert_obs(h.obs(0), {k + "0": val for k, val in obs.items()})
+            np.testing.assert_array_equal(h.robots(0)[0], o.xr)
+            assert h.rewards()[0][0] == rr
     h.close()
 
 
