@@ -47,6 +47,9 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #ifndef GF_P1_LDSROW  // pass 1: each row's float32 position read as an LDS broadcast (1) or
 #define GF_P1_LDSROW 1  // by two v_readlane (0; A/B builds)
 #endif
+#ifndef GF_P1_PAIR  // pass 1 of the plain step: rows' positions read in pairs (A/B builds: 0)
+#define GF_P1_PAIR 1
+#endif
 #ifndef GF_STORE_TABLE  // network rows: float4 per nibble from a per-row 16-entry LDS table
 #define GF_STORE_TABLE 1  // (2 VALU per float4) or bit extraction (8 VALU; A/B builds: 0)
 #endif

@@ -1024,7 +1024,7 @@ void flock_step_kernel(StepArgs a) {
         rx32 = static_cast<float>(ri.px);
         ry32 = static_cast<float>(ri.py);
         if (wid == 0) rxy[lane] = make_float2(rx32, ry32);
-      } else if (!CTRL && KN == 0 && wid == 0 && lane < ((nrows + 3) & ~3)) {
+      } else if (GF_P1_PAIR && !CTRL && KN == 0 && wid == 0 && lane < ((nrows + 3) & ~3)) {
         rxy[lane] = make_float2(-1.0e18f, -1.0e18f);  // pass 1's padding rows (far away)
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
@@ -1120,7 +1120,7 @@ void flock_step_kernel(StepArgs a) {
             put_lane(nb0, nb1, Nb, r);
           }
         };
-        if constexpr (GF_P1_LDSROW && !CTRL && KN == 0) {  // (the others' budgets would spill)
+        if constexpr (GF_P1_LDSROW && GF_P1_PAIR && !CTRL && KN == 0) {  // (the others' budgets would spill)
           // rows in pairs, their two LDS reads issued together (the compiler will not
           // unroll a loop of ballots by a runtime count); rows past nrows sit far away
           // in rxy: no bits, no band, and their lanes store nothing
