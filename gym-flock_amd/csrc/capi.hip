@@ -2,6 +2,7 @@
 // stream-ordered launches, host transfers, RCCL metrics path and error reporting.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -148,6 +149,47 @@ struct fe_handle {
 };
 
 namespace {
+
+// fe_get_outputs(FE_OUT_MAPPED): the step's outputs into page-locked host arrays through
+// their mapped addresses, 16-byte stores where both sides allow (grid-stride).
+struct OutCopy {
+  const float* src[2];
+  float* dst[2];
+  size_t n[2];  // floats
+  const double* rsrc;
+  double* rdst;
+  int nr;
+};
+
+__global__ __launch_bounds__(256) void out_copy_kernel(OutCopy c) {
+  const size_t t0 = (size_t)blockIdx.x * 256 + threadIdx.x, st = (size_t)gridDim.x * 256;
+  for (int a = 0; a < 2; ++a) {
+    if (!c.dst[a]) continue;
+    const float* s = c.src[a];
+    float* d = c.dst[a];
+    const size_t n = c.n[a];
+    if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+      const size_t n4 = n >> 2;
+      for (size_t k = t0; k < n4; k += st) reinterpret_cast<float4*>(d)[k] = reinterpret_cast<const float4*>(s)[k];
+      for (size_t k = (n4 << 2) + t0; k < n; k += st) d[k] = s[k];
+    } else {
+      for (size_t k = t0; k < n; k += st) d[k] = s[k];
+    }
+  }
+  if (c.rdst)
+    for (size_t k = t0; k < (size_t)c.nr; k += st) c.rdst[k] = c.rsrc[k];
+}
+
+// The device address of page-locked host memory, or nullptr (pageable: its failed
+// lookup's error is cleared so later launch checks do not see it).
+void* mapped_ptr(void* p) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
 
 // `stream` waits for the second half-batch stream (enqueue only, no host sync).
 int join_s2(fe_handle* h) {
@@ -937,12 +979,31 @@ int fe_get_controls(fe_handle* h, int env, double* dst) {
 
 int fe_get_outputs(fe_handle* h, int env, float* state_values, float* network, double* rewards, int flags) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (flags != 0) return fail(GF_EINVAL, "flags must be 0");
+  if (flags & ~FE_OUT_MAPPED) return fail(GF_EINVAL, "flags: 0 or FE_OUT_MAPPED");
   if (int rc = check_env(h, env)) return rc;
   if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
   if (int rc = use_dev(h)) return rc;
   const size_t N = h->cfg.n_agents;
   const size_t nsv = env < 0 ? h->BN * 6 : N * 6, nnet = env < 0 ? h->BN * N : N * N;
+  if (flags & FE_OUT_MAPPED) {
+    // page-locked destinations by one copy kernel; any other one by its own copy below
+    OutCopy c{};
+    c.src[0] = h->sv + (env < 0 ? 0 : env * N * 6);
+    c.src[1] = h->net + (env < 0 ? 0 : env * N * N);
+    c.n[0] = nsv;
+    c.n[1] = nnet;
+    c.rsrc = cur_reward(h);
+    c.nr = h->cfg.n_envs;
+    if (state_values && (c.dst[0] = static_cast<float*>(mapped_ptr(state_values)))) state_values = nullptr;
+    if (network && (c.dst[1] = static_cast<float*>(mapped_ptr(network)))) network = nullptr;
+    if (rewards && (c.rdst = static_cast<double*>(mapped_ptr(rewards)))) rewards = nullptr;
+    if (c.dst[0] || c.dst[1] || c.rdst) {
+      const size_t most = std::max(c.dst[0] ? nsv : 0, c.dst[1] ? nnet : 0) / 4 + 1;
+      const int grid = static_cast<int>(std::min<size_t>((most + 255) / 256, 1024));
+      hipLaunchKernelGGL(out_copy_kernel, dim3(grid), dim3(256), 0, h->stream, c);
+      GF_HIP(hipGetLastError());
+    }
+  }
   if (rewards)
     GF_HIP(hipMemcpyAsync(rewards, cur_reward(h), (size_t)h->cfg.n_envs * 8, hipMemcpyDeviceToHost, h->stream));
   if (state_values)
@@ -957,7 +1018,7 @@ int fe_get_outputs(fe_handle* h, int env, float* state_values, float* network, d
 int fe_host_alloc(size_t bytes, void** out) {
   if (!out || bytes == 0) return fail(GF_EINVAL, "bad argument");
   *out = nullptr;
-  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocMapped);
   if (e != hipSuccess) {
     *out = nullptr;
     return fail(GF_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));

@@ -26,6 +26,7 @@ FE_NO_NETWORK = 0x20
 FE_NO_STATE_VALUES = 0x40
 FE_U_RESIDENT = 0x80
 FE_PACKED_NETWORK = 0x100
+FE_OUT_MAPPED = 0x1  # fe_get_outputs flag
 
 
 class FeConfig(ctypes.Structure):
@@ -423,7 +424,12 @@ class FlockHandle:
         sv = new(lead + (6,), np.float32)
         net = new(lead + (n,), np.float32)
         rw = np.empty(self.n_envs)
-        check(self.lib.fe_get_outputs(self.h, -1 if env is None else int(env), ptr(sv), ptr(net), ptr(rw), 0))
+        if pool is not None:
+            rw = pool.array((self.n_envs,), np.float64)
+        # pool arrays are page-locked (those past the pool's cap are not: the library
+        # copies those by DMA), written by one copy kernel (FE_OUT_MAPPED)
+        check(self.lib.fe_get_outputs(self.h, -1 if env is None else int(env), ptr(sv), ptr(net), ptr(rw),
+                                      FE_OUT_MAPPED if pool is not None else 0))
         return sv, net, rw
 
     def knn(self, env=None):

@@ -55,6 +55,10 @@ enum gf_status {
 #define FE_NO_STATE_VALUES 0x40 /* skip the (N,6) state_values write              */
 #define FE_U_RESIDENT      0x80 /* u := the handle's action buffer as last set by
                                    fe_set_actions (already in HBM; u ignored)     */
+#define FE_OUT_MAPPED        0x1 /* fe_get_outputs: destinations that are page-locked
+                                   (fe_host_alloc) are written by one device copy
+                                   kernel through their mapped addresses instead of
+                                   one DMA copy each; others still take a copy     */
 #define FE_PACKED_NETWORK 0x100 /* also write the adjacency as bits (B,N,ceil(N/64))
                                    uint64 + degree (B,N) int32, the packed output
                                    mode; with FE_NO_NETWORK the
@@ -156,7 +160,9 @@ int fe_get_rewards(fe_handle* h, double* dst);
 /* The step's host outputs in one call with one stream sync (the drop-in env's
  * (state_values, network), reward tuple of step(), flocking_relative.py:109): any of
  * state_values (N,6) / network (N,N) of `env` (env < 0: all envs) and rewards (B) may be
- * NULL. flags: reserved, 0. Destinations from fe_host_alloc copy at full link rate. */
+ * NULL. flags: 0, or FE_OUT_MAPPED (page-locked destinations written by one copy
+ * kernel: one launch instead of up to three DMA copies, each of which costs ~12-15 us of
+ * latency at drop-in sizes). Returns after the data is in the destinations. */
 int fe_get_outputs(fe_handle* h, int env, float* state_values, float* network, double* rewards, int flags);
 /* Page-locked host memory for output arrays (the drop-in env hands such buffers to the
  * caller as fresh arrays and recycles them once released). */
