@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "device_alloc.h"
 #include "flock_internal.h"
 #include "gymflock.h"
 
@@ -257,7 +258,7 @@ int dalloc(T** p, size_t count) {
     *p = nullptr;
     return GF_OK;
   }
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+  hipError_t e = gf::device_alloc(reinterpret_cast<void**>(p), count * sizeof(T));
   if (e != hipSuccess) return fail(GF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   return GF_OK;
 }

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "coverage_internal.h"
+#include "device_alloc.h"
 #include "gymflock.h"
 
 namespace gf {
@@ -25,7 +26,7 @@ template <class T>
 int calloc_dev(T** p, size_t n) {
   *p = nullptr;
   if (n == 0) return GF_OK;
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+  hipError_t e = gf::device_alloc(reinterpret_cast<void**>(p), n * sizeof(T));
   if (e != hipSuccess) return cfail(GF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   e = hipMemset(*p, 0, n * sizeof(T));
   if (e != hipSuccess) return cfail(GF_EHIP, std::string("hipMemset: ") + hipGetErrorString(e));

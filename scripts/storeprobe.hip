@@ -114,10 +114,26 @@ void shape(const char* name, f4v* net, int rows, int N, int lds) {
   fflush(stdout);
 }
 
-int main() {
+int main(int argc, char** argv) {
   f4v* net;
   const size_t big = (size_t)32 * 8192 * 8192 * 4;
-  CK(hipMalloc(&net, big));
+  if (argc > 1 && argv[1][0] == 'c') {  // physically contiguous allocation
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&net), big, hipDeviceMallocContiguous));
+    printf("allocation: hipExtMallocWithFlags(hipDeviceMallocContiguous)\n");
+    if (argc > 2) {  // config-5 shapes only
+      shape<16>("8GiB N=8192 (cfg5)", net, 32 * 8192, 8192, 37376);
+      CK(hipFree(net));
+      return 0;
+    }
+  } else {
+    CK(hipMalloc(&net, big));
+    printf("allocation: hipMalloc\n");
+    if (argc > 2) {
+      shape<16>("8GiB N=8192 (cfg5)", net, 32 * 8192, 8192, 37376);
+      CK(hipFree(net));
+      return 0;
+    }
+  }
   for (int g : {2048, 8192, 32768}) {
     const float t8 = run_linear(net, big, g), t1 = run_linear(net, big / 8, g);
     printf("linear grid %5d: 8 GiB %8.1f us (%.2f TB/s)  1 GiB %8.1f us (%.2f TB/s)\n", g, t8,
