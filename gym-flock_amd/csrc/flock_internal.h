@@ -56,15 +56,6 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #ifndef GF_KNN_SLICE_LIST  // fused kNN: keys each feature-pass slice keeps (A/B builds)
 #define GF_KNN_SLICE_LIST 7
 #endif
-#ifndef GF_FEAT_LIST  // feature pass of the fused kNN step: a row's visited pairs listed in LDS
-#define GF_FEAT_LIST 0   // (this many per row and tile) and dealt round robin over its slices;
-#endif                   // 0 = each slice walks its own words (A/B builds)
-#ifndef GF_PAIR_LEAN  // feature pair terms: kNN key clamped in integers, 1/r2's range check
-#define GF_PAIR_LEAN 0  // at the lower end only (A/B builds)
-#endif
-#ifndef GF_FEAT_LIST_ALL  // the list for every FlockingRelative instantiation too (A/B builds)
-#define GF_FEAT_LIST_ALL 0
-#endif
 constexpr int kStoreTab = 16;      // network rows: float4 table entries per wave (one per nibble)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
 constexpr int kKnnRimGrid = 256;

@@ -199,9 +199,7 @@ __device__ __forceinline__ double recip_f64(double r2) {
   const double x0 = __builtin_amdgcn_rcp(r2);
   const double e = fma(-r2, x0, 1.0);
   const double x1 = fma(x0, e, x0);
-  // (GF_PAIR_LEAN: the pairs the step visits have r2 below comm_radius^2 or a finite
-  // candidate radius, so only the lower end is checked)
-  return (r2 >= 0x1p-1000 && (GF_PAIR_LEAN || r2 <= 0x1p+1000)) ? x1 : x0;
+  return (r2 >= 0x1p-1000 && r2 <= 0x1p+1000) ? x1 : x0;
 }
 
 __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
@@ -545,32 +543,6 @@ __device__ __forceinline__ unsigned group_min_u32(unsigned w, int S) {
   return w;
 }
 
-// Inclusive prefix sum over aligned groups of S consecutive lanes (fs = lane's index in
-// its group): DPP row shifts inside rows of 16, shuffles beyond.
-template <int SH>
-__device__ __forceinline__ int dpp_shr(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x110 + SH, 0xF, 0xF, true);
-}
-__device__ __forceinline__ int group_incl_scan(int x, int fs, int S) {
-  int t = dpp_shr<1>(x);
-  x += fs >= 1 ? t : 0;
-  t = dpp_shr<2>(x);
-  x += fs >= 2 ? t : 0;
-  if (S > 4) {
-    t = dpp_shr<4>(x);
-    x += fs >= 4 ? t : 0;
-  }
-  if (S > 8) {
-    t = dpp_shr<8>(x);
-    x += fs >= 8 ? t : 0;
-  }
-  for (int o = 16; o < S; o <<= 1) {
-    t = __shfl_up(x, o);
-    x += fs >= o ? t : 0;
-  }
-  return x;
-}
-
 // Lane l of (w0, w1) takes the wave-uniform 64-bit mask m.
 // Flocking-v0 predicted row's candidate bound: float32 d2 < bound covers every agent with
 // r2 < th (float32 error of d2 at |d| <= sqrt(th): 2^-23 |d| (Pi + Pj + |d|) + 2^-22 r2,
@@ -865,9 +837,6 @@ void flock_step_kernel(StepArgs a) {
   float* redf = reinterpret_cast<float*>(red + 4);
   float* inv = reinterpret_cast<float*>(red + 8);
   [[maybe_unused]] float* rthr = inv + R;                      // R kNN candidate radii^2 (0: none)
-  // feature pass: each row's visited pairs of one tile, listed (GF_FEAT_LIST per row)
-  constexpr bool FL = GF_FEAT_LIST > 0 && (KN > 0 || GF_FEAT_LIST_ALL) && !VAR;
-  [[maybe_unused]] uint16_t* flist = reinterpret_cast<uint16_t*>(inv + ((R * (KN ? 2 : 1) + 3) & ~3));
 
   const int nrows = min(R, N - i0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -957,10 +926,7 @@ void flock_step_kernel(StepArgs a) {
      if (false) {
 #endif
       // q = min(floor(r2 * ksc), qmax); fmin returns qmax for a NaN r2 (ranked last)
-      // (GF_PAIR_LEAN: the clamp in integers; a visited pair's r2 is finite, NaN never
-      // passes the adjacency or candidate tests)
-      const unsigned q = GF_PAIR_LEAN ? min(static_cast<unsigned>(r2 * ksc), a.knn_qmax)
-                                      : static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
+      const unsigned q = static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
       const unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
       if constexpr (GF_KNN_MED3) {
         knn_list_insert<KL>(kk, v);
@@ -1015,56 +981,6 @@ void flock_step_kernel(StepArgs a) {
     }
     const int wpt = (nch + S - 1) / S;
     const int wb = fs * wpt, we = min(nch, wb + wpt);
-    if constexpr (FL) {
-      // A slice walking only its own words runs as long as the wave's fullest word (at
-      // config 2 a lane's word holds 1.8 pairs on average, the wave's fullest ~5). Here
-      // the row's S slices list the row's pairs of this tile in LDS (a cheap loop over
-      // their own bits) and then take the list round robin (the row's pairs / S each).
-      // A row with more pairs than the list holds walks its words (below); the group of
-      // S lanes decides together.
-      int cnt = 0;
-      for (int w = wb; w < we; ++w) {
-        const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
-        const uint64_t cm = (KN && crow) ? crow[w] : 0ull;
-        cnt += __popcll(adj[(size_t)fr * Wn + (j0 >> 6) + w] | nm | cm);
-      }
-      const int inc = group_incl_scan(cnt, fs, S);
-      const int tot = __shfl(inc, lane | (S - 1));  // the group's last lane
-      if (tot <= GF_FEAT_LIST) {
-        uint16_t* lst = flist + fr * GF_FEAT_LIST;
-        int pos = inc - cnt;
-        for (int w = wb; w < we; ++w) {
-          const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
-          const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
-          const uint64_t cm = (KN && crow) ? crow[w] : 0ull;
-          uint64_t m = am | nm | cm;
-          if ((nm | cm) == 0ull) {  // neighbours only
-            while (m) {
-              const int k = __builtin_ctzll(m);
-              m &= m - 1;
-              lst[pos++] = static_cast<uint16_t>((w << 6) | k | (1 << 14));
-            }
-          } else {
-            while (m) {
-              const int k = __builtin_ctzll(m);
-              m &= m - 1;
-              lst[pos++] = static_cast<uint16_t>((w << 6) | k | ((static_cast<unsigned>(am >> k) & 1u) << 14) |
-                                                 ((static_cast<unsigned>(nm >> k) & 1u) << 15));
-            }
-          }
-        }
-        // the list is read back by other lanes of this wave: a wave's LDS operations
-        // complete in order, so only the compiler must keep them in order
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int e = fs; e < tot; e += S) {
-          const unsigned v = lst[e];
-          pair_terms(me, j0, v & 0x3FFF, (v >> 14) & 1u, CTRL && ((v >> 15) & 1u), ksc);
-        }
-        return;
-      }
-    }
     for (int w = wb; w < we; ++w) {
       const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
       const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
@@ -1824,7 +1740,6 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 2 : 1) + 15) / 16) * 16;
   s += 4 * kStoreTab * 16 + (((size_t)R * 8 + 31) & ~size_t(31));  // row table, rows' float32 positions
-  if (GF_FEAT_LIST > 0 && (knn || GF_FEAT_LIST_ALL)) s += (size_t)R * GF_FEAT_LIST * 2;  // pair lists
   return s;
 }
 
