@@ -588,16 +588,20 @@ def dry_host(args, world, rank):
     if args.dry_host_corrupt and rank == 1:
         gathered[0] += 1e-9
     _, ok = check_gathered(group, gathered, rew)
+    # the get_stats aggregates: per-env [mean vel_diffs, mean min_dists], host channel
+    summ = np.array([[st["vel_diffs"].mean(), st["min_dists"].mean()] for st in map(orc.stats, xs)]).reshape(B, 2)
+    gstats = HostRewardGather(group).gather(summ.ravel())
+    _, sok = check_gathered(group, gstats, summ)
     group.close()
     if rank == 0:
         print(json.dumps({"metric": "agent-steps/sec (dry host: CPU oracle, no GPU)", "value": world * B * N * K / max(every),
                           "unit": "agent-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
                           "ms_per_step": 1e3 * max(every) / K,
                           "per_rank_ms_per_step": [1e3 * e / K for e in every],
-                          "gathered_rewards_ok": ok, "dry_host": True,
+                          "gathered_rewards_ok": ok, "gathered_stats_ok": sok, "dry_host": True,
                           "config": {"n_agents": N, "envs_per_gpu": B, "global_envs": world * B}}), flush=True)
-    if not ok:
-        raise SystemExit("gathered rewards differ from the ranks' local rewards")
+    if not (ok and sok):
+        raise SystemExit("gathered rewards or stats differ from the ranks' local values")
 
 
 def cpu_share():
@@ -717,6 +721,10 @@ def main():
         extra["gathered_rewards_ok"] = every
         extra["gathered_rewards_check"] = ("every rank compared the whole gathered (world x B) vector of the last "
                                            "step with the ranks' local rewards sent over the host channel")
+        # the optional get_stats aggregates: per-env means, all-gathered once
+        gather.issue_stats()
+        _, sok = check_gathered(group, gather.stats_result(), env.stats_summary())
+        extra["gathered_stats_ok"] = sok
 
     # closed-loop step + fused controller (u = previous controller output), same workload
     if not args.no_controller_line:

@@ -118,6 +118,10 @@ struct fe_handle {
   hipEvent_t ag_ev[kBlocks] = {};
   bool ag_pending[kBlocks] = {};
   int last_gather = -1, last_count = 0;
+  double* stats_sum = nullptr;          // (B,2) get_stats means per env (fe_stats_summary)
+  double* stats_gather = nullptr;       // nranks x B x 2 (fe_allgather_stats)
+  hipEvent_t sg_ev = nullptr;           // completion of the latest stats all-gather
+  bool sg_pending = false;
   // flocking variant (fe_set_variant / fe_set_dt)
   bool has_variant = false;
   fe_variant var{};
@@ -272,7 +276,7 @@ void release(fe_handle* h) {
   if (h->kstream) hipStreamSynchronize(h->kstream);
   if (h->comm) ncclCommDestroy(h->comm);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->dt_env,
+                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->stats_sum, h->stats_gather, h->dt_env,
                   h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -280,6 +284,7 @@ void release(fe_handle* h) {
   if (h->step_ev) hipEventDestroy(h->step_ev);
   if (h->step_ev2) hipEventDestroy(h->step_ev2);
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
+  if (h->sg_ev) hipEventDestroy(h->sg_ev);
   for (hipEvent_t e : h->ag_ev)
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
@@ -922,6 +927,36 @@ int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists,
   return GF_OK;
 }
 
+namespace {
+// get_stats (:136-143) on every env of the current state, then each env's means of the
+// two arrays into stats_sum (B,2), on the handle's stream. A pending stats all-gather
+// still reads stats_sum: the stream waits for it first.
+int stats_summary_dev(fe_handle* h) {
+  if (!h->vel_diffs) {
+    if (int rc = dalloc(&h->vel_diffs, h->BN)) return rc;
+    if (int rc = dalloc(&h->min_dists, h->BN)) return rc;
+    if (int rc = dalloc(&h->degree, h->BN)) return rc;
+  }
+  if (!h->stats_sum)
+    if (int rc = dalloc(&h->stats_sum, (size_t)h->cfg.n_envs * 2)) return rc;
+  if (h->sg_pending) GF_HIP(hipStreamWaitEvent(h->stream, h->sg_ev, 0));
+  gf::StatsArgs s{h->x[h->cur], h->vel_diffs, h->min_dists, h->degree,
+                  h->cfg.comm_radius * h->cfg.comm_radius, h->cfg.n_agents, h->cfg.n_envs};
+  hipError_t e = gf::launch_stats(s, h->stream);
+  if (e == hipSuccess) e = gf::launch_stats_summary(s, h->stats_sum, h->stream);
+  if (e != hipSuccess) return fail_hip("stats launch", e);
+  return GF_OK;
+}
+}  // namespace
+
+int fe_stats_summary(fe_handle* h, double* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  if (int rc = use_dev(h)) return rc;
+  if (int rc = stats_summary_dev(h)) return rc;
+  return d2h(h, dst, h->stats_sum, (size_t)h->cfg.n_envs * 2 * sizeof(double));
+}
+
 int fe_get_state_values(fe_handle* h, int env, float* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
   if (int rc = check_env(h, env)) return rc;
@@ -1279,6 +1314,8 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
   GF_HIP(hipEventCreateWithFlags(&h->step_ev2, hipEventDisableTiming));
   for (auto& e : h->ag_ev) GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (int rc2 = dalloc(&h->gather, (size_t)kBlocks * nranks * kGatherBlock * h->cfg.n_envs)) return rc2;
+  GF_HIP(hipEventCreateWithFlags(&h->sg_ev, hipEventDisableTiming));
+  if (int rc2 = dalloc(&h->stats_gather, (size_t)nranks * h->cfg.n_envs * 2)) return rc2;
   return GF_OK;
 }
 
@@ -1332,6 +1369,40 @@ int fe_get_gathered_rewards(fe_handle* h, double* dst) {
 }
 
 int fe_gathered_steps(fe_handle* h) { return h ? h->last_count : 0; }
+
+int fe_allgather_stats(fe_handle* h) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->comm) return fail(GF_ESTATE, "fe_comm_init not called");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set");
+  // the summaries are taken on the whole current state (both step halves joined); the
+  // collective then runs on the side stream, like the reward all-gather
+  if (int rc = use_dev(h)) return rc;
+  if (int rc = stats_summary_dev(h)) return rc;
+  GF_HIP(hipEventRecord(h->step_ev, h->stream));
+  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
+  const size_t n = (size_t)h->cfg.n_envs * 2;
+  ncclResult_t r = ncclAllGather(h->stats_sum, h->stats_gather, n, ncclFloat64, h->comm, h->comm_stream);
+  if (r == ncclInProgress) {
+    if (int rc = comm_wait(h, std::chrono::steady_clock::now() + std::chrono::seconds((int)kCommInitTimeoutS),
+                           "ncclAllGather (stats)"))
+      return rc;
+  } else if (r != ncclSuccess) {
+    return fail(GF_ECOMM, std::string("ncclAllGather (stats): ") + ncclGetErrorString(r));
+  }
+  GF_HIP(hipEventRecord(h->sg_ev, h->comm_stream));
+  h->sg_pending = true;
+  return GF_OK;
+}
+
+int fe_get_gathered_stats(fe_handle* h, double* dst) {
+  if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (!h->sg_pending) return fail(GF_ESTATE, "no stats all-gather issued");
+  if (int rc = use_dev(h)) return rc;
+  GF_HIP(hipEventSynchronize(h->sg_ev));
+  GF_HIP(hipMemcpy(dst, h->stats_gather, (size_t)h->nranks * h->cfg.n_envs * 2 * sizeof(double),
+                   hipMemcpyDeviceToHost));
+  return GF_OK;
+}
 
 int fe_comm_destroy(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");

@@ -161,6 +161,8 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
+// per env: mean vel_diffs, mean min_dists of launch_stats' outputs -> out (B,2)
+hipError_t launch_stats_summary(const StatsArgs& a, double* out, hipStream_t s);
 // Diagnostic: stream `bytes` of float4 stores into p (nt = non-temporal), the
 // write-bandwidth ceiling of the network buffer on this device.
 hipError_t launch_fill(void* p, size_t bytes, bool nt, hipStream_t s);

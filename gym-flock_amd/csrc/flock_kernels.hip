@@ -534,15 +534,6 @@ __device__ __forceinline__ void with_slices(int S, F&& f) {
     default: f(std::integral_constant<int, 64>{}); break;
   }
 }
-__device__ __forceinline__ unsigned group_min_u32(unsigned w, int S) {
-  if (S > 1) w = min(w, dpp_u32(w, 0xB1));
-  if (S > 2) w = min(w, dpp_u32(w, 0x4E));
-  if (S > 4) w = min(w, dpp_u32(w, 0x141));
-  if (S > 8) w = min(w, dpp_u32(w, 0x140));
-  for (int o = 16; o < S; o <<= 1) w = min(w, static_cast<unsigned>(__shfl_xor(static_cast<int>(w), o)));
-  return w;
-}
-
 // Lane l of (w0, w1) takes the wave-uniform 64-bit mask m.
 // Flocking-v0 predicted row's candidate bound: float32 d2 < bound covers every agent with
 // r2 < th (float32 error of d2 at |d| <= sqrt(th): 2^-23 |d| (Pi + Pj + |d|) + 2^-22 r2,
@@ -1713,6 +1704,28 @@ __global__ __launch_bounds__(kThreads) void flock_stats_kernel(StatsArgs a) {
 }
 
 
+// get_stats() summaries per env for the multi-GPU metrics path: the
+// means of vel_diffs and min_dists over the env's N agents (np.mean of the two arrays
+// flocking_relative.py:140-142 returns), one workgroup per env, a fixed summation tree
+// (deterministic bits; ulps from NumPy's pairwise order).
+__global__ __launch_bounds__(kThreads) void flock_stats_summary_kernel(const double* vd, const double* md,
+                                                                       double* out, int N) {
+  __shared__ double red[8];
+  const size_t e0 = (size_t)blockIdx.x * N;
+  double s0 = 0, s1 = 0;
+  for (int i = threadIdx.x; i < N; i += kThreads) {
+    s0 += vd[e0 + i];
+    s1 += md[e0 + i];
+  }
+  s0 = block_sum(s0, red);
+  s1 = block_sum(s1, red);
+  if (threadIdx.x == 0) {
+    out[2 * (size_t)blockIdx.x] = s0 / static_cast<double>(N);
+    out[2 * (size_t)blockIdx.x + 1] = s1 / static_cast<double>(N);
+  }
+}
+
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- host
@@ -1857,6 +1870,11 @@ extern "C" __attribute__((visibility("default"))) int fe_diag_stamps(unsigned lo
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s) {
   const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
   hipLaunchKernelGGL(flock_stats_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats_summary(const StatsArgs& a, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(flock_stats_summary_kernel, dim3(a.B), dim3(kThreads), 0, s, a.vel_diffs, a.min_dists, out, a.N);
   return hipGetLastError();
 }
 

@@ -88,6 +88,7 @@ SIGNATURES = {
     "fe_controller": [_P, _I, _P],
     "fe_get_stats": [_P, _I, _P, _P],
     "fe_get_stats_ex": [_P, _I, _P, _P, _P],
+    "fe_stats_summary": [_P, _P],
     "fe_get_state_values": [_P, _I, _P],
     "fe_get_network": [_P, _I, _P],
     "fe_get_network_rows": [_P, _I, _I, _I, _P],
@@ -110,6 +111,8 @@ SIGNATURES = {
     "fe_allgather_rewards": [_P],
     "fe_get_gathered_rewards": [_P, _P],
     "fe_gathered_steps": [_P],
+    "fe_allgather_stats": [_P],
+    "fe_get_gathered_stats": [_P, _P],
     "fe_comm_destroy": [_P],
     "fe_set_variant": [_P, _P],
     "fe_set_dt": [_P, _P],
@@ -374,6 +377,12 @@ class FlockHandle:
         check(self.lib.fe_get_stats_ex(self.h, int(env), ptr(vd), ptr(md), ptr(deg)))
         return vd, md, deg
 
+    def stats_summary(self):
+        """(B, 2): np.mean(vel_diffs), np.mean(min_dists) of every env's current state."""
+        out = np.empty((self.n_envs, 2))
+        check(self.lib.fe_stats_summary(self.h, ptr(out)))
+        return out
+
     # -- outputs
     def state_values(self, env=None):
         shape = (self.n_envs, self.n_agents, 6) if env is None else (self.n_agents, 6)
@@ -500,6 +509,16 @@ class FlockHandle:
         out = np.empty((self.nranks, max(steps, 1), self.n_envs))
         check(self.lib.fe_get_gathered_rewards(self.h, ptr(out)))
         return out[:, :steps]
+
+    def allgather_stats(self):
+        """Enqueue the all-gather of every rank's stats_summary() (side stream)."""
+        check(self.lib.fe_allgather_stats(self.h))
+
+    def gathered_stats(self):
+        """(nranks, B, 2) summaries of the latest stats all-gather, rank-major."""
+        out = np.empty((self.nranks, self.n_envs, 2))
+        check(self.lib.fe_get_gathered_stats(self.h, ptr(out)))
+        return out
 
 
 class CoverageHandle:

@@ -3,7 +3,8 @@
 Envs are independent, so the batch is split into contiguous ranges, one per rank
 (one process per GPU); the step path has no exchange. The only collective is the
 metrics path: per-env rewards are all-gathered so every rank (or the trainer on
-rank 0) sees the whole batch's rewards in global env order.
+rank 0) sees the whole batch's rewards in global env order; optionally the per-env
+get_stats summaries (means of vel_diffs and min_dists) likewise.
 
 Transports for that all-gather:
   - RcclRewardGather: RCCL over xGMI, issued by libgymflock on a side stream right
@@ -47,6 +48,15 @@ class RcclRewardGather:
     def result(self):
         g = self.handle.gathered_rewards()  # (world, steps, B)
         return np.concatenate(list(g), axis=1)
+
+    def issue_stats(self):
+        """The optional get_stats aggregates: every rank's per-env means of
+        vel_diffs and min_dists of the current state, all-gathered on the side stream."""
+        self.handle.allgather_stats()
+
+    def stats_result(self):
+        """(world * B, 2) per-env [mean vel_diffs, mean min_dists] in global env order."""
+        return self.handle.gathered_stats().reshape(-1, 2)
 
 
 def check_equal_shards(group, n_envs):
@@ -93,10 +103,11 @@ class HostRewardGather:
 
 
 def check_gathered(group, gathered, local_rewards):
-    """Every rank checks the whole gathered (world * B,) reward vector against the ranks'
-    local rewards, sent over the host channel and concatenated in rank order. Returns
-    (this rank's check, every rank's check)."""
-    want = HostRewardGather(group).gather(local_rewards)
+    """Every rank checks the whole gathered (world * B,) reward vector (or any per-env
+    float64 array, e.g. the (world * B, 2) stats summaries) against the ranks' local
+    values, sent over the host channel and concatenated in rank order. Returns (this
+    rank's check, every rank's check)."""
+    want = HostRewardGather(group).gather(np.asarray(local_rewards, dtype=np.float64).ravel())
     got = np.asarray(gathered, dtype=np.float64).ravel()
     ok = bool(got.shape == want.shape and np.array_equal(got, want))
     return ok, all(group.allgather_bool(ok))

@@ -122,6 +122,10 @@ class VecFlockingRelative:
     def stats(self, env=0):
         return self.h.stats(env)
 
+    def stats_summary(self):
+        """(B, 2) per-env np.mean(vel_diffs), np.mean(min_dists) (get_stats, :136-143)."""
+        return self.h.stats_summary()
+
     def sync(self):
         self.h.sync()
 

@@ -146,6 +146,10 @@ int fe_get_stats(fe_handle* h, int env, double* vel_diffs, double* min_dists);
 /* get_stats plus each agent's degree (r2 < comm_radius^2): reset()'s acceptance test
  * (:177-184) on the device. Any output pointer may be NULL. */
 int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists, int32_t* degree);
+/* Per-env summaries of get_stats for the metrics path: dst (B,2) = np.mean(vel_diffs),
+ * np.mean(min_dists) of every env's current state (flocking_relative.py:136-143), taken
+ * on the device (a fixed summation tree: deterministic, ulps from NumPy's order). */
+int fe_stats_summary(fe_handle* h, double* dst);
 
 /* Outputs (host copies; env < 0 copies all B envs) ---------------------------- */
 int fe_get_state_values(fe_handle* h, int env, float* dst);  /* (N,6) :128-129 */
@@ -201,6 +205,11 @@ int fe_allgather_rewards(fe_handle* h);
  * steps = fe_gathered_steps(h) (oldest first). */
 int fe_get_gathered_rewards(fe_handle* h, double* dst);
 int fe_gathered_steps(fe_handle* h);
+/* Enqueue (side stream) an all-gather of every rank's fe_stats_summary of the current
+ * state: the optional get_stats aggregates of SURVEY.md §8e. fe_get_gathered_stats waits
+ * for it; dst gets (nranks, B, 2), rank-major (global env order). */
+int fe_allgather_stats(fe_handle* h);
+int fe_get_gathered_stats(fe_handle* h, double* dst);
 int fe_comm_destroy(fe_handle* h);
 
 /* ============================ Coverage-v0 ==================================== */

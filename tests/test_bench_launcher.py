@@ -38,6 +38,7 @@ def test_launcher_dry_host(world):
     assert len(d["per_rank_ms_per_step"]) == world
     assert d["ms_per_step"] == max(d["per_rank_ms_per_step"])
     assert d["gathered_rewards_ok"] is True
+    assert d["gathered_stats_ok"] is True
     assert d["config"]["global_envs"] == 2 * world
     assert "torch" not in p.stderr.decode()
 

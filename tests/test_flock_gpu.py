@@ -842,3 +842,44 @@ def test_host_pool_recycles_and_caps():
     gc.collect()
     assert pool.live == 0
     pool.trim()
+
+
+def test_stats_summary_matches_oracle():
+    """fe_stats_summary: per-env np.mean of get_stats' two arrays (flocking_relative.py:
+    136-143), taken on the device for every env of the batch (the metrics path's payload)."""
+    B, N = 5, 200
+    h = nat.FlockHandle(N, B)
+    x0 = synthetic_batch(B, N)
+    h.set_state(x0)
+    u = np.random.RandomState(3).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    h.step(u, 0)
+    summ = h.stats_summary()
+    assert summ.shape == (B, 2)
+    for b in range(B):
+        st = orc.stats(h.get_state(b))
+        np.testing.assert_allclose(summ[b], [st["vel_diffs"].mean(), st["min_dists"].mean()], rtol=1e-13)
+        vd, md, _ = h.stats(b)  # the same device arrays the summary reduces
+        np.testing.assert_allclose(summ[b], [vd.mean(), md.mean()], rtol=1e-13)
+
+
+def test_allgather_stats_one_rank_equals_local_summary():
+    """The RCCL all-gather of the stats summaries (fe_allgather_stats) at one rank: the
+    gathered (1, B, 2) block is the local summary, bit for bit, and stays valid while the
+    next steps run; before any all-gather the getter refuses."""
+    B, N = 6, 128
+    h = nat.FlockHandle(N, B)
+    h.set_state(synthetic_batch(B, N))
+    u = np.random.RandomState(5).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    h.comm_init(1, 0, nat.FlockHandle.comm_unique_id(), timeout=60.0)
+    with pytest.raises(nat.GymFlockError):
+        h.gathered_stats()
+    for _ in range(3):
+        h.step(u, 0)
+    h.allgather_stats()
+    want = h.stats_summary()
+    got = h.gathered_stats()
+    assert got.shape == (1, B, 2)
+    np.testing.assert_array_equal(got[0], want)
+    h.step(u, 0)  # a new summary waits for the pending gather before overwriting its source
+    h.allgather_stats()
+    np.testing.assert_array_equal(h.gathered_stats()[0], h.stats_summary())
