@@ -50,6 +50,12 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 #ifndef GF_P1_PAIR  // pass 1 of the plain step: rows' positions read in pairs (A/B builds: 0)
 #define GF_P1_PAIR 1
 #endif
+#ifndef GF_P1_PAIR_KNN  // the same paired row reads in the fused kNN step (A/B builds: 0)
+#define GF_P1_PAIR_KNN 1
+#endif
+#ifndef GF_KNN_PTAB  // fused kNN: candidate bounds and predicted-row order from LDS tables
+#define GF_KNN_PTAB 1  // (1) or v_readlane / per-row lane compares (0; A/B builds)
+#endif
 #ifndef GF_STORE_TABLE  // network rows: float4 per nibble from a per-row 16-entry LDS table
 #define GF_STORE_TABLE 1  // (2 VALU per float4) or bit extraction (8 VALU; A/B builds: 0)
 #endif

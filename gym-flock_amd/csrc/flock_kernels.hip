@@ -534,6 +534,8 @@ __device__ __forceinline__ void with_slices(int S, F&& f) {
     default: f(std::integral_constant<int, 64>{}); break;
   }
 }
+__device__ __forceinline__ int wid_of(unsigned tid) { return __builtin_amdgcn_readfirstlane(tid >> 6); }
+
 // Lane l of (w0, w1) takes the wave-uniform 64-bit mask m.
 // Flocking-v0 predicted row's candidate bound: float32 d2 < bound covers every agent with
 // r2 < th (float32 error of d2 at |d| <= sqrt(th): 2^-23 |d| (Pi + Pj + |d|) + 2^-22 r2,
@@ -828,6 +830,10 @@ void flock_step_kernel(StepArgs a) {
   float* redf = reinterpret_cast<float*>(red + 4);
   float* inv = reinterpret_cast<float*>(red + 8);
   [[maybe_unused]] float* rthr = inv + R;                      // R kNN candidate radii^2 (0: none)
+  // (GF_KNN_PTAB) each wave's copy of the rows' candidate bounds (read as LDS broadcasts)
+  // and the block's predicted rows in order (prow[p]: the p-th predicted row)
+  [[maybe_unused]] float* ptc = rthr + R + wid_of(threadIdx.x) * R;
+  [[maybe_unused]] int* prow = reinterpret_cast<int*>(rthr + 5 * R);
 
   const int nrows = min(R, N - i0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1015,7 +1021,7 @@ void flock_step_kernel(StepArgs a) {
         rx32 = static_cast<float>(ri.px);
         ry32 = static_cast<float>(ri.py);
         if (wid == 0) rxy[lane] = make_float2(rx32, ry32);
-      } else if (GF_P1_PAIR && !CTRL && KN == 0 && wid == 0 && lane < ((nrows + 3) & ~3)) {
+      } else if (GF_P1_PAIR && !CTRL && (KN == 0 || GF_P1_PAIR_KNN) && wid == 0 && lane < ((nrows + 3) & ~3)) {
         rxy[lane] = make_float2(-1.0e18f, -1.0e18f);  // pass 1's padding rows (far away)
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
@@ -1025,6 +1031,14 @@ void flock_step_kernel(StepArgs a) {
         const bool pr = h >= static_cast<float>(0.64 * a.cr2) && h < 1.0e30f && !GF_ABLATE(a, 0x20000);
         predm = __ballot(pr);
         if (wid == 0 && lane < nrows) rthr[lane] = pr ? 2.25f * h : 0.f;
+        if constexpr (GF_KNN_PTAB) {
+          if (wid == 0 && predm) {  // lane p: the p-th predicted row (published by block_max)
+            int rp = 0, p = 0;
+            for (uint64_t pm = predm; pm; pm &= pm - 1, ++p)
+              if (lane == p) rp = __builtin_ctzll(pm);
+            if (lane < nrows) prow[lane] = rp;
+          }
+        }
       }
     }
     const float Pt = block_max(pt, redf);  // also the barrier that publishes the tile
@@ -1070,7 +1084,49 @@ void flock_step_kernel(StepArgs a) {
 #ifndef GF_PROBE_NO_FUSED
       if constexpr (KN > 0) fused = 2 * __popcll(predm) >= nrows;
 #endif
-      if (fused) {
+      // (GF_KNN_PTAB) the rows' candidate bounds of this tile in the wave's LDS table
+      [[maybe_unused]] float tcr_l = -1.f;
+      if constexpr (KN > 0 && GF_KNN_PTAB) {
+        if (predm) {
+          tcr_l = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
+          if (lane < nrows) ptc[lane] = tcr_l;  // read back by this wave only (in-order LDS)
+        }
+      }
+      if (fused && GF_KNN_PTAB) {
+        // rows in pairs (their LDS reads issued together), as the plain step; rows past
+        // nrows sit far away in rxy and are never predicted
+        auto frow = [&](int r, float2 pr) {
+          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
+          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
+          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
+          band |= (Aa ^ Ma) | (Ab ^ Mb);
+          put_lane(wa0, wa1, Aa, r);
+          put_lane(wb0, wb1, Ab, r);
+          if constexpr (CTRL) {
+            const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
+            const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
+            band |= (Na ^ NMa) | (Nb ^ NMb);
+            put_lane(na0, na1, Na, r);
+            put_lane(nb0, nb1, Nb, r);
+          }
+          if ((predm >> r) & 1) {  // wave-uniform
+            const float tc = ptc[r];
+            put_lane(fca0, fca1, __ballot(d2.x < tc), fp);
+            put_lane(fcb0, fcb1, __ballot(d2.y < tc), fp);
+            ++fp;
+          }
+        };
+        if constexpr (GF_P1_LDSROW && GF_P1_PAIR && GF_P1_PAIR_KNN && !CTRL) {
+          const int nr4 = (nrows + 3) & ~3;
+          for (int r = 0; r < nr4; r += 2) {
+            const float2 p0 = rxy[r], p1 = rxy[r + 1];
+            frow(r, p0);
+            frow(r + 1, p1);
+          }
+        } else {
+          for (int r = 0; r < nrows; ++r) frow(r, row_pos(r));
+        }
+      } else if (fused) {
         const float ftcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
         for (int r = 0; r < nrows; ++r) {
           const float2 pr = row_pos(r);
@@ -1111,7 +1167,7 @@ void flock_step_kernel(StepArgs a) {
             put_lane(nb0, nb1, Nb, r);
           }
         };
-        if constexpr (GF_P1_LDSROW && GF_P1_PAIR && !CTRL && KN == 0) {  // (the others' budgets would spill)
+        if constexpr (GF_P1_LDSROW && GF_P1_PAIR && !CTRL && (KN == 0 || GF_P1_PAIR_KNN)) {  // (the controller's budget would spill)
           // rows in pairs, their two LDS reads issued together (the compiler will not
           // unroll a loop of ballots by a runtime count); rows past nrows sit far away
           // in rxy: no bits, no band, and their lanes store nothing
@@ -1189,7 +1245,7 @@ void flock_step_kernel(StepArgs a) {
           // row lane's candidate test: float32 d2 < tcr covers every agent with r2 < thr
           // (float32 error of d2 at |d| <= sqrt(thr): 2^-23 |d| (Pi + Pj + |d|) +
           // 2^-22 r2, taken x8); none at huge coordinates (those rows go to the rim kNN)
-          const float tcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
+          const float tcr = GF_KNN_PTAB ? tcr_l : cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
           unsigned ca0 = 0, ca1 = 0, cb0 = 0, cb1 = 0;
           int p = 0, rp = 0;
           if (fused) {
@@ -1198,14 +1254,15 @@ void flock_step_kernel(StepArgs a) {
           } else
           for (uint64_t pm = predm; pm; pm &= pm - 1, ++p) {
             const int r = __builtin_ctzll(pm);
-            if (lane == p) rp = r;
+            if (!GF_KNN_PTAB && lane == p) rp = r;
             const float2 pr = row_pos(r);
-            const float tc = readlane_f(tcr, r);
+            const float tc = GF_KNN_PTAB ? ptc[r] : readlane_f(tcr, r);
             const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
             put_lane(ca0, ca1, __ballot(d2.x < tc), p);
             put_lane(cb0, cb1, __ballot(d2.y < tc), p);
           }
           if (lane < p) {
+            if constexpr (GF_KNN_PTAB) rp = prow[lane];
             const int dl = i0 + rp - (j0 + (ca << 6));
             const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
             const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
@@ -1751,7 +1808,8 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
-  s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 2 : 1) + 15) / 16) * 16;
+  // inv (R floats); kNN: rthr (R), the waves' candidate-bound tables (4R), prow (R ints)
+  s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? (GF_KNN_PTAB ? 7 : 2) : 1) + 15) / 16) * 16;
   s += 4 * kStoreTab * 16 + (((size_t)R * 8 + 31) & ~size_t(31));  // row table, rows' float32 positions
   return s;
 }
