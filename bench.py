@@ -766,9 +766,9 @@ def main():
 
     # Flocking-v0 (§8f rank 1): the same step plus the 7-nearest-neighbour observation
     # (flocking.py:20-25), dense network kept; a second handle with n_neighbors=7. The
-    # first handle is closed first: the kNN handle runs four HIP streams, the process's 4
-    # hardware queues (GPU_MAX_HW_QUEUES); a second live handle shares them, which serialises the
-    # step halves and the kNN stream (271 vs 230 us per step with both handles alive)
+    # first handle is closed first so the lines stay independent (a kNN handle runs two
+    # HIP streams, so two handles fit the process's 4 hardware queues: 235.2 vs 235.7 us
+    # with a second live handle, profiles/r03/knn_second_handle.txt)
     env.close()
     if not args.no_knn_line:
         envk = VecFlockingRelative(B, N, device=local_rank, env_offset=rank * B, n_neighbors=7)

@@ -3,7 +3,7 @@
 # build, fe_diag switches), one rocprofv3 --pmc pass per configuration.
 set -e
 export TMPDIR=/tmp
-O=$PWD/gpurun_out/s15
+O=$PWD/gpurun_out/${S15_OUT:-s15}
 mkdir -p $O
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD"
 L=$PWD/build/lib_diag/libgymflock.so
