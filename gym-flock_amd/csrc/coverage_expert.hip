@@ -242,6 +242,19 @@ constexpr int kGreedyRobotsPerBlock = 256 / kGreedyLanes;
 #endif
 constexpr int kGreedyInFlight = GF_GREEDY_INFLIGHT;  // rounds of 16-byte loads issued together
 
+#ifndef GF_GREEDY_SWAR  // uint8 rows: four targets per 32-bit operation (1) or one (0; A/B)
+#define GF_GREEDY_SWAR 1
+#endif
+// 0/1 bytes -> 0/255 bytes: (f << 8) - f, byte by byte without carries (two full-rate
+// operations; a 32-bit multiply by 255 issues at a quarter of the rate)
+__device__ __forceinline__ uint32_t ff_bytes(uint32_t f) { return (f << 8) - f; }
+// First byte of w equal to v (w must hold one): the zero-byte test on w ^ v..v, whose
+// lowest flagged byte is exact (borrows only flag bytes above a zero byte).
+__device__ __forceinline__ int first_byte_eq(uint32_t w, uint32_t v) {
+  const uint32_t x = w ^ (v * 0x01010101u);
+  return __builtin_ctz((x - 0x01010101u) & ~x & 0x80808080u) >> 3;
+}
+
 __global__ __launch_bounds__(256) void cov_greedy_kernel(CovGreedyArgs a) {
   const int b = blockIdx.x;
   const int sl = threadIdx.x & (kGreedyLanes - 1);
@@ -251,6 +264,7 @@ __global__ __launch_bounds__(256) void cov_greedy_kernel(CovGreedyArgs a) {
   const int ir = vr ? i : 0;
   const int R = a.R, Tm = a.Tmax;
   const int T = a.ntg[b];
+  const bool swar = GF_GREEDY_SWAR && a.cost8 && !a.wide[b];
   int c;
   if (a.dirty[b]) {  // robots were placed externally: closest_targets (:427-432)
     const double* tg = a.tgt + (size_t)b * Tm * 2;
@@ -288,7 +302,55 @@ __global__ __launch_bounds__(256) void cov_greedy_kernel(CovGreedyArgs a) {
     const uint32_t kt = (v << 16) | (uint32_t)t;  // min value, then first index (np.argmin)
     key = kt < key ? kt : key;
   };
-  if (a.cost8 && !a.wide[b]) {  // one byte per entry (inf = 255): 16 targets per load
+  if (swar) {
+    // One byte per entry; masked (visited, inf = 255, target 0 once anything is visited)
+    // entries become 255, above every hop count (<= 254 here), so the argmin of the
+    // masked row in bytes is the reference's (min value, then first index). Each lane
+    // takes four targets per 32-bit operation: the masked word c | 255 * visited, its
+    // smallest byte, and the first word (in t order) holding the lane's minimum; the
+    // group's minimum value m and the first index of m follow from those words.
+    const uint8_t* row8 = a.cost8 + ((size_t)b * Tm + c) * Tm;
+    uint32_t lmin = 0x100u, lword = 0xFFFFFFFFu;
+    int lpos = 0;
+    auto word = [&](uint32_t m, int tb) {
+      const uint32_t dm = min(min(m & 0xFFu, (m >> 8) & 0xFFu), min((m >> 16) & 0xFFu, m >> 24));
+      if (dm < lmin) {  // strict: the lane's first word holding its minimum
+        lmin = dm;
+        lword = m;
+        lpos = tb;
+      }
+    };
+    constexpr int kStride = 16 * kGreedyLanes;
+    int t0 = 0;
+    if ((Tm & 15) == 0) {
+      for (; t0 + kGreedyInFlight * kStride <= T; t0 += kGreedyInFlight * kStride) {
+        uint4 cv[kGreedyInFlight], fv[kGreedyInFlight];
+#pragma unroll
+        for (int k = 0; k < kGreedyInFlight; ++k) {
+          const int t = t0 + k * kStride + 16 * sl;
+          cv[k] = *reinterpret_cast<const uint4*>(row8 + t);
+          fv[k] = *reinterpret_cast<const uint4*>(vis + t);
+        }
+        if (t0 == 0 && sl == 0 && any_vis) fv[0].x |= 1u;  // target 0 (the np.where quirk)
+#pragma unroll
+        for (int k = 0; k < kGreedyInFlight; ++k) {
+          const int t = t0 + k * kStride + 16 * sl;
+          word(cv[k].x | ff_bytes(fv[k].x), t);
+          word(cv[k].y | ff_bytes(fv[k].y), t + 4);
+          word(cv[k].z | ff_bytes(fv[k].z), t + 8);
+          word(cv[k].w | ff_bytes(fv[k].w), t + 12);
+        }
+      }
+    }
+    for (int t = t0 + sl; t < T; t += kGreedyLanes) {  // the rest, one target per word
+      const bool msk = vis[t] || (t == 0 && any_vis);
+      word((msk ? 0xFFu : (uint32_t)row8[t]) | 0xFFFFFF00u, t);
+    }
+    const uint32_t m = group_min_u32<kGreedyLanes>(lmin);
+    const uint32_t cand = (lmin == m && m <= 0xFFu) ? (uint32_t)(lpos + first_byte_eq(lword, m)) : 0xFFFFu;
+    const uint32_t goal = group_min_u32<kGreedyLanes>(cand);
+    key = ((m >= 0xFFu ? (uint32_t)kMaxCost : m) << 16) | goal;
+  } else if (a.cost8 && !a.wide[b]) {  // one byte per entry (inf = 255): 16 targets per load
     const uint8_t* row8 = a.cost8 + ((size_t)b * Tm + c) * Tm;
     constexpr int kStride = 16 * kGreedyLanes;
     int t0 = 0;

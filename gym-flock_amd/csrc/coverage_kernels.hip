@@ -545,7 +545,7 @@ __global__ __launch_bounds__(kCovThreads) void cov_reset_kernel(CovArgs a, const
   float* nodes = a.nodes + (size_t)b * M * 3;
   int local = 0;
   for (int t = threadIdx.x; t < Tm; t += kCovThreads) {
-    const uint8_t v = t < T ? visited0[(size_t)b * Tm + t] : 1;
+    const uint8_t v = t < T ? (visited0[(size_t)b * Tm + t] ? 1 : 0) : 1;  // flags are 0 / 1
     a.visited[(size_t)b * Tm + t] = v;
     if (t < T) {
       nodes[3 * (t + R) + 2] = v ? 0.0f : 1.0f;
