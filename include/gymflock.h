@@ -206,8 +206,11 @@ int fe_allgather_rewards(fe_handle* h);
 int fe_get_gathered_rewards(fe_handle* h, double* dst);
 int fe_gathered_steps(fe_handle* h);
 /* Enqueue (side stream) an all-gather of every rank's fe_stats_summary of the current
- * state: the optional get_stats aggregates of SURVEY.md §8e. fe_get_gathered_stats waits
- * for it; dst gets (nranks, B, 2), rank-major (global env order). */
+ * state: the optional get_stats aggregates of SURVEY.md §8e. The summaries are taken
+ * on the handle's stream after both step halves (a join, so the next step is one launch,
+ * unlike the reward all-gather); call it per episode or logging interval, not per step.
+ * fe_get_gathered_stats waits for it; dst gets (nranks, B, 2), rank-major (global env
+ * order). */
 int fe_allgather_stats(fe_handle* h);
 int fe_get_gathered_stats(fe_handle* h, double* dst);
 int fe_comm_destroy(fe_handle* h);
