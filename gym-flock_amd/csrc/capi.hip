@@ -451,7 +451,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
     const int B = a.B, B0 = (B + 1) / 2;
     const gf::StepArgs a1 = env_range(h, a, B0, B - B0, uf64);
     hipError_t e = hipSuccess;
-    if (h->dephase && GF_DEPHASE && B0 >= 2) {
+    if (h->dephase && B0 >= 2) {
       // both streams idle (the first split step after other work): the second half
       // would start beside the first and the two would run in phase for many steps.
       // The first half's first quarter goes alone, the second half starts after it, and
@@ -542,7 +542,7 @@ int launch_knn_cur(fe_handle* h, int mode) {
       k1.obs = k.obs + e0 * 4 * K;
       k1.r2k = k.r2k + e0;
       k1.rimflag = k.rimflag + (size_t)B0 * ((N + gf::kThreads - 1) / gf::kThreads);
-      k.grid_cap = k1.grid_cap = GF_RIM_HALF_GRID;
+      k.grid_cap = k1.grid_cap = gf::kKnnRimHalfGrid;
       hipError_t e = gf::launch_knn(k, h->stream);
       if (e == hipSuccess) e = gf::launch_knn(k1, h->stream2);
       if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);

@@ -232,19 +232,11 @@ __device__ __forceinline__ uint32_t group_min_u32(uint32_t w) {
 // wave, 32 per workgroup. A wave per robot left ~100k waves, each a chain of dependent
 // loads, for 512 envs x 200 robots: 47.1 -> 33.4 us per expert step with 16 lanes, 32.4
 // with 8.
-#ifndef GF_GREEDY_LANES
-#define GF_GREEDY_LANES 8
-#endif
-constexpr int kGreedyLanes = GF_GREEDY_LANES;
+constexpr int kGreedyLanes = 8;
 constexpr int kGreedyRobotsPerBlock = 256 / kGreedyLanes;
-#ifndef GF_GREEDY_INFLIGHT
-#define GF_GREEDY_INFLIGHT 4
-#endif
-constexpr int kGreedyInFlight = GF_GREEDY_INFLIGHT;  // rounds of 16-byte loads issued together
+constexpr int kGreedyInFlight = 4;  // rounds of 16-byte loads issued together
 
-#ifndef GF_GREEDY_SWAR  // uint8 rows: four targets per 32-bit operation (1) or one (0; A/B)
-#define GF_GREEDY_SWAR 1
-#endif
+// uint8 rows are searched four targets per 32-bit operation (SWAR)
 // 0/1 bytes -> 0/255 bytes: (f << 8) - f, byte by byte without carries (two full-rate
 // operations; a 32-bit multiply by 255 issues at a quarter of the rate)
 __device__ __forceinline__ uint32_t ff_bytes(uint32_t f) { return (f << 8) - f; }
@@ -264,7 +256,7 @@ __global__ __launch_bounds__(256) void cov_greedy_kernel(CovGreedyArgs a) {
   const int ir = vr ? i : 0;
   const int R = a.R, Tm = a.Tmax;
   const int T = a.ntg[b];
-  const bool swar = GF_GREEDY_SWAR && a.cost8 && !a.wide[b];
+  const bool swar = a.cost8 && !a.wide[b];
   int c;
   if (a.dirty[b]) {  // robots were placed externally: closest_targets (:427-432)
     const double* tg = a.tgt + (size_t)b * Tm * 2;

@@ -19,18 +19,6 @@ namespace gf {
 namespace {
 
 constexpr int kCovThreads = 256;
-#ifndef GF_COV_STEP_NT  // R <= 256: threads per env workgroup (A/B builds: 64 or 128 hold
-#define GF_COV_STEP_NT 256  // 4 or 2 robots per lane; one wave measured 8.9 vs 7.3 us)
-#endif
-#ifndef GF_COV_LDS_ORDER  // claim rounds: compiler-only ordering of the wave's LDS operations
-#define GF_COV_LDS_ORDER 1
-#endif
-#ifndef GF_COV_SKIP_CONST  // steps skip the tail's constant robot-index stores (A/B: 0)
-#define GF_COV_SKIP_CONST 1
-#endif
-#ifndef GF_COV_TAGGED  // claim rounds tagged (no table clearing) or cleared (A/B builds)
-#define GF_COV_TAGGED 0
-#endif
 
 // Phase timeline (diagnostic builds only, -DGF_STAMPS): thread 0 of each workgroup
 // records s_memrealtime (100 MHz) at: start (0), first round trip done (1), claims done
@@ -337,16 +325,10 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
       // A wave's LDS operations complete in order, so a round needs no workgroup
       // barrier, only waits for its own LDS operations.
       if (tid < 64) {
-        // wait for this wave's LDS operations only (a fence would also wait for the
-        // node prefetch still in flight from global memory)
-        // GF_COV_LDS_ORDER: a wave's LDS instructions execute in issue order, so only the
-        // compiler must keep them in order (the reads' results are waited for as used)
-        auto lds_fence = [] {
-          if (GF_COV_LDS_ORDER)
-            asm volatile("" ::: "memory");
-          else
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        };
+        // a wave's LDS instructions execute in issue order, so only the compiler must
+        // keep them in order (the reads' results are waited for as used; a fence would
+        // also wait for the node prefetch still in flight from global memory)
+        auto lds_fence = [] { asm volatile("" ::: "memory"); };
         // four named robots, not an array: an array indexed in a loop stays in scratch
         struct Rb {
           int i, c, n, v;
@@ -362,15 +344,6 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
           r.v = r.n;  // guess: every move succeeds
         };
         // branch-free rounds: a robot that does not move adds INT_MAX (no-op).
-#if GF_COV_TAGGED
-        // Claims carry the round: (tag << 9) | robot, the tag falling by one per round, so
-        // atomicMin keeps this round's first claimer over any earlier round's, and an
-        // entry with another tag is no claim this round (no table clearing between rounds)
-        int tag = 1 << 12;
-        auto put = [&](const Rb& r) { atomicMin(&first[r.v], r.mv ? (tag << 9) | r.i : INT_MAX); };
-        auto eval = [&](Rb& r, int e) {
-          const int f = (e >> 9) == tag ? (e & 511) : INT_MAX;
-#else
         // A mover's claim sits on its chosen node or its own; both are cleared between
         // rounds (a non-mover's own node: no mover's test reads it, since movers onto it
         // are blocked by its stay claim; robots past R sit on node 0, a slot no target uses)
@@ -380,7 +353,6 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
           first[r.c] = INT_MAX;
         };
         auto eval = [&](Rb& r, int f) {
-#endif
           const int v = (r.fr && f >= r.i) ? r.n : r.c;  // r.fr implies r.mv
           const bool ch = v != r.v;
           r.v = v;
@@ -398,13 +370,9 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
           // all four evaluated (no short circuit)
           const int changed = int(eval(r0, f0)) | int(eval(r1, f1)) | int(eval(r2, f2)) | int(eval(r3, f3));
           if (!__any(changed)) break;
-#if GF_COV_TAGGED
-          --tag;  // at most R + 1 <= 257 rounds: the tag stays positive
-#else
           lds_fence();
           clear(r0), clear(r1), clear(r2), clear(r3);
           lds_fence();
-#endif
         }
         if (r0.i < R) new_s[r0.i] = r0.v;
         if (r1.i < R) new_s[r1.i] = r1.v;
@@ -492,7 +460,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     const int k = base + 4 * i;
     *reinterpret_cast<int4*>(snd + k) = q;
     *reinterpret_cast<int4*>(rcv + k + 4 * R) = q;
-    if (full || !GF_COV_SKIP_CONST) {
+    if (full) {
       const int4 ii = make_int4(i, i, i, i);
       *reinterpret_cast<int4*>(snd + k + 4 * R) = ii;
       *reinterpret_cast<int4*>(rcv + k) = ii;
@@ -659,11 +627,8 @@ hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {
   // per step, and the hipLaunchKernelGGL wrapper's repacking measured ~0.15 us more per
   // launch (scripts/graphprobe.hip)
   void* args[] = {const_cast<CovArgs*>(&a)};
-  const bool narrow = a.R <= kCovThreads && GF_COV_STEP_NT != kCovThreads;
-  const void* f = narrow ? reinterpret_cast<const void*>(&cov_step_kernel<GF_COV_STEP_NT>)
-                         : reinterpret_cast<const void*>(&cov_step_kernel<kCovThreads>);
-  return hipLaunchKernel(f, dim3(a.B), dim3(narrow ? GF_COV_STEP_NT : kCovThreads), args,
-                         cov_step_lds_bytes(a.R, a.M), s);
+  return hipLaunchKernel(reinterpret_cast<const void*>(&cov_step_kernel<kCovThreads>), dim3(a.B), dim3(kCovThreads),
+                         args, cov_step_lds_bytes(a.R, a.M), s);
 }
 
 #ifdef GF_STAMPS

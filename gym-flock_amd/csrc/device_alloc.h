@@ -3,10 +3,6 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
-#ifndef GF_CONTIGUOUS_OUTPUTS  // buffers >= 256 MiB physically contiguous when possible
-#define GF_CONTIGUOUS_OUTPUTS 1   // (A/B builds: 0)
-#endif
-
 namespace gf {
 
 // Large buffers (the dense network: 1 GiB at config 2, 8 GiB at config 5; the Coverage
@@ -15,7 +11,7 @@ namespace gf {
 // profiles/r03/ab_contiguous_outputs.txt). If the device cannot provide one, plain
 // hipMalloc; the failed request's error is cleared so later launch checks do not see it.
 inline hipError_t device_alloc(void** p, size_t bytes) {
-  if (bytes >= (size_t(256) << 20) && GF_CONTIGUOUS_OUTPUTS &&
+  if (bytes >= (size_t(256) << 20) &&
       hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess)
     return hipSuccess;
   (void)hipGetLastError();

@@ -17,57 +17,14 @@ namespace gf {
 constexpr int kThreads = 256;   // 4 wave64s per workgroup
 constexpr int kTileMax = 1024;      // max agents per LDS tile (32 KiB of float64 state)
 constexpr int kTileDefault = 512;   // default tile (measured best, see step_tile)
-#ifndef GF_LDS_PLAIN_FLOOR_KIB  // (a compile-time knob for A/B builds, scripts/build_variant.sh)
-#define GF_LDS_PLAIN_FLOOR_KIB 24
-#endif
-constexpr size_t kStepLdsPlainFloor = GF_LDS_PLAIN_FLOOR_KIB * 1024;  // plain step: 6 workgroups per CU, not 7
+constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
-#ifndef GF_DEPHASE  // split steps: de-phase the halves at the first split step (A/B builds)
-#define GF_DEPHASE 1
-#endif
-#ifndef GF_KNN_MED3  // fused kNN: list insertion by v_med3_u32 (1) or a min/max chain (0)
-#define GF_KNN_MED3 1
-#endif
-#ifndef GF_RECIP_NR  // pair terms' 1/r2: 0 = IEEE division, 1 = rcp + Newton without the
-#define GF_RECIP_NR 1  // controller, 2 = everywhere (A/B builds)
-#endif
-#ifndef GF_KNN_LATE_GATHER  // fused kNN: the neighbour's state is loaded after the epilogue (1)
-#define GF_KNN_LATE_GATHER 0  // or before it, its latency under the epilogue's sums (0)
-#endif
-#ifndef GF_KNN_LEAN  // fused kNN: velocity sums in the reward block epilogue (1) or staged (0)
-#define GF_KNN_LEAN 0  // (A/B builds)
-#endif
-#ifndef GF_INLINE_RIM_U  // fused kNN inline rim scan: columns in flight per lane
-#define GF_INLINE_RIM_U 4
-#endif
-#ifndef GF_P1_FMA  // pass 1: float32 d2 as one fused multiply-add (the band covers its
-#define GF_P1_FMA 1   // rounding, which is smaller than the unfused form's); 0 = unfused (A/B)
-#endif
-#ifndef GF_P1_LDSROW  // pass 1: each row's float32 position read as an LDS broadcast (1) or
-#define GF_P1_LDSROW 1  // by two v_readlane (0; A/B builds)
-#endif
-#ifndef GF_P1_PAIR  // pass 1 of the plain step: rows' positions read in pairs (A/B builds: 0)
-#define GF_P1_PAIR 1
-#endif
-#ifndef GF_P1_PAIR_KNN  // the same paired row reads in the fused kNN step (A/B builds: 0)
-#define GF_P1_PAIR_KNN 1
-#endif
-#ifndef GF_KNN_PTAB  // fused kNN: candidate bounds and predicted-row order from LDS tables
-#define GF_KNN_PTAB 1  // (1) or v_readlane / per-row lane compares (0; A/B builds)
-#endif
-#ifndef GF_STORE_TABLE  // network rows: float4 per nibble from a per-row 16-entry LDS table
-#define GF_STORE_TABLE 1  // (2 VALU per float4) or bit extraction (8 VALU; A/B builds: 0)
-#endif
-#ifndef GF_KNN_SLICE_LIST  // fused kNN: keys each feature-pass slice keeps (A/B builds)
-#define GF_KNN_SLICE_LIST 7
-#endif
+constexpr int kInlineRimU = 4;      // fused kNN inline rim scan: columns in flight per lane
 constexpr int kStoreTab = 16;      // network rows: float4 table entries per wave (one per nibble)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
-constexpr int kKnnRimGrid = 256;
-#ifndef GF_RIM_HALF_GRID  // rim kNN workgroups per half-batch launch (A/B builds)
-#define GF_RIM_HALF_GRID (gf::kKnnRimGrid / 2)
-#endif    // rim kNN: workgroups walking the flagged blocks
+constexpr int kKnnRimGrid = 256;     // rim kNN: workgroups walking the flagged blocks
+constexpr int kKnnRimHalfGrid = kKnnRimGrid / 2;  // the same per half-batch launch
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
                                     // scanned wave-cooperatively from L2, more through the grid
 // kNN LDS: positions (16 B per agent), the grid's cell offsets, agent indices by cell

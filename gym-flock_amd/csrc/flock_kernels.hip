@@ -189,10 +189,9 @@ __device__ __forceinline__ St load_state(const StepArgs& a, size_t g) {
   }
 }
 
-// Sorted insertion of (r2, j) into a K-list; ties go to the lower index (stable).
 // 1/r2 for the feature pair terms (float32 outputs) without the controller: v_rcp_f64
 // refined by one Newton step (about 2^-50 relative, 3 float64 ops instead of the 10 of a
-// correctly rounded division; GF_RECIP_NR). The controller keeps the IEEE division.
+// correctly rounded division). The controller keeps the IEEE division.
 __device__ __forceinline__ double recip_f64(double r2) {
   // one Newton step on v_rcp_f64; outside [2^-1000, 2^1000] (zero, denormals, huge,
   // inf, NaN) the raw v_rcp_f64 value, chosen without a branch
@@ -343,7 +342,7 @@ __device__ __forceinline__ void step_inline_rim(const StepArgs& a, size_t env0, 
       lr[m] = __builtin_inf();
       lj[m] = INT_MAX;
     }
-    constexpr int U = GF_INLINE_RIM_U;  // columns in flight per lane
+    constexpr int U = kInlineRimU;  // columns in flight per lane
     for (int j0 = lane; j0 < N; j0 += U * 64) {
       St p[U];
 #pragma unroll
@@ -455,14 +454,7 @@ __device__ __forceinline__ float2 pos32(const St& s) {
 // pass 1's float32 squared distance of a row (xi, yi) to a wave's two columns
 __device__ __forceinline__ f2v d2_f32(float xi, float yi, f2v qx, f2v qy) {
   const f2v dx = xi - qx, dy = yi - qy;
-  if constexpr (GF_P1_FMA)
-    return __builtin_elementwise_fma(dx, dx, dy * dy);
-  else
-    return dx * dx + dy * dy;
-}
-
-__device__ __forceinline__ float readlane_f(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+  return __builtin_elementwise_fma(dx, dx, dy * dy);
 }
 
 // A value the whole wave holds (compiler-visible as scalar).
@@ -568,7 +560,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
   const int per = (nrows + 3) >> 2;
   // fast form (N % 1024 == 0): every lane owns float4 columns lane + 64m of a row, so
   // its nibble sits at a fixed bit offset of 32-bit words 8 apart; four words are read
-  // ahead and each float becomes sign-extended bit & bits(1/deg) (2 VALU per float).
+  // ahead and each nibble selects a float4 from the row's table (below).
   // The host picks it per kernel (StepArgs.store_fast; diag 64 / 128 force it off / on).
   const bool fast = (N & 1023) == 0 && !GF_ABLATE(a, (4 | 64)) && (a.store_fast || GF_ABLATE(a, 128));
   const unsigned* bits32 = reinterpret_cast<const unsigned*>(adj);
@@ -586,7 +578,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
       for (int q = lane; q < (N >> 2); q += 64) r4[q] = f4v{iv, 0.f, iv, 0.f};
       continue;
     }
-    if (fast && GF_STORE_TABLE) {
+    if (fast) {
       // the row's 16 float4 values by nibble in the wave's LDS table (a wave's LDS
       // operations run in order: the previous row's reads precede this write, and this
       // write the reads below), then per float4 one bit-field extract and one address
@@ -602,24 +594,6 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
         for (int k = 0; k < 4; ++k) w[k] = wr[8 * (c + k)];
 #pragma unroll
         for (int k = 0; k < 4; ++k) dst[64 * (c + k)] = tab[__builtin_amdgcn_ubfe(w[k], o0, 4)];
-      }
-    } else if (fast) {
-      const int ivb = __float_as_int(iv);
-      const unsigned* wr = bits32 + (size_t)r * 2 * Wn + wsel;
-      f4v* dst = reinterpret_cast<f4v*>(rowp) + lane;
-#pragma unroll 1
-      for (int c = 0; c < (N >> 8); c += 4) {
-        int w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = static_cast<int>(wr[8 * (c + k)]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const f4v v = {__int_as_float(__builtin_amdgcn_sbfe(w[k], o0, 1) & ivb),
-                         __int_as_float(__builtin_amdgcn_sbfe(w[k], o0 + 1, 1) & ivb),
-                         __int_as_float(__builtin_amdgcn_sbfe(w[k], o0 + 2, 1) & ivb),
-                         __int_as_float(__builtin_amdgcn_sbfe(w[k], o0 + 3, 1) & ivb)};
-          dst[64 * (c + k)] = v;
-        }
       }
     } else if (vec4) {
       f4v* r4 = reinterpret_cast<f4v*>(rowp);
@@ -643,7 +617,7 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
 // row combined, state_values (:124-129), the updated state, the controller (:194-226)
 // and, by the env's first block, the reward (instant_cost :145-147). `writer` = the
 // thread holding slice 0 of a valid row.
-template <bool DYN, bool UF64, bool CTRL, bool VAR, bool SVACC = true>
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
 __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile, double* red, const St& me,
                                               double f0, double f1, double f2, double f3, double f4,
                                               double f5, double gx, double gy, double svx, double svy, int b,
@@ -665,14 +639,8 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
     }
   });
 
-  // SVACC: every thread summed its share of the env's velocities while staging the tiles;
-  // otherwise (the fused kNN step, whose registers are short) the reward block sums them
-  // here in the same per-thread order (j = tid, tid + kThreads, ...), so the bits agree
-  double Svx = 0, Svy = 0;
-  if constexpr (SVACC) {
-    Svx = block_sum(svx, red);
-    Svy = block_sum(svy, red);
-  }
+  // every thread summed its share of the env's velocities while staging the tiles
+  const double Svx = block_sum(svx, red), Svy = block_sum(svy, red);
 
   if (writer && !GF_ABLATE(a, 256)) {  // diag 256: skip the per-row outputs (timing only)
     const size_t g = env0 + i_row;
@@ -721,23 +689,6 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
   // instant_cost (:145-147) = -(var(vx) + var(vy)), two-pass like np.var, by the env's
   // first row block; single-tile envs read the velocities from the LDS tile
   if (a.reward && i0 == 0 && !GF_ABLATE(a, 512)) {  // diag 512: skip the reward (timing only)
-    if constexpr (!SVACC) {
-      double sx = 0, sy = 0;
-      if (N <= T) {
-        for (int t = tid; t < N; t += kThreads) {
-          sx += tile[t].vx;
-          sy += tile[t].vy;
-        }
-      } else {
-        for (int j = tid; j < N; j += kThreads) {
-          const St s = load_state<DYN, UF64, VAR>(a, env0 + j);
-          sx += s.vx;
-          sy += s.vy;
-        }
-      }
-      Svx = block_sum(sx, red);
-      Svy = block_sum(sy, red);
-    }
     const double mx = Svx / static_cast<double>(N), my = Svy / static_cast<double>(N);
     double qx = 0, qy = 0;
     if (N <= T) {
@@ -767,21 +718,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 // no spills; its LDS is floored to hold it at 6 workgroups per CU, see
 // kStepLdsPlainFloor), 6 with the controller (79 VGPRs, 23.2 KiB of LDS: 6 per CU);
 // variants are not capped (their extra state would spill).
-#ifndef GF_STEP_WAVES_PLAIN
-#define GF_STEP_WAVES_PLAIN 6
-#endif
-#ifndef GF_STEP_WAVES_PF
-#define GF_STEP_WAVES_PF 4
-#endif
-#ifndef GF_STEP_WAVES_CTRL
-#define GF_STEP_WAVES_CTRL 6
-#endif
-#ifndef GF_STEP_WAVES_KNN
-#define GF_STEP_WAVES_KNN 5
-#endif
-#ifndef GF_STEP_WAVES_KNN_CTRL
-#define GF_STEP_WAVES_KNN_CTRL 4
-#endif
+constexpr int kWavesPlain = 6, kWavesPf = 4, kWavesCtrl = 6, kWavesKnn = 5, kWavesKnnCtrl = 4;
 // Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
 // wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
 // its HW_ID / XCC_ID, for scripts/phase_timeline.py. Product builds compile it out.
@@ -805,9 +742,9 @@ __device__ unsigned long long gf_stamp_buf[8192 * 16];
 // feature pass, and the row's k nearest indices and observation are written (below).
 template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
 __global__ __launch_bounds__(kThreads, VAR ? 1
-                                           : (PF ? GF_STEP_WAVES_PF
-                                                 : (KN ? (CTRL ? GF_STEP_WAVES_KNN_CTRL : GF_STEP_WAVES_KNN)
-                                                       : (CTRL ? GF_STEP_WAVES_CTRL : GF_STEP_WAVES_PLAIN))))
+                                           : (PF ? kWavesPf
+                                                 : (KN ? (CTRL ? kWavesKnnCtrl : kWavesKnn)
+                                                       : (CTRL ? kWavesCtrl : kWavesPlain))))
 void flock_step_kernel(StepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
@@ -830,7 +767,7 @@ void flock_step_kernel(StepArgs a) {
   float* redf = reinterpret_cast<float*>(red + 4);
   float* inv = reinterpret_cast<float*>(red + 8);
   [[maybe_unused]] float* rthr = inv + R;                      // R kNN candidate radii^2 (0: none)
-  // (GF_KNN_PTAB) each wave's copy of the rows' candidate bounds (read as LDS broadcasts)
+  // each wave's copy of the rows' candidate bounds (read as LDS broadcasts)
   // and the block's predicted rows in order (prow[p]: the p-th predicted row)
   [[maybe_unused]] float* ptc = rthr + R + wid_of(threadIdx.x) * R;
   [[maybe_unused]] int* prow = reinterpret_cast<int*>(rthr + 5 * R);
@@ -879,8 +816,6 @@ void flock_step_kernel(StepArgs a) {
   const bool frow = fr < nrows;
   double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
   double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
-  // the fused kNN step leaves the velocity sums to the reward block's epilogue (4 VGPRs)
-  constexpr bool kSvAcc = CTRL || KN == 0 || !GF_KNN_LEAN;
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
   // kNN rows predicted to lack k neighbours (their k-th nearest two states back was
   // at >= 0.8 comm_radius): predm (wave-uniform) marks them, rthr[r] holds row r's
@@ -902,7 +837,7 @@ void flock_step_kernel(StepArgs a) {
   // merge detects the only way that can happen and leaves such a row unranked. (Lists
   // of 4 or 5 measured no faster: with 4, ~1 % of the rows hold 5 of their 8 nearest in
   // one slice and fall to the exact scan.)
-  constexpr int KL = KN > 0 ? (KN < GF_KNN_SLICE_LIST ? KN : GF_KNN_SLICE_LIST) : 1;
+  constexpr int KL = KN > 0 ? KN : 1;
   [[maybe_unused]] unsigned kk[KL];
   if constexpr (KN > 0) {
 #pragma unroll
@@ -917,31 +852,16 @@ void flock_step_kernel(StepArgs a) {
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
     if constexpr (KN > 0) {
-#ifndef GF_PROBE_NO_INSERT
-     if (!GF_ABLATE(a, 0x200000)) {  // diag 0x200000: no insertion (timing only)
-#else
-     if (false) {
-#endif
-      // q = min(floor(r2 * ksc), qmax); fmin returns qmax for a NaN r2 (ranked last)
-      const unsigned q = static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
-      const unsigned v = (q << a.knn_jbits) | static_cast<unsigned>(j0 + c);
-      if constexpr (GF_KNN_MED3) {
-        knn_list_insert<KL>(kk, v);
-      } else {
-        unsigned w = v;
-#pragma unroll
-        for (int m = 0; m < KL; ++m) {
-          const unsigned lo = min(kk[m], w);
-          w = max(kk[m], w);
-          kk[m] = lo;
-        }
+      if (!GF_ABLATE(a, 0x200000)) {  // diag 0x200000: no insertion (timing only)
+        // q = min(floor(r2 * ksc), qmax); fmin returns qmax for a NaN r2 (ranked last)
+        const unsigned q = static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
+        knn_list_insert<KL>(kk, (q << a.knn_jbits) | static_cast<unsigned>(j0 + c));
       }
-     }
       if (!isadj && !(CTRL && isnear)) return;  // a candidate only: no features
     }
     // one reciprocal per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
     // reference's two divisions; far inside the float32 outputs' tolerance)
-    const double ir = (GF_RECIP_NR >= (CTRL ? 2 : 1)) ? recip_f64(r2) : 1.0 / r2, irr = ir * ir;
+    const double ir = CTRL ? 1.0 / r2 : recip_f64(r2), irr = ir * ir;
     const double q1x = dx * irr, q2x = dx * ir;
     const double q1y = dy * irr, q2y = dy * ir;
     if (isadj) {
@@ -1001,10 +921,8 @@ void flock_step_kernel(StepArgs a) {
       tile[t] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
       pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
-      if constexpr (kSvAcc) {
-        svx += s.vx;
-        svy += s.vy;
-      }
+      svx += s.vx;
+      svy += s.vy;
     };
     if constexpr (PF >= 1) {
 #pragma unroll
@@ -1021,7 +939,7 @@ void flock_step_kernel(StepArgs a) {
         rx32 = static_cast<float>(ri.px);
         ry32 = static_cast<float>(ri.py);
         if (wid == 0) rxy[lane] = make_float2(rx32, ry32);
-      } else if (GF_P1_PAIR && !CTRL && (KN == 0 || GF_P1_PAIR_KNN) && wid == 0 && lane < ((nrows + 3) & ~3)) {
+      } else if (!CTRL && wid == 0 && lane < ((nrows + 3) & ~3)) {
         rxy[lane] = make_float2(-1.0e18f, -1.0e18f);  // pass 1's padding rows (far away)
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
@@ -1031,13 +949,11 @@ void flock_step_kernel(StepArgs a) {
         const bool pr = h >= static_cast<float>(0.64 * a.cr2) && h < 1.0e30f && !GF_ABLATE(a, 0x20000);
         predm = __ballot(pr);
         if (wid == 0 && lane < nrows) rthr[lane] = pr ? 2.25f * h : 0.f;
-        if constexpr (GF_KNN_PTAB) {
-          if (wid == 0 && predm) {  // lane p: the p-th predicted row (published by block_max)
-            int rp = 0, p = 0;
-            for (uint64_t pm = predm; pm; pm &= pm - 1, ++p)
-              if (lane == p) rp = __builtin_ctzll(pm);
-            if (lane < nrows) prow[lane] = rp;
-          }
+        if (wid == 0 && predm) {  // lane p: the p-th predicted row (published by block_max)
+          int rp = 0, p = 0;
+          for (uint64_t pm = predm; pm; pm &= pm - 1, ++p)
+            if (lane == p) rp = __builtin_ctzll(pm);
+          if (lane < nrows) prow[lane] = rp;
         }
       }
     }
@@ -1060,11 +976,8 @@ void flock_step_kernel(StepArgs a) {
     }
     ba.lo = uniform_f(ba.lo); ba.hi = uniform_f(ba.hi);
     bn.lo = uniform_f(bn.lo); bn.hi = uniform_f(bn.hi);
-    // row r's float32 position: an LDS broadcast (no VALU) or two v_readlane
-    auto row_pos = [&](int r) {
-      if constexpr (GF_P1_LDSROW) return rxy[r];
-      else return make_float2(readlane_f(rx32, r), readlane_f(ry32, r));
-    };
+    // row r's float32 position: an LDS broadcast (no VALU)
+    auto row_pos = [&](int r) { return rxy[r]; };
     for (int cp = GF_ABLATE(a, 8) ? npair : wid; cp < npair; cp += 4) {
       const int ca = cp << 1;
       const bool has_b = ca + 1 < nch;
@@ -1079,20 +992,18 @@ void flock_step_kernel(StepArgs a) {
       uint64_t band = 0;
       // most rows predicted: their candidate test rides on the adjacency loop's d2
       unsigned fca0 = 0, fca1 = 0, fcb0 = 0, fcb1 = 0;
-      int fp = 0, frp = 0;
+      int fp = 0;
       bool fused = false;
-#ifndef GF_PROBE_NO_FUSED
       if constexpr (KN > 0) fused = 2 * __popcll(predm) >= nrows;
-#endif
-      // (GF_KNN_PTAB) the rows' candidate bounds of this tile in the wave's LDS table
+      // the rows' candidate bounds of this tile in the wave's LDS table
       [[maybe_unused]] float tcr_l = -1.f;
-      if constexpr (KN > 0 && GF_KNN_PTAB) {
+      if constexpr (KN > 0) {
         if (predm) {
           tcr_l = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
           if (lane < nrows) ptc[lane] = tcr_l;  // read back by this wave only (in-order LDS)
         }
       }
-      if (fused && GF_KNN_PTAB) {
+      if (fused) {
         // rows in pairs (their LDS reads issued together), as the plain step; rows past
         // nrows sit far away in rxy and are never predicted
         auto frow = [&](int r, float2 pr) {
@@ -1116,7 +1027,7 @@ void flock_step_kernel(StepArgs a) {
             ++fp;
           }
         };
-        if constexpr (GF_P1_LDSROW && GF_P1_PAIR && GF_P1_PAIR_KNN && !CTRL) {
+        if constexpr (!CTRL) {
           const int nr4 = (nrows + 3) & ~3;
           for (int r = 0; r < nr4; r += 2) {
             const float2 p0 = rxy[r], p1 = rxy[r + 1];
@@ -1125,31 +1036,6 @@ void flock_step_kernel(StepArgs a) {
           }
         } else {
           for (int r = 0; r < nrows; ++r) frow(r, row_pos(r));
-        }
-      } else if (fused) {
-        const float ftcr = cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
-        for (int r = 0; r < nrows; ++r) {
-          const float2 pr = row_pos(r);
-          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
-          const uint64_t Aa = __ballot(d2.x < ba.lo), Ab = __ballot(d2.y < ba.lo);
-          const uint64_t Ma = __ballot(!(d2.x >= ba.hi)), Mb = __ballot(!(d2.y >= ba.hi));
-          band |= (Aa ^ Ma) | (Ab ^ Mb);
-          put_lane(wa0, wa1, Aa, r);
-          put_lane(wb0, wb1, Ab, r);
-          if constexpr (CTRL) {
-            const uint64_t Na = __ballot(d2.x <= bn.lo), Nb = __ballot(d2.y <= bn.lo);
-            const uint64_t NMa = __ballot(!(d2.x > bn.hi)), NMb = __ballot(!(d2.y > bn.hi));
-            band |= (Na ^ NMa) | (Nb ^ NMb);
-            put_lane(na0, na1, Na, r);
-            put_lane(nb0, nb1, Nb, r);
-          }
-          if ((predm >> r) & 1) {  // wave-uniform
-            const float tc = readlane_f(ftcr, r);
-            if (lane == fp) frp = r;
-            put_lane(fca0, fca1, __ballot(d2.x < tc), fp);
-            put_lane(fcb0, fcb1, __ballot(d2.y < tc), fp);
-            ++fp;
-          }
         }
       } else {
         auto row1 = [&](int r, float2 pr) {
@@ -1167,7 +1053,7 @@ void flock_step_kernel(StepArgs a) {
             put_lane(nb0, nb1, Nb, r);
           }
         };
-        if constexpr (GF_P1_LDSROW && GF_P1_PAIR && !CTRL && (KN == 0 || GF_P1_PAIR_KNN)) {  // (the controller's budget would spill)
+        if constexpr (!CTRL) {  // (the controller's budget would spill)
           // rows in pairs, their two LDS reads issued together (the compiler will not
           // unroll a loop of ballots by a runtime count); rows past nrows sit far away
           // in rxy: no bits, no band, and their lanes store nothing
@@ -1245,24 +1131,22 @@ void flock_step_kernel(StepArgs a) {
           // row lane's candidate test: float32 d2 < tcr covers every agent with r2 < thr
           // (float32 error of d2 at |d| <= sqrt(thr): 2^-23 |d| (Pi + Pj + |d|) +
           // 2^-22 r2, taken x8); none at huge coordinates (those rows go to the rim kNN)
-          const float tcr = GF_KNN_PTAB ? tcr_l : cand_bound(lane < nrows ? rthr[lane] : 0.f, pu);
           unsigned ca0 = 0, ca1 = 0, cb0 = 0, cb1 = 0;
           int p = 0, rp = 0;
           if (fused) {
             ca0 = fca0; ca1 = fca1; cb0 = fcb0; cb1 = fcb1;
-            p = fp; rp = frp;
+            p = fp;
           } else
           for (uint64_t pm = predm; pm; pm &= pm - 1, ++p) {
             const int r = __builtin_ctzll(pm);
-            if (!GF_KNN_PTAB && lane == p) rp = r;
             const float2 pr = row_pos(r);
-            const float tc = GF_KNN_PTAB ? ptc[r] : readlane_f(tcr, r);
+            const float tc = ptc[r];
             const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
             put_lane(ca0, ca1, __ballot(d2.x < tc), p);
             put_lane(cb0, cb1, __ballot(d2.y < tc), p);
           }
           if (lane < p) {
-            if constexpr (GF_KNN_PTAB) rp = prow[lane];
+            rp = prow[lane];
             const int dl = i0 + rp - (j0 + (ca << 6));
             const uint64_t ka = (static_cast<unsigned>(dl) < 64u) ? ~(1ull << dl) : ~0ull;
             const uint64_t kb = (static_cast<unsigned>(dl - 64) < 64u) ? ~(1ull << (dl - 64)) : ~0ull;
@@ -1381,7 +1265,7 @@ void flock_step_kernel(StepArgs a) {
         // the neighbour's state: its loads are issued here and used after the
         // epilogue, so their latency runs under the epilogue's sums
         if (!GF_ABLATE(a, 32)) {  // diag 32: no observation gather (timing only)
-          if constexpr (!GF_KNN_LATE_GATHER) kraw = load_raw<DYN, UF64>(a, env0 + j);
+          kraw = load_raw<DYN, UF64>(a, env0 + j);
           kj = j;
           kgo = true;
         }
@@ -1391,11 +1275,10 @@ void flock_step_kernel(StepArgs a) {
   }
 
   const St me = frow ? rows[fr] : St{0, 0, 0, 0};
-  step_epilogue<DYN, UF64, CTRL, VAR, kSvAcc>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
+  step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
                                       frow && fs == 0, S, tid);
   if constexpr (KN > 0) {
     if (kgo) {  // Flocking-v0 observation x_i - x_j of this lane's neighbour (flocking.py:24)
-      if constexpr (GF_KNN_LATE_GATHER) kraw = load_raw<DYN, UF64>(a, env0 + kj);
       const St o = state_from_raw<DYN, UF64>(a, kraw);
       if (fs == KN - 1 && a.knn_r2) {  // the row's k-th nearest r2: candidate radius two steps on
         const double dx = me.px - o.px, dy = me.py - o.py;
@@ -1412,9 +1295,7 @@ void flock_step_kernel(StepArgs a) {
     // agent's post-update position (recomputed from x_in and u, bit-identical to the
     // step's), with the rim kernel's ranking and outputs (knn_wave_scan, knn_write_row)
     const uint64_t todo = __ballot(kinl && fs == 0);
-#ifndef GF_PROBE_NO_INLINE_RIM
     if (todo) step_inline_rim<DYN, UF64, KN>(a, env0, todo, i_row, me);
-#endif
   }
   GF_STAMP(10);
 #if defined(GF_STAMPS) && GF_STAMPS >= 2
@@ -1809,7 +1690,7 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
   s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   // inv (R floats); kNN: rthr (R), the waves' candidate-bound tables (4R), prow (R ints)
-  s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? (GF_KNN_PTAB ? 7 : 2) : 1) + 15) / 16) * 16;
+  s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 7 : 1) + 15) / 16) * 16;
   s += 4 * kStoreTab * 16 + (((size_t)R * 8 + 31) & ~size_t(31));  // row table, rows' float32 positions
   return s;
 }
