@@ -554,19 +554,28 @@ def launch(args):
 
 def dry_host(args, world, rank):
     """--dry-host: the multi-rank path's host side with no GPU and no HIP library: the
-    host-channel rendezvous (token checked), the equal-shard check, K timed steps of the
+    host-channel rendezvous (token checked), the shard-size exchange, K timed steps of the
     CPU oracle on this rank's envs between barriers, the reward all-gather over the host
-    channel and every rank's whole-vector check. Rank 0 prints a line shaped like the
-    GPU one (n_gpus, per-rank ms, gathered_rewards_ok)."""
+    channel in the RCCL path's padded block layout (every rank ships the largest shard's
+    width, shard.pad_block; shard.unpad_gathered restores the env order) and every rank's
+    whole-vector check. Rank 0 prints a line shaped like the GPU one (n_gpus, per-rank ms,
+    gathered_rewards_ok)."""
     from gym_flock.hostgroup import HostGroup
     from gym_flock.init_states import synthetic_state
-    from gym_flock.shard import HostRewardGather, check_equal_shards, check_gathered
+    from gym_flock.shard import check_gathered, exchange_shard_sizes, pad_block, unpad_gathered
     from oracle import flocking as orc
     group = HostGroup.from_env(timeout=120.0)
     ranks = Ranks(group)
     N, K = args.n_agents, args.steps
     B = args.n_envs + (1 if args.dry_host_uneven and rank == world - 1 else 0)
-    check_equal_shards(group, B)
+    sizes = exchange_shard_sizes(group, B)
+    W = max(sizes)
+
+    def padded_gather(local):  # the RCCL gathers' block layout, over the host channel
+        blk = pad_block(local, W).reshape(W, -1)
+        parts = [np.frombuffer(p, np.float64).reshape(W, -1) for p in group.allgather_bytes(blk.tobytes())]
+        return unpad_gathered(parts, sizes, axis=0)
+
     xs = [synthetic_state(N, rank * B + b) for b in range(B)]
     us = [np.random.RandomState(10_000 + rank * B + b).uniform(-1, 1, size=(N, 2)).astype(np.float32)
           for b in range(B)]
@@ -586,13 +595,13 @@ def dry_host(args, world, rank):
     el = time.perf_counter() - t0
     group.barrier()
     every = ranks.gather(el)
-    gathered = HostRewardGather(group).gather(rew)
+    gathered = padded_gather(rew).ravel()
     if args.dry_host_corrupt and rank == 1:
         gathered[0] += 1e-9
     _, ok = check_gathered(group, gathered, rew)
     # the get_stats aggregates: per-env [mean vel_diffs, mean min_dists], host channel
     summ = np.array([[st["vel_diffs"].mean(), st["min_dists"].mean()] for st in map(orc.stats, xs)]).reshape(B, 2)
-    gstats = HostRewardGather(group).gather(summ.ravel())
+    gstats = padded_gather(summ)
     _, sok = check_gathered(group, gstats, summ)
     group.close()
     if rank == 0:
@@ -601,7 +610,8 @@ def dry_host(args, world, rank):
                           "ms_per_step": 1e3 * max(every) / K,
                           "per_rank_ms_per_step": [1e3 * e / K for e in every],
                           "gathered_rewards_ok": ok, "gathered_stats_ok": sok, "dry_host": True,
-                          "config": {"n_agents": N, "envs_per_gpu": B, "global_envs": world * B}}), flush=True)
+                          "shard_sizes": sizes,
+                          "config": {"n_agents": N, "envs_per_gpu": B, "global_envs": sum(sizes)}}), flush=True)
     if not (ok and sok):
         raise SystemExit("gathered rewards or stats differ from the ranks' local values")
 
@@ -632,7 +642,7 @@ def main():
     ap.add_argument("--n-agents", type=int, default=1024)
     ap.add_argument("--n-envs", type=int, default=256, help="envs per GPU")
     ap.add_argument("--metrics-every", type=int, default=8,
-                    help="steps per reward all-gather (N>1); each collective carries all those steps")
+                    help="steps per reward all-gather (N>1, at most 64); each collective carries all those steps")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--clock-warmup-ms", type=float, default=300.0,
                     help="untimed wall time of steps before the warmup steps (reported)")
@@ -657,6 +667,8 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-rank path (host channel + RCCL reward all-gather) even at 1 rank")
     args = ap.parse_args()
+    if not 1 <= args.metrics_every <= 64:
+        ap.error("--metrics-every must be in [1, 64] (the reward ring holds 64 steps)")
     if args.cpu_worker is not None:
         return cpu_worker(args.n_agents, args.cpu_worker, args.seed, args.pin_core)
     if args.workload == "coverage":
@@ -680,7 +692,7 @@ def main():
         group = HostGroup.from_env()
     ranks = Ranks(group)
 
-    from gym_flock.shard import check_gathered, init_rccl_gather
+    from gym_flock.shard import check_gathered, init_rccl_gather, rccl_report
     from gym_flock.vec import VecFlockingRelative
 
     N, B, K, W = args.n_agents, args.n_envs, args.steps, args.warmup
@@ -689,8 +701,11 @@ def main():
     x_init = env.reset(seed=0)
     u = np.random.RandomState(1234 + rank).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
     env.set_actions(u)
+    warm = clock_warmup(lambda: env.step(resident=True), env.sync, args.clock_warmup_ms)
+    env.set_state(x_init)
     gather = None
     if multi:
+        # after the clock warmup: the first reward gather ships the steps since init
         # RCCL prints a version banner on the process's stdout at communicator init; the
         # bench's stdout carries only the JSON line, so fd 1 points at stderr meanwhile
         sys.stdout.flush()
@@ -702,14 +717,14 @@ def main():
             os.dup2(saved, 1)
             os.close(saved)
     log("setup %.1fs: N=%d B=%d per GPU, world=%d" % (time.perf_counter() - t_setup, N, B, world))
+    ungathered = [0]  # steps since the last reward all-gather
 
     def plain(s):
         env.step(resident=True)
+        ungathered[0] += 1
         if gather is not None and (s + 1) % args.metrics_every == 0:
-            gather.issue()
-
-    warm = clock_warmup(lambda: env.step(resident=True), env.sync, args.clock_warmup_ms)
-    env.set_state(x_init)
+            gather.issue()  # every step since the previous issue, in one collective
+            ungathered[0] = 0
     for s in range(W):
         plain(s)
     per_rank = []
@@ -717,8 +732,12 @@ def main():
 
     extra = {}
     if gather is not None:
-        gather.issue()  # one all-gather after the timed region
-        allr = gather.result()  # (steps, world*B), the last row is the latest step
+        # RCCL's own view of the ranks, checked on rank 0's line: one communicator of
+        # world ranks, user ranks 0..world-1, a distinct GPU (PCI bus id) per rank
+        extra["rccl"] = rccl_report(group, gather, world)
+        if ungathered[0]:
+            gather.issue()  # the steps after the last in-loop all-gather
+        allr = gather.result()  # (steps, total envs), the last row is the latest step
         _, every = check_gathered(group, allr[-1], env.rewards())
         extra["gathered_rewards_ok"] = every
         extra["gathered_rewards_check"] = ("every rank compared the whole gathered (world x B) vector of the last "

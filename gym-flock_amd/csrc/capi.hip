@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -36,12 +37,11 @@ int fail_hip(const char* what, hipError_t e) {
     if (e_ != hipSuccess) return fail_hip(#expr, e_);       \
   } while (0)
 
-// Reward ring: step t writes slot t % 16. The metrics all-gather ships one block of
-// up to 8 consecutive steps at a time while the steps fill the other block.
-constexpr int kRewardSlots = 16;
-constexpr int kGatherBlock = 8;
-constexpr int kBlocks = kRewardSlots / kGatherBlock;
-// fe_comm_init's bound on the communicator's creation and its shard-size check
+// Reward ring: the t-th reward-writing launch writes slot t % kRewardSlots. The metrics
+// all-gather ships every step written since the previous gather (at most kRewardSlots).
+constexpr int kRewardSlots = 64;
+// fe_comm_init's bound on the communicator's creation, its shard-size exchange and every
+// later wait for a collective
 constexpr double kCommInitTimeoutS = 300.0;
 
 }  // namespace
@@ -81,6 +81,7 @@ struct fe_handle {
   float* net = nullptr;
   double* reward_ring = nullptr;        // kRewardSlots x B
   int rslot = 0;
+  int64_t steps_written = 0;            // reward-writing launches so far (slot = count % slots)
   // kNN outputs, one pair per state buffer: knn_idx[i] / knn_obs[i] belong to x[i], so
   // a fused step (which writes those of its output state) never overlaps the rim kNN of
   // the previous state, and the kread events that guard x[i] guard them too
@@ -108,18 +109,32 @@ struct fe_handle {
   int64_t timing_count = 0;
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
-  // RCCL metrics path
+  // RCCL metrics path. Shards may differ in size: every gathered block is padded to the
+  // largest shard (max_envs), rank r's entries past its n_envs are zero.
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  double* gather = nullptr;             // kBlocks x nranks x kGatherBlock x B
+  int max_envs = 0;
+  std::vector<int32_t> shard_sizes;     // every rank's n_envs (fe_comm_init's exchange)
+  double comm_timeout = kCommInitTimeoutS;  // bound on every wait for a collective
+  double* gsend = nullptr;              // kRewardSlots x max_envs: the gathered steps, padded
+  double* gather = nullptr;             // nranks x kRewardSlots x max_envs
   hipEvent_t step_ev = nullptr;
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
-  hipEvent_t ag_ev[kBlocks] = {};
-  bool ag_pending[kBlocks] = {};
-  int last_gather = -1, last_count = 0;
+  hipEvent_t ag_ev = nullptr;           // completion of the latest reward all-gather
+  // ring slots a reward gather's staging copy still reads: steps [first, ...) until ev
+  struct RingRead {
+    int64_t first;
+    hipEvent_t ev;
+  };
+  std::deque<RingRead> ring_reads;
+  std::vector<hipEvent_t> ev_free;      // recycled RingRead events
+  int64_t gathered_upto = 0;            // steps before this one were shipped (or skipped)
+  bool ag_issued = false;
+  int last_count = 0;
   double* stats_sum = nullptr;          // (B,2) get_stats means per env (fe_stats_summary)
-  double* stats_gather = nullptr;       // nranks x B x 2 (fe_allgather_stats)
+  double* ssend = nullptr;              // (max_envs,2) the stats gather's padded send block
+  double* stats_gather = nullptr;       // nranks x max_envs x 2 (fe_allgather_stats)
   hipEvent_t sg_ev = nullptr;           // completion of the latest stats all-gather
   bool sg_pending = false;
   // flocking variant (fe_set_variant / fe_set_dt)
@@ -267,33 +282,66 @@ int dalloc(T** p, size_t count) {
   return GF_OK;
 }
 
+// Tear down the metrics path: the communicator (aborted when a collective may never
+// complete, else destroyed once the side stream has drained) and everything fe_comm_init
+// made for it, so that a later fe_comm_init starts from scratch.
+void comm_release(fe_handle* h, bool abort) {
+  if (h->comm) {
+    if (abort) {
+      ncclCommAbort(h->comm);  // a collective stuck on a missing peer exits
+    } else {
+      if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
+      ncclCommDestroy(h->comm);
+    }
+    h->comm = nullptr;
+  }
+  if (h->comm_stream) {
+    hipStreamSynchronize(h->comm_stream);
+    hipStreamDestroy(h->comm_stream);
+    h->comm_stream = nullptr;
+  }
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev})
+    if (*e) {
+      hipEventDestroy(*e);
+      *e = nullptr;
+    }
+  for (auto& r : h->ring_reads) hipEventDestroy(r.ev);
+  h->ring_reads.clear();
+  for (hipEvent_t e : h->ev_free) hipEventDestroy(e);
+  h->ev_free.clear();
+  for (double** p : {&h->gsend, &h->gather, &h->ssend, &h->stats_gather})
+    if (*p) {
+      hipFree(*p);
+      *p = nullptr;
+    }
+  h->ag_issued = h->sg_pending = false;
+  h->last_count = 0;
+  h->nranks = 1;
+  h->rank = 0;
+  h->max_envs = 0;
+  h->shard_sizes.clear();
+}
+
 void release(fe_handle* h) {
   if (!h) return;
   hipSetDevice(h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
-  if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
   if (h->kstream) hipStreamSynchronize(h->kstream);
-  if (h->comm) ncclCommDestroy(h->comm);
+  comm_release(h, false);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
-                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->gather, h->stats_sum, h->stats_gather, h->dt_env,
+                  h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->stats_sum, h->dt_env,
                   h->adj_bits[0], h->adj_bits[1], h->pdeg[0], h->pdeg[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
-  if (h->step_ev) hipEventDestroy(h->step_ev);
-  if (h->step_ev2) hipEventDestroy(h->step_ev2);
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
-  if (h->sg_ev) hipEventDestroy(h->sg_ev);
-  for (hipEvent_t e : h->ag_ev)
-    if (e) hipEventDestroy(e);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
                        h->kread[0].ev, h->kread[1].ev})
     if (e) hipEventDestroy(e);
   if (h->kstream) hipStreamDestroy(h->kstream);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
-  if (h->comm_stream) hipStreamDestroy(h->comm_stream);
   delete h;
 }
 
@@ -304,16 +352,20 @@ int check_env(const fe_handle* h, int env) {
 
 double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h->cfg.n_envs; }
 
-// Advance the reward ring before a launch that writes rewards; if an all-gather may
-// still be reading that slot, order the stream behind it (a device-side wait).
+// Advance the reward ring before a launch that writes rewards. The slot last held the
+// step kRewardSlots launches back; if a reward gather's staging copy may still read it,
+// both step streams wait for that copy first (a device-side wait, no host sync).
 int next_reward_slot(fe_handle* h) {
-  h->rslot = (h->rslot + 1) % kRewardSlots;
-  const int blk = h->rslot / kGatherBlock;
-  if (h->rslot % kGatherBlock == 0 && h->ag_pending[blk]) {  // re-entering a gathered block
-    GF_HIP(hipStreamWaitEvent(h->stream, h->ag_ev[blk], 0));
-    if (h->stream2) GF_HIP(hipStreamWaitEvent(h->stream2, h->ag_ev[blk], 0));
-    h->ag_pending[blk] = false;
+  const int64_t s = h->steps_written;
+  h->rslot = static_cast<int>(s % kRewardSlots);
+  while (!h->ring_reads.empty() && h->ring_reads.front().first <= s - kRewardSlots) {
+    const hipEvent_t e = h->ring_reads.front().ev;
+    GF_HIP(hipStreamWaitEvent(h->stream, e, 0));
+    if (h->stream2) GF_HIP(hipStreamWaitEvent(h->stream2, e, 0));
+    h->ring_reads.pop_front();
+    h->ev_free.push_back(e);
   }
+  h->steps_written = s + 1;
   return GF_OK;
 }
 
@@ -1227,72 +1279,107 @@ int fe_comm_unique_id(uint8_t id[128]) {
 
 int fe_check_shard_sizes(int nranks, const int32_t* n_envs) {
   if (nranks < 1 || !n_envs) return fail(GF_EINVAL, "bad argument");
-  for (int r = 1; r < nranks; ++r)
-    if (n_envs[r] != n_envs[0]) {
-      std::string m = "unequal env shards over ranks (the reward all-gather needs one count per rank): n_envs =";
+  for (int r = 0; r < nranks; ++r)
+    if (n_envs[r] < 1) {
+      std::string m = "bad env shard sizes over ranks (every rank holds at least one env): n_envs =";
       for (int q = 0; q < nranks; ++q) m += " " + std::to_string(n_envs[q]);
       return fail(GF_ECOMM, m);
     }
   return GF_OK;
 }
 
+}  // extern "C"
+
 namespace {
+using Clock = std::chrono::steady_clock;
+
+Clock::time_point deadline_in(double seconds) {
+  return Clock::now() + std::chrono::microseconds(static_cast<int64_t>(seconds * 1e6));
+}
+
 // A non-blocking communicator's pending work: poll its async error until it leaves
-// ncclInProgress or the deadline passes (then abort it, so no rank waits forever on a
-// peer that never joined or died).
-int comm_wait(fe_handle* h, std::chrono::steady_clock::time_point deadline, const char* what) {
+// ncclInProgress or the deadline passes; then the metrics path is torn down (the
+// communicator aborted), so no rank waits forever on a peer that never joined or died.
+int comm_wait(fe_handle* h, Clock::time_point deadline, const char* what) {
   for (;;) {
     ncclResult_t st = ncclSuccess;
     ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
     if (r != ncclSuccess) st = r;
     if (st == ncclSuccess) return GF_OK;
-    if (st != ncclInProgress || std::chrono::steady_clock::now() > deadline) {
-      ncclCommAbort(h->comm);
-      h->comm = nullptr;
+    if (st != ncclInProgress || Clock::now() > deadline) {
+      comm_release(h, true);
       if (st != ncclInProgress) return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(st));
       return fail(GF_ECOMM, std::string(what) + ": timed out (a rank did not join or stopped responding)");
     }
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
 }
-}  // namespace
 
-int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[128], double timeout_s) {
-  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks || !(timeout_s > 0)) return fail(GF_EINVAL, "bad argument");
-  if (h->comm) return fail(GF_ESTATE, "communicator already initialised");
-  if (int rc = use_dev(h)) return rc;
-  const auto deadline = std::chrono::steady_clock::now() +
-                        std::chrono::microseconds((int64_t)(timeout_s * 1e6));
-  ncclUniqueId uid;
-  std::memcpy(&uid, id, 128);
-  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
-  config.blocking = 0;
-  ncclResult_t r = ncclCommInitRankConfig(&h->comm, nranks, uid, rank, &config);
-  if (r != ncclSuccess && r != ncclInProgress) {
-    if (h->comm) ncclCommAbort(h->comm);
-    h->comm = nullptr;
-    return fail(GF_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+// Wait for an event recorded on the side stream behind a collective, bounded like
+// comm_wait: the communicator's async error is polled beside the event, and on expiry
+// (a rank that died mid-run never posts its part) the metrics path is torn down.
+int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what) {
+  const auto deadline = deadline_in(h->comm_timeout);
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return GF_OK;
+    if (q != hipErrorNotReady) return fail_hip(what, q);
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
+    if (r != ncclSuccess) st = r;
+    const bool err = st != ncclSuccess && st != ncclInProgress;
+    if (err || Clock::now() > deadline) {
+      comm_release(h, true);
+      if (err) return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(st));
+      return fail(GF_ECOMM, std::string(what) + ": timed out (a rank stopped responding); communicator aborted");
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
-  if (int rc = comm_wait(h, deadline, "ncclCommInitRankConfig")) return rc;
+}
+
+// A collective just enqueued on the non-blocking communicator: wait until it is queued.
+int comm_enqueued(fe_handle* h, ncclResult_t r, const char* what) {
+  if (r == ncclInProgress) return comm_wait(h, deadline_in(h->comm_timeout), what);
+  if (r != ncclSuccess) {
+    comm_release(h, true);
+    return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(r));
+  }
+  return GF_OK;
+}
+
+// A zeroed device buffer of the metrics path (the pad columns of the send blocks are
+// never written afterwards).
+template <class T>
+int comm_alloc(fe_handle* h, T** p, size_t count) {
+  if (int rc = dalloc(p, count)) return rc;
+  if (*p) GF_HIP(hipMemsetAsync(*p, 0, count * sizeof(T), h->comm_stream));
+  return GF_OK;
+}
+
+// fe_comm_init once the communicator exists: the side stream, the shard-size exchange
+// and the gather buffers. On failure the caller tears everything down.
+int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
   GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
-  // every rank's shard size, before any reward all-gather relies on them being equal
+  // every rank's shard size, before any gather pads to the largest
   int32_t* dsz = nullptr;
   if (int rc = dalloc(&dsz, (size_t)nranks)) return rc;
   std::vector<int32_t> sizes(nranks);
   const int32_t mine = h->cfg.n_envs;
-  GF_HIP(hipMemcpyAsync(dsz + rank, &mine, 4, hipMemcpyHostToDevice, h->comm_stream));
-  r = ncclAllGather(dsz + rank, dsz, 1, ncclInt32, h->comm, h->comm_stream);
-  int rc = (r == ncclSuccess || r == ncclInProgress) ? comm_wait(h, deadline, "shard-size all-gather")
-                                                     : fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  int rc = GF_OK;
+  const hipError_t e = hipMemcpyAsync(dsz + rank, &mine, 4, hipMemcpyHostToDevice, h->comm_stream);
+  if (e != hipSuccess) rc = fail_hip("shard-size upload", e);
+  if (rc == GF_OK) {
+    const ncclResult_t r = ncclAllGather(dsz + rank, dsz, 1, ncclInt32, h->comm, h->comm_stream);
+    rc = (r == ncclSuccess || r == ncclInProgress) ? comm_wait(h, deadline, "shard-size all-gather")
+                                                   : fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  }
   if (rc == GF_OK) {
     hipError_t q;
     while ((q = hipStreamQuery(h->comm_stream)) == hipErrorNotReady) {
-      if (std::chrono::steady_clock::now() > deadline) break;
+      if (Clock::now() > deadline) break;
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
     if (q == hipErrorNotReady) {
-      ncclCommAbort(h->comm);
-      h->comm = nullptr;
       rc = fail(GF_ECOMM, "shard-size all-gather: timed out (a rank stopped responding)");
     } else if (q != hipSuccess) {
       rc = fail(GF_EHIP, std::string("shard-size all-gather: ") + hipGetErrorString(q));
@@ -1303,19 +1390,49 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
     }
   }
   hipFree(dsz);
-  if (rc != GF_OK) {
-    if (h->comm) ncclCommDestroy(h->comm);
-    h->comm = nullptr;
-    return rc;
-  }
-  h->nranks = nranks;
-  h->rank = rank;
+  if (rc != GF_OK) return rc;
+  h->shard_sizes = sizes;
+  h->max_envs = *std::max_element(sizes.begin(), sizes.end());
+  const size_t W = h->max_envs;
   GF_HIP(hipEventCreateWithFlags(&h->step_ev, hipEventDisableTiming));
   GF_HIP(hipEventCreateWithFlags(&h->step_ev2, hipEventDisableTiming));
-  for (auto& e : h->ag_ev) GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (int rc2 = dalloc(&h->gather, (size_t)kBlocks * nranks * kGatherBlock * h->cfg.n_envs)) return rc2;
+  GF_HIP(hipEventCreateWithFlags(&h->ag_ev, hipEventDisableTiming));
   GF_HIP(hipEventCreateWithFlags(&h->sg_ev, hipEventDisableTiming));
-  if (int rc2 = dalloc(&h->stats_gather, (size_t)nranks * h->cfg.n_envs * 2)) return rc2;
+  if ((rc = comm_alloc(h, &h->gsend, (size_t)kRewardSlots * W)) ||
+      (rc = comm_alloc(h, &h->gather, (size_t)nranks * kRewardSlots * W)) || (rc = comm_alloc(h, &h->ssend, W * 2)) ||
+      (rc = comm_alloc(h, &h->stats_gather, (size_t)nranks * W * 2)))
+    return rc;
+  GF_HIP(hipStreamSynchronize(h->comm_stream));
+  h->nranks = nranks;
+  h->rank = rank;
+  h->gathered_upto = h->steps_written;  // the first gather ships the steps after init
+  return GF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[128], double timeout_s) {
+  if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks || !(timeout_s > 0)) return fail(GF_EINVAL, "bad argument");
+  if (h->comm) return fail(GF_ESTATE, "communicator already initialised");
+  if (int rc = use_dev(h)) return rc;
+  const auto deadline = deadline_in(timeout_s);
+  h->comm_timeout = timeout_s;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+  config.blocking = 0;
+  const ncclResult_t r = ncclCommInitRankConfig(&h->comm, nranks, uid, rank, &config);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    comm_release(h, true);
+    return fail(GF_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  }
+  if (int rc = comm_wait(h, deadline, "ncclCommInitRankConfig")) return rc;
+  if (int rc = comm_setup(h, nranks, rank, deadline)) {
+    const std::string msg = g_err;
+    comm_release(h, true);  // abort: a peer may still be inside the shard-size collective
+    return fail(rc, msg);
+  }
   return GF_OK;
 }
 
@@ -1323,48 +1440,89 @@ int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
   return fe_comm_init_timeout(h, nranks, rank, id, kCommInitTimeoutS);
 }
 
+int fe_comm_info(fe_handle* h, int32_t* count, int32_t* user_rank, int32_t* device, char* bus_id, int bus_id_len) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  int c = 0, ur = 0, d = 0;
+  ncclResult_t r = ncclCommCount(h->comm, &c);
+  if (r == ncclSuccess) r = ncclCommUserRank(h->comm, &ur);
+  if (r == ncclSuccess) r = ncclCommCuDevice(h->comm, &d);
+  if (r != ncclSuccess) return fail(GF_ECOMM, std::string("ncclComm query: ") + ncclGetErrorString(r));
+  if (count) *count = c;
+  if (user_rank) *user_rank = ur;
+  if (device) *device = d;
+  if (bus_id && bus_id_len > 0) GF_HIP(hipDeviceGetPCIBusId(bus_id, bus_id_len, d));
+  return GF_OK;
+}
+
+int fe_comm_shard_sizes(fe_handle* h, int32_t* sizes, int32_t* max_envs) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (sizes) std::copy(h->shard_sizes.begin(), h->shard_sizes.end(), sizes);
+  if (max_envs) *max_envs = h->max_envs;
+  return GF_OK;
+}
+
 int fe_allgather_rewards(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm) return fail(GF_ESTATE, "fe_comm_init not called");
+  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
   // a step-path call: the gather's stream waits for both step streams' latest work
   // (events only), so back-to-back split steps around it stay split and out of phase
-  // (use_dev's join would make the next step a single launch: every 8th step of the
-  // multi-rank bench)
+  // (use_dev's join would make the next step a single launch)
   if (int rc = use_dev_step(h)) return rc;
-  const size_t B = h->cfg.n_envs;
-  const int blk = h->rslot / kGatherBlock;
-  const int count = h->rslot % kGatherBlock + 1;  // steps of this block written so far
-  const double* src = h->reward_ring + (size_t)blk * kGatherBlock * B;
-  double* dst = h->gather + (size_t)blk * h->nranks * kGatherBlock * B;
+  const int64_t first = h->gathered_upto, count = h->steps_written - first;
+  if (count <= 0) return fail(GF_ESTATE, "no step since the last reward all-gather");
+  if (count > kRewardSlots) {
+    // the ranks step in lockstep, so every rank takes this branch at the same call and
+    // none is left inside a collective
+    h->gathered_upto = h->steps_written;
+    return fail(GF_ESTATE, "the rewards of " + std::to_string(count - kRewardSlots) +
+                               " step(s) were overwritten before a gather (gather at least every " +
+                               std::to_string(kRewardSlots) + " steps)");
+  }
+  const size_t B = h->cfg.n_envs, W = h->max_envs;
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
   GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
   if (h->stream2) {
     GF_HIP(hipEventRecord(h->step_ev2, h->stream2));
     GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev2, 0));
   }
-  ncclResult_t r = ncclAllGather(src, dst, (size_t)count * B, ncclFloat64, h->comm, h->comm_stream);
-  if (r == ncclInProgress) {  // the communicator is non-blocking: wait until it is enqueued
-    if (int rc = comm_wait(h, std::chrono::steady_clock::now() + std::chrono::seconds((int)kCommInitTimeoutS),
-                           "ncclAllGather"))
-      return rc;
-  } else if (r != ncclSuccess) {
-    return fail(GF_ECOMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  // the steps' ring slots (two runs when they wrap) into the padded send block
+  const int s0 = static_cast<int>(first % kRewardSlots);
+  const int n1 = static_cast<int>(std::min<int64_t>(count, kRewardSlots - s0));
+  GF_HIP(hipMemcpy2DAsync(h->gsend, W * 8, h->reward_ring + (size_t)s0 * B, B * 8, B * 8, n1,
+                          hipMemcpyDeviceToDevice, h->comm_stream));
+  if (n1 < count)
+    GF_HIP(hipMemcpy2DAsync(h->gsend + (size_t)n1 * W, W * 8, h->reward_ring, B * 8, B * 8, count - n1,
+                            hipMemcpyDeviceToDevice, h->comm_stream));
+  hipEvent_t rd = nullptr;  // the copy's completion: the slots are free again
+  if (!h->ev_free.empty()) {
+    rd = h->ev_free.back();
+    h->ev_free.pop_back();
+  } else {
+    GF_HIP(hipEventCreateWithFlags(&rd, hipEventDisableTiming));
   }
-  GF_HIP(hipEventRecord(h->ag_ev[blk], h->comm_stream));
-  h->ag_pending[blk] = true;
-  h->last_gather = blk;
-  h->last_count = count;
+  h->ring_reads.push_back({first, rd});
+  GF_HIP(hipEventRecord(rd, h->comm_stream));
+  if (int rc = comm_enqueued(h, ncclAllGather(h->gsend, h->gather, (size_t)count * W, ncclFloat64, h->comm,
+                                              h->comm_stream),
+                             "ncclAllGather (rewards)"))
+    return rc;
+  GF_HIP(hipEventRecord(h->ag_ev, h->comm_stream));
+  h->ag_issued = true;
+  h->last_count = static_cast<int>(count);
+  h->gathered_upto = h->steps_written;
   return GF_OK;
 }
 
 int fe_get_gathered_rewards(fe_handle* h, double* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
-  if (h->last_gather < 0) return fail(GF_ESTATE, "no all-gather issued");
+  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->ag_issued) return fail(GF_ESTATE, "no all-gather issued");
   if (int rc = use_dev(h)) return rc;
-  const size_t n = (size_t)h->nranks * h->last_count * h->cfg.n_envs;
-  GF_HIP(hipEventSynchronize(h->ag_ev[h->last_gather]));
-  GF_HIP(hipMemcpy(dst, h->gather + (size_t)h->last_gather * h->nranks * kGatherBlock * h->cfg.n_envs, n * 8,
-                   hipMemcpyDeviceToHost));
+  if (int rc = comm_event_wait(h, h->ag_ev, "reward all-gather")) return rc;
+  const size_t n = (size_t)h->nranks * h->last_count * h->max_envs;
+  GF_HIP(hipMemcpy(dst, h->gather, n * 8, hipMemcpyDeviceToHost));
   return GF_OK;
 }
 
@@ -1372,7 +1530,7 @@ int fe_gathered_steps(fe_handle* h) { return h ? h->last_count : 0; }
 
 int fe_allgather_stats(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm) return fail(GF_ESTATE, "fe_comm_init not called");
+  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
   if (!h->has_state) return fail(GF_ESTATE, "state not set");
   // the summaries are taken on the whole current state (both step halves joined); the
   // collective then runs on the side stream, like the reward all-gather
@@ -1380,15 +1538,13 @@ int fe_allgather_stats(fe_handle* h) {
   if (int rc = stats_summary_dev(h)) return rc;
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
   GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
-  const size_t n = (size_t)h->cfg.n_envs * 2;
-  ncclResult_t r = ncclAllGather(h->stats_sum, h->stats_gather, n, ncclFloat64, h->comm, h->comm_stream);
-  if (r == ncclInProgress) {
-    if (int rc = comm_wait(h, std::chrono::steady_clock::now() + std::chrono::seconds((int)kCommInitTimeoutS),
-                           "ncclAllGather (stats)"))
-      return rc;
-  } else if (r != ncclSuccess) {
-    return fail(GF_ECOMM, std::string("ncclAllGather (stats): ") + ncclGetErrorString(r));
-  }
+  // into the padded send block, on the side stream (after the previous stats gather)
+  GF_HIP(hipMemcpyAsync(h->ssend, h->stats_sum, (size_t)h->cfg.n_envs * 2 * sizeof(double), hipMemcpyDeviceToDevice,
+                        h->comm_stream));
+  if (int rc = comm_enqueued(h, ncclAllGather(h->ssend, h->stats_gather, (size_t)h->max_envs * 2, ncclFloat64,
+                                              h->comm, h->comm_stream),
+                             "ncclAllGather (stats)"))
+    return rc;
   GF_HIP(hipEventRecord(h->sg_ev, h->comm_stream));
   h->sg_pending = true;
   return GF_OK;
@@ -1396,21 +1552,18 @@ int fe_allgather_stats(fe_handle* h) {
 
 int fe_get_gathered_stats(fe_handle* h, double* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
+  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
   if (!h->sg_pending) return fail(GF_ESTATE, "no stats all-gather issued");
   if (int rc = use_dev(h)) return rc;
-  GF_HIP(hipEventSynchronize(h->sg_ev));
-  GF_HIP(hipMemcpy(dst, h->stats_gather, (size_t)h->nranks * h->cfg.n_envs * 2 * sizeof(double),
-                   hipMemcpyDeviceToHost));
+  if (int rc = comm_event_wait(h, h->sg_ev, "stats all-gather")) return rc;
+  GF_HIP(hipMemcpy(dst, h->stats_gather, (size_t)h->nranks * h->max_envs * 2 * sizeof(double), hipMemcpyDeviceToHost));
   return GF_OK;
 }
 
 int fe_comm_destroy(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (h->comm) {
-    if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
-    ncclCommDestroy(h->comm);
-    h->comm = nullptr;
-  }
+  if (int rc = use_dev(h)) return rc;
+  comm_release(h, false);
   return GF_OK;
 }
 

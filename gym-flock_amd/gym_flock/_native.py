@@ -108,6 +108,8 @@ SIGNATURES = {
     "fe_comm_init": [_P, _I, _I, _P],
     "fe_comm_init_timeout": [_P, _I, _I, _P, ctypes.c_double],
     "fe_check_shard_sizes": [_I, _P],
+    "fe_comm_info": [_P, _P, _P, _P, ctypes.c_char_p, _I],
+    "fe_comm_shard_sizes": [_P, _P, _P],
     "fe_allgather_rewards": [_P],
     "fe_get_gathered_rewards": [_P, _P],
     "fe_gathered_steps": [_P],
@@ -198,11 +200,26 @@ class HostPool:
     cap (a caller keeping many steps' outputs), arrays are ordinary numpy memory."""
 
     def __init__(self, cap_bytes=256 << 20):
+        import collections
         import threading
         self.cap = int(cap_bytes)
         self.live = 0
         self.free = {}
         self.lock = threading.Lock()
+        # released buffers, queued without a lock: _release runs from weakref finalizers,
+        # which the cyclic GC may fire inside any allocation, including one made while
+        # self.lock is held by this very thread (deque.append is atomic)
+        self.released = collections.deque()
+
+    def _drain(self):
+        # caller holds self.lock
+        while True:
+            try:
+                p, nbytes = self.released.popleft()
+            except IndexError:
+                return
+            self.live -= nbytes
+            self.free.setdefault(nbytes, []).append(p)
 
     def array(self, shape, dtype):
         import weakref
@@ -211,6 +228,7 @@ class HostPool:
         if nbytes == 0:
             return np.empty(shape, dtype)
         with self.lock:
+            self._drain()
             lst = self.free.get(nbytes)
             p = lst.pop() if lst else None
             if p is None and self.live + nbytes > self.cap:
@@ -231,13 +249,12 @@ class HostPool:
         return np.frombuffer(buf, dtype=dtype).reshape(shape)
 
     def _release(self, p, nbytes):
-        with self.lock:
-            self.live -= nbytes
-            self.free.setdefault(nbytes, []).append(p)
+        self.released.append((p, nbytes))  # no lock, no allocation beyond the tuple
 
     def trim(self):
         """Free the recycled (unused) buffers."""
         with self.lock:
+            self._drain()
             ps = [p for lst in self.free.values() for p in lst]
             self.free = {}
         for p in ps:
@@ -284,8 +301,10 @@ class FlockHandle:
         self.h = h
 
     def close(self):
-        if getattr(self, "h", None):
-            self.lib.fe_destroy(self.h)
+        h = getattr(self, "h", None)
+        if h:
+            self.lib.fe_destroy(h)
+            h.value = None  # any copy of the handle object now passes NULL (GF_EINVAL)
             self.h = None
 
     __del__ = close
@@ -493,20 +512,41 @@ class FlockHandle:
         return bytes(buf)
 
     def comm_init(self, nranks, rank, uid, timeout=300.0):
-        """RCCL communicator for the reward all-gather: bounded by `timeout` seconds, and
-        rejected (GF_ECOMM) unless every rank holds the same number of envs."""
+        """RCCL communicator for the metrics all-gathers, bounded by `timeout` seconds
+        (also the bound of every later wait for a collective). Shards may differ in size."""
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self.lib.fe_comm_init_timeout(self.h, int(nranks), int(rank), ctypes.cast(buf, ctypes.c_void_p),
                                             float(timeout)))
         self.nranks = int(nranks)
+        self.shard_sizes, self.max_envs = self.comm_shard_sizes()
+
+    def comm_shard_sizes(self):
+        """(every rank's n_envs as a list, the largest: the gathers' padded width)."""
+        sizes = np.empty(self.nranks, np.int32)
+        mx = ctypes.c_int32()
+        check(self.lib.fe_comm_shard_sizes(self.h, ptr(sizes), ctypes.byref(mx)))
+        return [int(v) for v in sizes], int(mx.value)
+
+    def comm_info(self):
+        """The communicator as RCCL reports it: {count, user_rank, device, pci_bus_id}."""
+        c, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        bus = ctypes.create_string_buffer(64)
+        check(self.lib.fe_comm_info(self.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(d), bus, 64))
+        return {"count": c.value, "user_rank": r.value, "device": d.value,
+                "pci_bus_id": bus.value.decode(errors="replace")}
+
+    def comm_destroy(self):
+        check(self.lib.fe_comm_destroy(self.h))
 
     def allgather_rewards(self):
+        """Enqueue the all-gather of every step's rewards since the previous one."""
         check(self.lib.fe_allgather_rewards(self.h))
 
     def gathered_rewards(self):
-        """(nranks, steps, B) rewards of the steps covered by the latest all-gather."""
+        """(nranks, steps, max_envs) rewards of the steps covered by the latest all-gather
+        (rank r's columns past its n_envs are zero padding)."""
         steps = self.lib.fe_gathered_steps(self.h)
-        out = np.empty((self.nranks, max(steps, 1), self.n_envs))
+        out = np.empty((self.nranks, max(steps, 1), self.max_envs))
         check(self.lib.fe_get_gathered_rewards(self.h, ptr(out)))
         return out[:, :steps]
 
@@ -515,8 +555,8 @@ class FlockHandle:
         check(self.lib.fe_allgather_stats(self.h))
 
     def gathered_stats(self):
-        """(nranks, B, 2) summaries of the latest stats all-gather, rank-major."""
-        out = np.empty((self.nranks, self.n_envs, 2))
+        """(nranks, max_envs, 2) summaries of the latest stats all-gather, rank-major."""
+        out = np.empty((self.nranks, self.max_envs, 2))
         check(self.lib.fe_get_gathered_stats(self.h, ptr(out)))
         return out
 
@@ -540,8 +580,12 @@ class CoverageHandle:
         self._step_resident = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_RESIDENT)
 
     def close(self):
-        if getattr(self, "h", None):
-            self.lib.cov_destroy(self.h)
+        h = getattr(self, "h", None)
+        if h:
+            self.lib.cov_destroy(h)
+            # the bound resident-step partial holds this same object: it now passes NULL
+            # (GF_EINVAL) instead of the freed handle
+            h.value = None
             self.h = None
 
     __del__ = close

@@ -17,7 +17,9 @@ GYMFLOCK_HOST_PORT), bench.py's own launcher, or explicit arguments.
 Messages are raw bytes or fixed-format struct values (float64, int64, bool); nothing
 received is ever unpickled or evaluated. A shared token (GYMFLOCK_HOST_TOKEN, set by
 bench.py's launcher) must accompany every rank's hello, so a stray local process that
-reaches rank 0's port during the rendezvous is refused.
+reaches rank 0's port during the rendezvous is refused: its connection is dropped (as is
+one that sends nothing within HELLO_TIMEOUT, a bad rank or a duplicate) and the
+rendezvous goes on until every rank has joined or the timeout passes.
 """
 import hmac
 import os
@@ -60,6 +62,7 @@ class HostGroup:
             raise ValueError("rank out of range")
         self.peers = {}  # rank 0: rank -> socket
         self.up = None   # other ranks: socket to rank 0
+        self.refused = []  # rank 0: addresses of connections dropped in the rendezvous
         if self.world == 1:
             return
         deadline = time.monotonic() + timeout
@@ -67,24 +70,33 @@ class HostGroup:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((addr, int(port)))
-            srv.listen(self.world)
-            srv.settimeout(max(1.0, deadline - time.monotonic()))
+            srv.listen(self.world + 4)
+            ok = False
             try:
                 while len(self.peers) < self.world - 1:
-                    c, _ = srv.accept()
+                    left = deadline - time.monotonic()
+                    if left <= 0:
+                        raise TimeoutError("hostgroup: %d of %d ranks joined before the rendezvous timeout"
+                                           % (len(self.peers) + 1, self.world))
+                    srv.settimeout(left)
+                    try:
+                        c, who = srv.accept()
+                    except socket.timeout:
+                        continue
+                    r = self._hello(c, token, min(self.HELLO_TIMEOUT, max(0.1, deadline - time.monotonic())))
+                    if r is None:
+                        # a stray or broken client: dropped, the rendezvous goes on
+                        c.close()
+                        self.refused.append(who)
+                        continue
                     c.settimeout(timeout)
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    hello = _recv_exact(c, 4 + _TOKEN_LEN)
-                    (r,) = struct.unpack("!I", hello[:4])
-                    if not hmac.compare_digest(hello[4:], token):
-                        c.close()
-                        raise RuntimeError("hostgroup: a peer presented the wrong token in the rendezvous")
-                    if not (0 < r < self.world) or r in self.peers:
-                        c.close()
-                        raise RuntimeError("hostgroup: unexpected rank %d in rendezvous" % r)
                     self.peers[r] = c
+                ok = True
             finally:
                 srv.close()
+                if not ok:
+                    self.close()
         else:
             while True:
                 try:
@@ -98,6 +110,23 @@ class HostGroup:
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             s.sendall(struct.pack("!I", self.rank) + token)
             self.up = s
+
+    HELLO_TIMEOUT = 5.0  # seconds a connecting peer has to present its rank and token
+
+    def _hello(self, c, token, limit):
+        """The rank a new connection announces, or None (short read, timeout, wrong token,
+        bad or duplicate rank): the caller drops such a connection."""
+        try:
+            c.settimeout(limit)
+            hello = _recv_exact(c, 4 + _TOKEN_LEN)
+        except (OSError, ConnectionError):
+            return None
+        (r,) = struct.unpack("!I", hello[:4])
+        if not hmac.compare_digest(hello[4:], token):
+            return None
+        if not (0 < r < self.world) or r in self.peers:
+            return None
+        return r
 
     @classmethod
     def from_env(cls, timeout=300.0):

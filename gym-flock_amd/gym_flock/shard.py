@@ -8,7 +8,9 @@ get_stats summaries (means of vel_diffs and min_dists) likewise.
 
 Transports for that all-gather:
   - RcclRewardGather: RCCL over xGMI, issued by libgymflock on a side stream right
-    after the step kernel (fe_allgather_rewards) — the GPU path.
+    after the step kernel (fe_allgather_rewards) — the GPU path. Each rank's block is
+    padded to the largest shard (pad_block's layout); unpad_gathered restores the global
+    env order, so shard_range's uneven splits work unchanged.
   - HostRewardGather: the torch-free host channel (hostgroup.HostGroup) on host
     copies — the CPU tests and CPU-only callers.
   - GlooRewardGather: torch.distributed (gloo) on host copies — for callers that
@@ -31,23 +33,44 @@ def shard_range(total_envs, world_size, rank):
     return start, start + q + (1 if rank < r else 0)
 
 
-class RcclRewardGather:
-    """All-gather of per-env rewards with RCCL (equal shard sizes on every rank).
+def pad_block(local, width, axis=0):
+    """A rank's per-env array padded with zeros to `width` envs along `axis`: the block
+    layout of the RCCL gathers (include/gymflock.h: every rank ships max_envs columns,
+    those past its own n_envs zero)."""
+    local = np.asarray(local, dtype=np.float64)
+    pad = [(0, 0)] * local.ndim
+    pad[axis] = (0, int(width) - local.shape[axis])
+    return np.pad(local, pad)
 
-    issue() after a step enqueues one collective for the steps since the start of the
-    current 8-step block (call it every 8 steps to ship each step's rewards once);
-    result() returns them as (steps, world * B) in global env order."""
+
+def unpad_gathered(blocks, sizes, axis=0):
+    """Rank-major gathered blocks, each padded to the largest shard, -> global env order:
+    rank r's first sizes[r] entries along `axis` (the env axis of one rank's block),
+    concatenated in rank order."""
+    blocks = np.asarray(blocks)
+    if len(blocks) != len(sizes):
+        raise ValueError("%d gathered blocks for %d ranks" % (len(blocks), len(sizes)))
+    return np.concatenate([np.take(b, np.arange(n), axis=axis) for b, n in zip(blocks, sizes)], axis=axis)
+
+
+class RcclRewardGather:
+    """All-gather of per-env rewards with RCCL; shards may differ in size (the library
+    pads every rank's block to the largest shard, result() drops the padding).
+
+    issue() after a step enqueues one collective carrying every step since the previous
+    issue() (at any interval up to 64 steps); result() returns them as (steps, total_envs)
+    in global env order."""
 
     def __init__(self, handle, world_size, rank, unique_id, timeout=300.0):
         self.handle = handle
         handle.comm_init(world_size, rank, unique_id, timeout)
+        self.sizes = handle.shard_sizes
 
     def issue(self):
         self.handle.allgather_rewards()
 
     def result(self):
-        g = self.handle.gathered_rewards()  # (world, steps, B)
-        return np.concatenate(list(g), axis=1)
+        return unpad_gathered(self.handle.gathered_rewards(), self.sizes, axis=1)  # (world, steps, W)
 
     def issue_stats(self):
         """The optional get_stats aggregates: every rank's per-env means of
@@ -55,32 +78,36 @@ class RcclRewardGather:
         self.handle.allgather_stats()
 
     def stats_result(self):
-        """(world * B, 2) per-env [mean vel_diffs, mean min_dists] in global env order."""
-        return self.handle.gathered_stats().reshape(-1, 2)
+        """(total_envs, 2) per-env [mean vel_diffs, mean min_dists] in global env order."""
+        return unpad_gathered(self.handle.gathered_stats(), self.sizes, axis=0)  # (world, W, 2)
+
+    def comm_info(self):
+        """The communicator as RCCL reports it on this rank (fe_comm_info)."""
+        return self.handle.comm_info()
 
 
-def check_equal_shards(group, n_envs):
-    """Every rank's env count over the host channel; raises on every rank unless they are
-    equal (the RCCL reward all-gather ships one count per rank; fe_comm_init checks the
-    same on the device). Returns the per-rank counts."""
+def exchange_shard_sizes(group, n_envs):
+    """Every rank's env count over the host channel (in rank order, on every rank)."""
     sizes = group.allgather_i64(int(n_envs))
-    if len(set(sizes)) != 1:
-        raise RuntimeError("unequal env shards over ranks: n_envs per rank = %s (the reward all-gather "
-                           "needs the same count on every rank)" % sizes)
+    if min(sizes) < 1:
+        raise RuntimeError("bad env shard sizes over ranks: n_envs per rank = %s" % sizes)
     return sizes
 
 
 def init_rccl_gather(group, handle, world, rank, timeout=300.0):
     """The multi-rank path's RCCL setup, bounded by the host channel: the ranks' shard
-    sizes are compared first; rank 0's unique id goes out only once every rank has joined
+    sizes are exchanged first; rank 0's unique id goes out only once every rank has joined
     the channel (HostGroup's rendezvous); each rank's bounded communicator init
     (fe_comm_init_timeout) reports success over the channel, and every rank raises if any
     rank failed, instead of leaving the others in RCCL. Returns an RcclRewardGather."""
-    check_equal_shards(group, handle.n_envs)
+    sizes = exchange_shard_sizes(group, handle.n_envs)
     uid = group.broadcast_bytes(handle.comm_unique_id() if rank == 0 else b"")
     err = None
     try:
         gather = RcclRewardGather(handle, world, rank, uid, timeout)
+        if gather.sizes != sizes:
+            raise RuntimeError("RCCL's shard-size exchange %s differs from the host channel's %s"
+                               % (gather.sizes, sizes))
     except Exception as e:  # reported to every rank below, then re-raised here
         err, gather = e, None
     ok = group.allgather_bool(err is None)
@@ -89,6 +116,28 @@ def init_rccl_gather(group, handle, world, rank, timeout=300.0):
     if not all(ok):
         raise RuntimeError("RCCL communicator init failed on rank(s) %s" % [r for r, v in enumerate(ok) if not v])
     return gather
+
+
+def rccl_report(group, gather, world):
+    """Every rank's communicator as RCCL reports it, collected on every rank, with the
+    checks rank 0 makes before it reports a multi-rank figure: ncclCommCount equals the
+    number of ranks everywhere, the user ranks are 0..world-1 in order, and no two ranks
+    share a device PCI bus id (one process per GPU). Raises if any check fails."""
+    import json
+    mine = json.dumps(gather.comm_info(), sort_keys=True).encode()
+    infos = [json.loads(p.decode()) for p in group.allgather_bytes(mine)]
+    problems = []
+    if any(i["count"] != world for i in infos):
+        problems.append("ncclCommCount %s != %d ranks" % ([i["count"] for i in infos], world))
+    if [i["user_rank"] for i in infos] != list(range(world)):
+        problems.append("user ranks %s" % [i["user_rank"] for i in infos])
+    buses = [i["pci_bus_id"] for i in infos]
+    if len(set(buses)) != len(buses):
+        problems.append("ranks share a GPU: PCI bus ids %s" % buses)
+    if problems:
+        raise RuntimeError("RCCL communicator check failed: " + "; ".join(problems))
+    return {"ranks": infos, "count": world, "distinct_devices": len(set(buses)),
+            "shard_sizes": list(gather.sizes)}
 
 
 class HostRewardGather:

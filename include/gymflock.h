@@ -184,35 +184,47 @@ int fe_set_dt(fe_handle* h, const double* dt);
 
 /* Multi-GPU metrics path (RCCL over xGMI) ---------------------- */
 /* The env batch is sharded contiguously over ranks (one process per GPU); the
- * step path has no exchange. Only per-env rewards are all-gathered, on a side
- * stream, so the collective never sits on the step critical path. */
+ * step path has no exchange. Only per-env rewards (and, optionally, get_stats
+ * summaries) are all-gathered, on a side stream, so the collective never sits on the
+ * step critical path. Shards may differ in size (shard.py's shard_range gives the first
+ * B % world ranks one env more): every gathered block is padded to the largest shard,
+ * max_envs, and rank r's entries past its own n_envs are zero. Every wait for a
+ * collective is bounded by the init timeout: a rank that never joins or stops
+ * responding makes the others' calls return GF_ECOMM (the communicator is then aborted
+ * and the handle keeps stepping) instead of hanging. All ranks make the same sequence
+ * of metrics calls after the same number of steps. */
 int fe_comm_unique_id(uint8_t id[128]);
-/* Creates the communicator (non-blocking RCCL init, polled), then all-gathers every
- * rank's n_envs and fails with GF_ECOMM unless they are equal (the reward all-gather
- * ships one count per rank). A rank that never joins, or stops responding, makes every
- * other rank's call return GF_ECOMM after the timeout (fe_comm_init: 300 s) instead of
- * hanging; the communicator is then aborted. */
+/* Creates the communicator (non-blocking RCCL init, polled) and all-gathers every
+ * rank's n_envs (fe_comm_shard_sizes). Bounded by timeout_s (fe_comm_init: 300 s). */
 int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]);
 int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[128], double timeout_s);
-/* The shard-size rule fe_comm_init applies to the gathered sizes: GF_OK when every
- * n_envs[r] (r < nranks) is equal, else GF_ECOMM naming them. Host-only (no device). */
+/* The rule fe_comm_init applies to the exchanged sizes: GF_OK when every n_envs[r]
+ * (r < nranks) is >= 1, else GF_ECOMM naming them. Host-only (no device). */
 int fe_check_shard_sizes(int nranks, const int32_t* n_envs);
+/* The communicator as RCCL sees it: ncclCommCount, ncclCommUserRank, the HIP device
+ * ordinal it runs on (ncclCommCuDevice) and that device's PCI bus id (bus_id_len bytes,
+ * hipDeviceGetPCIBusId). Any output pointer may be NULL. */
+int fe_comm_info(fe_handle* h, int32_t* count, int32_t* user_rank, int32_t* device, char* bus_id, int bus_id_len);
+/* Every rank's n_envs (sizes[nranks]) and the largest, the gathers' padded width. */
+int fe_comm_shard_sizes(fe_handle* h, int32_t* sizes, int32_t* max_envs);
 /* Enqueue (side stream, after the latest step) an all-gather of the per-env rewards of
- * the steps since the start of the current 8-step block: one collective per 8 steps
- * carries every step's rewards. */
+ * every step since the previous reward all-gather (or since fe_comm_init), each step
+ * exactly once, at any interval up to 64 steps. GF_ESTATE if no step was taken since,
+ * or if more than 64 were (the oldest were overwritten: the call then skips them all). */
 int fe_allgather_rewards(fe_handle* h);
-/* Wait for the latest all-gather; dst gets (nranks, steps, B) rewards, rank-major,
- * steps = fe_gathered_steps(h) (oldest first). */
+/* Wait (bounded) for the latest reward all-gather; dst gets (nranks, steps, max_envs)
+ * rewards, rank-major, steps = fe_gathered_steps(h) (oldest first). */
 int fe_get_gathered_rewards(fe_handle* h, double* dst);
 int fe_gathered_steps(fe_handle* h);
 /* Enqueue (side stream) an all-gather of every rank's fe_stats_summary of the current
  * state: the optional get_stats aggregates of SURVEY.md §8e. The summaries are taken
  * on the handle's stream after both step halves (a join, so the next step is one launch,
  * unlike the reward all-gather); call it per episode or logging interval, not per step.
- * fe_get_gathered_stats waits for it; dst gets (nranks, B, 2), rank-major (global env
- * order). */
+ * fe_get_gathered_stats waits (bounded) for it; dst gets (nranks, max_envs, 2),
+ * rank-major. */
 int fe_allgather_stats(fe_handle* h);
 int fe_get_gathered_stats(fe_handle* h, double* dst);
+/* Destroys the communicator and the metrics path's buffers; fe_comm_init may follow. */
 int fe_comm_destroy(fe_handle* h);
 
 /* ============================ Coverage-v0 ==================================== */

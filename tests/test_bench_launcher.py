@@ -1,9 +1,10 @@
 """bench.py's own multi-rank launcher (`--gpus N` without WORLD_SIZE), on the CPU: the
 parent spawns N workers with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, they meet over the
 host channel (token-checked rendezvous), time their steps between barriers, all-gather
-their rewards and check the whole vector; the parent relays rank 0's line. `--dry-host`
-uses the CPU oracle's rewards and never loads HIP. Failures must give a non-zero exit:
-unequal shards, a corrupted gathered vector, WORLD_SIZE != --gpus, more ranks than GPUs."""
+their rewards in the RCCL path's padded block layout (uneven shards included) and check
+the whole vector; the parent relays rank 0's line. `--dry-host` uses the CPU oracle's
+rewards and never loads HIP. Failures must give a non-zero exit: a corrupted gathered
+vector, WORLD_SIZE != --gpus, more ranks than GPUs."""
 import json
 import os
 import subprocess
@@ -44,14 +45,23 @@ def test_launcher_dry_host(world):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("flag", ["--dry-host-uneven", "--dry-host-corrupt"])
-def test_launcher_fails_loudly(flag):
-    p = run(["--gpus", "3", "--dry-host", flag] + SMALL)
+def test_launcher_uneven_shards_padded():
+    """The last rank holds one env more (shard_range's split of 3 * 2 + 1 envs): the
+    gathers ship every rank's block padded to the largest shard, and the unpadded vector
+    equals every rank's local values."""
+    p = run(["--gpus", "3", "--dry-host", "--dry-host-uneven"] + SMALL)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    d = json.loads(p.stdout.decode().strip().splitlines()[0])
+    assert d["shard_sizes"] == [2, 2, 3] and d["config"]["global_envs"] == 7
+    assert d["gathered_rewards_ok"] is True and d["gathered_stats_ok"] is True
+
+
+@pytest.mark.timeout(200)
+def test_launcher_fails_loudly():
+    p = run(["--gpus", "3", "--dry-host", "--dry-host-corrupt"] + SMALL)
     assert p.returncode != 0
     assert p.stdout.decode().strip() == ""
     assert "run failed" in p.stderr.decode()
-    if flag == "--dry-host-uneven":
-        assert "unequal env shards" in p.stderr.decode()
 
 
 @pytest.mark.timeout(60)

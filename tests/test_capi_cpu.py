@@ -182,15 +182,39 @@ def test_reference_module_paths_import():
     assert u._get_pos_diff(p).shape == (3, 3, 2) and u._get_pos_diff(p, p[:2]).shape == (3, 2, 2)
 
 
-def test_unequal_shards_rejected_by_comm_rule():
+def test_shard_size_rule():
     """fe_comm_init all-gathers every rank's n_envs and applies fe_check_shard_sizes:
-    unequal shards (which would make ncclAllGather's counts disagree: a hang or corrupt
-    gather) are GF_ECOMM; equal ones pass. The rule itself runs on the host."""
+    uneven shards are accepted (the gathers pad every block to the largest shard);
+    a size below 1 (a corrupted exchange: a handle always holds an env) is GF_ECOMM.
+    The rule itself runs on the host."""
     from gym_flock import _native as nat
     nat.check_shard_sizes([256] * 8)
     nat.check_shard_sizes([3])
-    for bad in ([256, 255], [4, 4, 4, 0], [1, 2, 3, 4, 5, 6, 7, 8]):
+    nat.check_shard_sizes([256, 255])
+    nat.check_shard_sizes([1, 2, 3, 4, 5, 6, 7, 8])
+    for bad in ([4, 4, 4, 0], [2, -1]):
         with pytest.raises(nat.GymFlockError) as e:
             nat.check_shard_sizes(bad)
         assert e.value.code == nat.GF_ECOMM
-        assert "unequal env shards" in str(e.value)
+        assert "bad env shard sizes" in str(e.value)
+
+
+def test_unpad_gathered_layout():
+    """shard.unpad_gathered on the RCCL gathers' block layout (rank-major blocks padded
+    to the largest shard, include/gymflock.h): rewards (world, steps, W) and stats
+    (world, W, 2) come back in global env order, padding dropped."""
+    from gym_flock.shard import pad_block, shard_range, unpad_gathered
+    total, world, steps = 11, 4, 3
+    sizes = [b - a for a, b in (shard_range(total, world, r) for r in range(world))]
+    W = max(sizes)
+    rew = np.arange(steps * total, dtype=np.float64).reshape(steps, total) + 0.5
+    st = np.arange(total * 2, dtype=np.float64).reshape(total, 2) - 7.25
+    rblocks, sblocks = [], []
+    for r in range(world):
+        a, b = shard_range(total, world, r)
+        rblocks.append(pad_block(rew[:, a:b], W, axis=1))
+        sblocks.append(pad_block(st[a:b], W, axis=0))
+    assert all(blk.shape == (steps, W) for blk in rblocks)
+    np.testing.assert_array_equal(unpad_gathered(np.stack(rblocks), sizes, axis=1), rew)
+    np.testing.assert_array_equal(unpad_gathered(np.stack(sblocks), sizes, axis=0), st)
+

@@ -275,27 +275,6 @@ def test_flocking_v0_env_api():
     env.close()
 
 
-def test_rccl_reward_gather_single_rank():
-    """The metrics path at one rank: every 8-step block of rewards comes back from the
-    RCCL all-gather in step order (multi-rank runs use the same calls per rank)."""
-    from gym_flock.shard import RcclRewardGather
-    B, N = 4, 64
-    v = VecFlockingRelative(B, N)
-    v.reset(seed=3)
-    g = RcclRewardGather(v.h, 1, 0, v.h.comm_unique_id())
-    u = np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
-    hist = []
-    for t in range(19):
-        v.step(u)
-        hist.append(v.rewards())
-        g.issue()
-        got = g.result()  # the latest reward computations of this 8-slot block
-        assert 1 <= got.shape[0] <= 8
-        k = min(got.shape[0], len(hist))
-        np.testing.assert_array_equal(got[-k:], np.array(hist[-k:]))
-    v.close()
-
-
 def test_config5_size_sampled_rows():
     """N=8192 (BASELINE.json configs[4]'s agent count; 16-row blocks, 16 LDS tiles per
     row sweep): the whole state and reward, and 40 sampled rows of the network,

@@ -105,35 +105,57 @@ def test_eight_ranks_rendezvous_and_whole_vector_check():
 
 
 @pytest.mark.timeout(60)
-def test_rendezvous_refuses_wrong_token():
-    """A process that reaches rank 0's port with the wrong token is refused (bench.py's
-    launcher sets GYMFLOCK_HOST_TOKEN); nothing it sends is ever unpickled."""
+def test_rendezvous_drops_stray_peers_and_goes_on():
+    """Processes that reach rank 0's port during the rendezvous with the wrong token, or
+    that connect and send nothing, are dropped (bench.py's launcher sets
+    GYMFLOCK_HOST_TOKEN; nothing received is ever unpickled), and the real rank 1 still
+    joins; with rank 1 missing, rank 0 fails at the timeout with its peers closed."""
     import struct
     import threading
+    import time
     sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-flock_amd")]
     from gym_flock.hostgroup import HostGroup
     port = _free_port()
-    err = []
+    out, err = [], []
 
-    def rank0():
+    def rank0(timeout):
         try:
-            HostGroup(0, 2, "127.0.0.1", port, timeout=20, token=b"k" * 32)
+            g = HostGroup(0, 2, "127.0.0.1", port, timeout=timeout, token=b"k" * 32)
+            out.append(g)
         except Exception as e:  # noqa: BLE001
             err.append(e)
 
-    t = threading.Thread(target=rank0)
+    def connect():
+        for _ in range(200):
+            try:
+                return socket.create_connection(("127.0.0.1", port), timeout=5)
+            except OSError:
+                time.sleep(0.05)
+        raise AssertionError("rank 0 never listened")
+
+    HostGroup.HELLO_TIMEOUT = 1.0
+    t = threading.Thread(target=rank0, args=(30,))
     t.start()
-    for _ in range(100):
-        try:
-            s = socket.create_connection(("127.0.0.1", port), timeout=5)
-            break
-        except OSError:
-            import time
-            time.sleep(0.05)
-    s.sendall(struct.pack("!I", 1) + b"x" * 32)
-    t.join(timeout=30)
-    s.close()
-    assert err and "wrong token" in str(err[0])
+    bad = connect()
+    bad.sendall(struct.pack("!I", 1) + b"x" * 32)   # wrong token
+    silent = connect()                                # says nothing
+    g1 = HostGroup(1, 2, "127.0.0.1", port, timeout=30, token=b"k" * 32)
+    t.join(timeout=40)
+    bad.close()
+    silent.close()
+    assert not err and out, err
+    g0 = out[0]
+    assert len(g0.refused) == 2
+    threading.Thread(target=lambda: g1.barrier()).start()
+    g0.barrier()
+    g0.close()
+    g1.close()
+
+    # nobody joins: a bounded failure, not a hang
+    port = _free_port()
+    t0 = time.monotonic()
+    rank0(2)
+    assert err and "ranks joined" in str(err[-1]) and time.monotonic() - t0 < 10
 
 
 def test_struct_messages_only():

@@ -1,0 +1,143 @@
+"""The RCCL metrics path (include/gymflock.h fe_comm_* / fe_allgather_*)
+on one GPU: the reward all-gather ships every step since the previous gather exactly
+once at any interval, refuses a gap longer than the ring; a communicator whose peers
+never join fails within its timeout and leaves the handle stepping; RCCL's own view of
+the communicator; destroy and re-init. Multi-rank layouts (uneven shards padded to the
+largest) are covered on the CPU (test_shard_gloo, test_capi_cpu)."""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import flocking as orc
+
+pytestmark = pytest.mark.gpu
+
+nat = pytest.importorskip("gym_flock._native")
+from gym_flock.init_states import synthetic_batch  # noqa: E402
+from gym_flock.shard import RcclRewardGather  # noqa: E402
+from gym_flock.vec import VecFlockingRelative  # noqa: E402
+
+
+@pytest.mark.parametrize("interval", [3, 5, 8, 13])
+def test_reward_gather_every_step_once(interval):
+    """Gathers every `interval` steps over 70 steps (the 64-slot ring wraps): the
+    concatenated gathered rows equal the rewards of every step, in order, each once."""
+    B, N = 4, 64
+    v = VecFlockingRelative(B, N)
+    v.reset(seed=3)
+    g = RcclRewardGather(v.h, 1, 0, v.h.comm_unique_id(), timeout=60.0)
+    u = np.random.RandomState(0).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    hist, got = [], []
+    for t in range(70):
+        v.step(u)
+        hist.append(v.rewards())
+        if (t + 1) % interval == 0:
+            g.issue()
+            got.append(g.result())
+            assert got[-1].shape == (interval, B)
+    if len(hist) % interval:
+        g.issue()
+        got.append(g.result())
+    np.testing.assert_array_equal(np.concatenate(got), np.array(hist))
+    with pytest.raises(nat.GymFlockError) as e:  # nothing new to ship
+        g.issue()
+    assert e.value.code == nat.GF_ESTATE
+    v.close()
+
+
+def test_reward_gather_gap_longer_than_ring():
+    """More than 64 steps between gathers: the oldest rewards were overwritten, so the
+    gather refuses (GF_ESTATE) and skips them; the next gather ships the next steps."""
+    B, N = 3, 32
+    v = VecFlockingRelative(B, N)
+    v.reset(seed=1)
+    g = RcclRewardGather(v.h, 1, 0, v.h.comm_unique_id(), timeout=60.0)
+    u = np.random.RandomState(1).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    for _ in range(65):
+        v.step(u)
+    with pytest.raises(nat.GymFlockError) as e:
+        g.issue()
+    assert e.value.code == nat.GF_ESTATE and "overwritten" in str(e.value)
+    want = []
+    for _ in range(2):
+        v.step(u)
+        want.append(v.rewards())
+    g.issue()
+    np.testing.assert_array_equal(g.result(), np.array(want))
+    v.close()
+
+
+def test_comm_info_destroy_reinit():
+    """RCCL's own view at one rank (count 1, user rank 0, device 0 and its PCI bus id);
+    fe_comm_destroy tears the metrics path down and a second init works."""
+    B, N = 2, 32
+    h = nat.FlockHandle(N, B)
+    h.set_state(synthetic_batch(B, N))
+    u = np.zeros((B, N, 2), np.float32)
+    for rnd in range(2):
+        h.comm_init(1, 0, nat.FlockHandle.comm_unique_id(), timeout=60.0)
+        info = h.comm_info()
+        assert info["count"] == 1 and info["user_rank"] == 0 and info["device"] == 0
+        assert len(info["pci_bus_id"]) >= 7, info
+        assert h.shard_sizes == [B] and h.max_envs == B
+        h.step(u, 0)
+        h.allgather_rewards()
+        np.testing.assert_array_equal(h.gathered_rewards()[0, -1], h.rewards())
+        h.comm_destroy()
+        with pytest.raises(nat.GymFlockError) as e:
+            h.allgather_rewards()
+        assert e.value.code == nat.GF_ESTATE
+    h.close()
+
+
+_LONE_RANK = r"""
+import sys, time
+import numpy as np
+sys.path[:0] = [{root!r}, {pkg!r}]
+from gym_flock import _native as nat
+from gym_flock.init_states import synthetic_batch
+from oracle import flocking as orc
+B, N = 2, 48
+h = nat.FlockHandle(N, B)
+x0 = synthetic_batch(B, N, seed0=4)
+h.set_state(x0)
+t0 = time.monotonic()
+try:
+    h.comm_init(2, 0, nat.FlockHandle.comm_unique_id(), timeout=5.0)
+    print("INIT_OK")
+except nat.GymFlockError as e:
+    print("CODE", e.code, "SECONDS", round(time.monotonic() - t0, 2))
+    print("MSG", str(e).replace("\n", " "))
+u = np.random.RandomState(2).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+h.step(u, 0)
+x1 = h.get_state()
+ok = all(np.array_equal(x1[b], orc.step(x0[b], u[b])["x"]) for b in range(B))
+print("STEP_OK", ok)
+h.close()
+"""
+
+
+def test_comm_init_peer_never_joins():
+    """Rank 0 of a 2-rank communicator whose rank 1 never starts: fe_comm_init_timeout
+    (5 s) returns GF_ECOMM within 15 s (non-blocking init polled, then aborted) and the
+    handle still steps, bit-exact against the oracle. In a child process, so a hang
+    there cannot take the test runner with it."""
+    code = _LONE_RANK.format(root=ROOT, pkg=os.path.join(ROOT, "gym-flock_amd"))
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=90)
+    wall = time.monotonic() - t0
+    out = p.stdout.decode()
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    assert "INIT_OK" not in out
+    fields = dict(ln.split(" ", 1) for ln in out.splitlines() if " " in ln)
+    code_s, secs = fields["CODE"].split(" SECONDS ")
+    assert int(code_s) == nat.GF_ECOMM, out
+    assert float(secs) < 15.0, out
+    assert "timed out" in fields["MSG"], out
+    assert fields["STEP_OK"] == "True", out
+    print("lone-rank init failed after %s s (child wall %.1f s): %s" % (secs, wall, fields["MSG"]))

@@ -1,7 +1,10 @@
 """World-size-2 gloo test of the multi-GPU path's logic on CPU: each rank owns a
 contiguous shard of the env batch (shard_range), computes its envs' rewards (here
-with the oracle, since there is no GPU) and all-gathers them (GlooRewardGather);
-the gathered vector must equal the single-process batch in global env order."""
+with the oracle, since there is no GPU) and all-gathers them, twice: with
+GlooRewardGather, and in the RCCL path's padded block layout (shard.pad_block on every
+rank, one fixed-size all-gather, shard.unpad_gathered: the code RcclRewardGather.result
+runs). 5 envs over 2 ranks are uneven shards (3 + 2). Both gathered vectors must equal
+the single-process batch in global env order."""
 import os
 import socket
 import sys
@@ -41,10 +44,19 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    from gym_flock.shard import pad_block, unpad_gathered
     start, stop = shard_range(TOTAL_ENVS, world, rank)
-    got = GlooRewardGather().gather(_rewards_for(start, stop))
+    local = _rewards_for(start, stop)
+    got = GlooRewardGather().gather(local)
+    sizes = [b - a for a, b in (shard_range(TOTAL_ENVS, world, r) for r in range(world))]
+    W = max(sizes)
+    blk = torch.from_numpy(pad_block(local, W))
+    parts = [torch.zeros(W, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(parts, blk)
+    padded = unpad_gathered(np.stack([p.numpy() for p in parts]), sizes, axis=0)
     if rank == 0:
-        q.put(got)
+        q.put((got, padded, sizes))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -57,8 +69,11 @@ def test_sharded_reward_allgather_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=100)
+    got, padded, sizes = q.get(timeout=100)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    np.testing.assert_array_equal(got, _rewards_for(0, TOTAL_ENVS))
+    assert sizes == [3, 2]
+    want = _rewards_for(0, TOTAL_ENVS)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(padded, want)
