@@ -351,8 +351,11 @@ def bench_dropin(args):
     iteration (u = env.controller(); env.step(u), the expert loop). Per-call wall time at
     N=100 and N=1024 for each way of fetching the outputs ("getters": three synchronous
     getters; "batched": one fe_get_outputs call and one sync into fresh numpy arrays;
-    "pooled": the same call into page-locked arrays from the env's HostPool), with the reference's op sequence (oracle/cpu_ref.py) timed
-    beside it on one core."""
+    "pooled": the same call into page-locked arrays from the env's HostPool; "direct", the
+    env default: one fe_step_host call, the kernel reading the actions from and writing the
+    outputs to page-locked memory, and computing the next expert action in the same launch
+    once controller() is in use), with the reference's op sequence (oracle/cpu_ref.py)
+    timed beside it on one core."""
     from gym_flock.envs.flocking.flocking_relative import FlockingRelativeEnv
     from gym_flock.init_states import synthetic_state
     from oracle.cpu_ref import CpuFlock
@@ -361,7 +364,7 @@ def bench_dropin(args):
         x0 = synthetic_state(n, 0)
         u32 = np.random.RandomState(5).uniform(-1, 1, size=(n, 2)).astype(np.float32)
         row = {}
-        for mode in ("getters", "batched", "pooled"):
+        for mode in ("getters", "batched", "pooled", "direct"):
             env = FlockingRelativeEnv()
             env.n_agents = n
             env._make_spaces()
@@ -399,7 +402,8 @@ def bench_dropin(args):
         out["n%d" % n] = row
     out["note"] = ("one env per FlockingRelativeEnv object, float32 host actions for step_ms, float64 controller() "
                    "output for controller_plus_step_ms; outputs copied to fresh host arrays every call, as the "
-                   "reference returns them; the env default is fetch_mode='pooled'")
+                   "reference returns them; the env default is fetch_mode='direct' (one launch and one wait per "
+                   "step, the expert action of the new state fused into it)")
     return out
 
 

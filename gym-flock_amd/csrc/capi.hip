@@ -97,6 +97,8 @@ struct fe_handle {
   int32_t* degree = nullptr;
   int u_resident_f64 = -1;              // dtype of the resident actions (-1: none)
   bool has_state = false, has_ctrl = false, has_obs = false, has_knn = false;
+  bool obs_on_host = false;             // the last launch wrote state_values / network to
+                                        // host arrays only (fe_step_host): device copies stale
   int R = 0, T = 0, bpe = 0;
   size_t BN = 0;
   int diag = 0;                         // ablation switches (diagnostic build only, fe_diag)
@@ -473,6 +475,7 @@ gf::StepArgs env_range(const fe_handle* h, const gf::StepArgs& a, int b0, int nb
   if (a.network) r.network = a.network + e0 * N;
   if (a.ctrl_out) r.ctrl_out = a.ctrl_out + e0 * 2;
   if (a.reward) r.reward = a.reward + b0;
+  if (a.reward2) r.reward2 = a.reward2 + b0;
   if (a.dt_env) r.dt_env = a.dt_env + b0;
   if (a.adj_bits) r.adj_bits = a.adj_bits + e0 * Wn;
   if (a.degree_out) r.degree_out = a.degree_out + e0;
@@ -838,6 +841,7 @@ int fe_compute_helpers(fe_handle* h, int flags) {
     h->has_ctrl = true;
   }
   h->has_obs = true;
+  h->obs_on_host = false;
   if (km)
     if (int rc = launch_knn_cur(h, km)) return rc;
   return GF_OK;
@@ -891,11 +895,69 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   if (ctrl) h->ccur ^= 1;
   h->has_ctrl = ctrl;
   h->has_obs = true;
+  h->obs_on_host = false;
   h->has_knn = false;
   if (km)
     if (int rc = launch_knn_cur(h, km)) return rc;
   // the host action buffer is borrowed only for this call: wait for its copy, not the step
   if (!(flags & (FE_U_DEVICE | FE_U_EXPERT | FE_U_RESIDENT))) GF_HIP(hipEventSynchronize(h->h2d_ev));
+  return GF_OK;
+}
+
+int fe_step_host(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                 double* controls, int flags) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->has_state) return fail(GF_ESTATE, "state not set (call fe_set_state first)");
+  if (flags & ~(FE_U_F64 | FE_WITH_CONTROLLER)) return fail(GF_EINVAL, "flags: FE_U_F64 and FE_WITH_CONTROLLER only");
+  if (controls) flags |= FE_WITH_CONTROLLER;
+  // one launch on the handle's stream, after all of its outstanding work
+  if (int rc = use_dev(h)) return rc;
+  const bool dyn = u != nullptr, ctrl = flags & FE_WITH_CONTROLLER, uf64 = dyn && (flags & FE_U_F64);
+  const void* up = nullptr;
+  if (dyn) {
+    up = mapped_ptr(const_cast<void*>(u));  // page-locked: the kernel reads it in place
+    if (!up) {
+      GF_HIP(hipMemcpyAsync(h->u, u, h->BN * 2 * (uf64 ? 8 : 4), hipMemcpyHostToDevice, h->stream));
+      up = h->u;
+      h->u_resident_f64 = -1;
+    }
+  }
+  if (int rc = next_reward_slot(h)) return rc;
+  // page-locked destinations are written by the kernel through their mapped addresses;
+  // others get the device buffer and a copy after the launch
+  float* sv_m = state_values ? static_cast<float*>(mapped_ptr(state_values)) : nullptr;
+  float* net_m = network ? static_cast<float*>(mapped_ptr(network)) : nullptr;
+  double* rw_m = rewards ? static_cast<double*>(mapped_ptr(rewards)) : nullptr;
+  double* ct_m = controls ? static_cast<double*>(mapped_ptr(controls)) : nullptr;
+  gf::StepArgs a = base_args(h);
+  a.x_in = h->x[h->cur];
+  if (dyn) {
+    a.x_out = h->x[h->cur ^ 1];
+    a.u = up;
+  }
+  a.state_values = state_values ? (sv_m ? sv_m : h->sv) : nullptr;
+  a.network = network ? (net_m ? net_m : h->net) : nullptr;
+  a.ctrl_out = ctrl ? (ct_m ? ct_m : h->ctrl[h->ccur ^ 1]) : nullptr;
+  a.reward = cur_reward(h);
+  a.reward2 = rw_m;
+  if (int rc = prepare_outputs(h, 0, a, dyn ? h->cur ^ 1 : -1)) return rc;
+  if (int rc = timed_launch(h, a, dyn, uf64, ctrl)) return rc;
+  if (dyn) h->cur ^= 1;
+  const size_t nsv = h->BN * 6, nnet = h->BN * (size_t)h->cfg.n_agents, nct = h->BN * 2;
+  if (state_values && !sv_m)
+    GF_HIP(hipMemcpyAsync(state_values, h->sv, nsv * 4, hipMemcpyDeviceToHost, h->stream));
+  if (network && !net_m) GF_HIP(hipMemcpyAsync(network, h->net, nnet * 4, hipMemcpyDeviceToHost, h->stream));
+  if (rewards && !rw_m)
+    GF_HIP(hipMemcpyAsync(rewards, cur_reward(h), (size_t)h->cfg.n_envs * 8, hipMemcpyDeviceToHost, h->stream));
+  if (ctrl && !ct_m) {
+    h->ccur ^= 1;
+    if (controls) GF_HIP(hipMemcpyAsync(controls, h->ctrl[h->ccur], nct * 8, hipMemcpyDeviceToHost, h->stream));
+  }
+  if (dyn || ctrl) h->has_ctrl = ctrl && !ct_m;  // device controls of the current state
+  h->has_obs = true;
+  h->obs_on_host = sv_m || net_m;
+  h->has_knn = false;
+  GF_HIP(hipStreamSynchronize(h->stream));
   return GF_OK;
 }
 
@@ -1013,6 +1075,7 @@ int fe_get_state_values(fe_handle* h, int env, float* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
   if (int rc = check_env(h, env)) return rc;
   if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (h->obs_on_host) return fail(GF_ESTATE, "the last step wrote its observations to host arrays (fe_step_host)");
   if (int rc = use_dev(h)) return rc;
   const size_t n = (size_t)h->cfg.n_agents * 6;
   return env < 0 ? d2h(h, dst, h->sv, h->BN * 6 * 4) : d2h(h, dst, h->sv + env * n, n * 4);
@@ -1022,6 +1085,7 @@ int fe_get_network(fe_handle* h, int env, float* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
   if (int rc = check_env(h, env)) return rc;
   if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (h->obs_on_host) return fail(GF_ESTATE, "the last step wrote its observations to host arrays (fe_step_host)");
   if (int rc = use_dev(h)) return rc;
   const size_t n = (size_t)h->cfg.n_agents * h->cfg.n_agents;
   return env < 0 ? d2h(h, dst, h->net, h->BN * h->cfg.n_agents * 4) : d2h(h, dst, h->net + env * n, n * 4);
@@ -1031,7 +1095,7 @@ int fe_get_network_rows(fe_handle* h, int env, int row0, int nrows, float* dst) 
   if (!h || !dst || env < 0 || row0 < 0 || nrows < 0 || row0 + nrows > h->cfg.n_agents)
     return fail(GF_EINVAL, "bad argument");
   if (int rc = check_env(h, env)) return rc;
-  if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (!h->has_obs || h->obs_on_host) return fail(GF_ESTATE, "no device observation (none yet, or fe_step_host wrote it to host arrays)");
   if (int rc = use_dev(h)) return rc;
   const size_t N = h->cfg.n_agents;
   return d2h(h, dst, h->net + (env * N + row0) * N, (size_t)nrows * N * 4);
@@ -1070,6 +1134,8 @@ int fe_get_outputs(fe_handle* h, int env, float* state_values, float* network, d
   if (flags & ~FE_OUT_MAPPED) return fail(GF_EINVAL, "flags: 0 or FE_OUT_MAPPED");
   if (int rc = check_env(h, env)) return rc;
   if (!h->has_obs) return fail(GF_ESTATE, "no observation computed yet");
+  if (h->obs_on_host && (state_values || network))
+    return fail(GF_ESTATE, "the last step wrote its observations to host arrays (fe_step_host)");
   if (int rc = use_dev(h)) return rc;
   const size_t N = h->cfg.n_agents;
   const size_t nsv = env < 0 ? h->BN * 6 : N * 6, nnet = env < 0 ? h->BN * N : N * N;

@@ -42,6 +42,7 @@ struct StepArgs {
   float* network;         // (B,N,N) or nullptr
   double* ctrl_out;       // (B,N,2) or nullptr (CTRL only)
   double* reward;         // (B) or nullptr
+  double* reward2;        // (B) or nullptr: a second copy (fe_step_host's page-locked array)
   double dt, action_scalar, cr, cr2;
   float dt_f, as_f;
   int N, B;

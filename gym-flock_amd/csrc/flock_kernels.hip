@@ -707,7 +707,11 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
     }
     const double Qx = block_sum(qx, red);
     const double Qy = block_sum(qy, red);
-    if (tid == 0) a.reward[b] = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
+    if (tid == 0) {
+      const double rw = -1.0 * (Qx / static_cast<double>(N) + Qy / static_cast<double>(N));
+      a.reward[b] = rw;
+      if (a.reward2) a.reward2[b] = rw;
+    }
   }
 }
 
@@ -761,8 +765,13 @@ void flock_step_kernel(StepArgs a) {
   St* tile = reinterpret_cast<St*>(smem + 4 * kStoreTab * 16 + ((R * 8 + 31) & ~31));  // float64 state, T
   St* rows = tile + T;                                         // this block's rows, R
   uint64_t* adj = reinterpret_cast<uint64_t*>(rows + R);       // R x Wn adjacency bits
-  uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits
-  uint64_t* candb = nearb + (CTRL ? (size_t)R * Wt : 0);       // (predicted rows) x Wt kNN candidates
+  // the controller without kNN (kOuter): pass 1 leaves in adj the float32 superset of both
+  // the adjacency and the controller's "near" pairs, and the feature pass decides both
+  // exactly in float64 (it computes every such pair's r2 anyway), writing the exact
+  // adjacency words back; the fused-kNN controller keeps separate near bits
+  constexpr bool kOuter = CTRL && KN == 0;
+  uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits (KN && CTRL)
+  uint64_t* candb = nearb + ((CTRL && !kOuter) ? (size_t)R * Wt : 0);  // (predicted rows) x Wt kNN candidates
   double* red = reinterpret_cast<double*>(candb + (KN ? (size_t)R * Wt : 0));
   float* redf = reinterpret_cast<float*>(red + 4);
   float* inv = reinterpret_cast<float*>(red + 8);
@@ -851,16 +860,24 @@ void flock_step_kernel(StepArgs a) {
     const St o = tile[c];
     const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
+    if constexpr (kOuter) {  // a pass-1 candidate: both decisions exactly (:117, :225)
+      isadj = r2 < a.cr2;
+      isnear = r2 <= a.cr;
+      if (!isadj && !isnear) return isadj;
+    }
     if constexpr (KN > 0) {
       if (!GF_ABLATE(a, 0x200000)) {  // diag 0x200000: no insertion (timing only)
         // q = min(floor(r2 * ksc), qmax); fmin returns qmax for a NaN r2 (ranked last)
         const unsigned q = static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
         knn_list_insert<KL>(kk, (q << a.knn_jbits) | static_cast<unsigned>(j0 + c));
       }
-      if (!isadj && !(CTRL && isnear)) return;  // a candidate only: no features
+      if (!isadj && !(CTRL && isnear)) return isadj;  // a candidate only: no features
     }
     // one reciprocal per pair: q = d / r2, d / r2^2 from 1/r2 (a few ulp from the
     // reference's two divisions; far inside the float32 outputs' tolerance)
+    // the controller (rtol 1e-9 on its output) keeps the IEEE division: v_rcp_f64 with one
+    // or two Newton steps measured the same (174.3 / 175.0 / 174.6 us per config-2 step,
+    // profiles/r04/ab_ctrl_recip.txt)
     const double ir = CTRL ? 1.0 / r2 : recip_f64(r2), irr = ir * ir;
     const double q1x = dx * irr, q2x = dx * ir;
     const double q1y = dy * irr, q2y = dy * ir;
@@ -880,6 +897,7 @@ void flock_step_kernel(StepArgs a) {
         gy += (-2.0 * q1y) + (2.0 * q2y);
       }
     }
+    return isadj;
   };
 
   // pass 2: features / gradients for the set bits of one tile, ascending j per slice.
@@ -899,14 +917,26 @@ void flock_step_kernel(StepArgs a) {
     const int wpt = (nch + S - 1) / S;
     const int wb = fs * wpt, we = min(nch, wb + wpt);
     for (int w = wb; w < we; ++w) {
-      const uint64_t am = adj[(size_t)fr * Wn + (j0 >> 6) + w];
+      uint64_t* aw = adj + (size_t)fr * Wn + (j0 >> 6) + w;
+      const uint64_t am = *aw;
+      if constexpr (kOuter) {  // candidates in, the exact adjacency word out
+        uint64_t m = am, ex = 0;
+        while (m) {
+          const int k = __builtin_ctzll(m);
+          m &= m - 1;
+          if (pair_terms(me, j0, (w << 6) + k, false, false, ksc)) ex |= 1ull << k;
+        }
+        *aw = ex;
+        continue;
+      }
       const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
       const uint64_t cm = (KN && crow) ? crow[w] : 0ull;
       uint64_t m = am | nm | cm;
       while (m) {
         const int k = __builtin_ctzll(m);
         m &= m - 1;
-        pair_terms(me, j0, (w << 6) + k, (am >> k) & 1ull, CTRL && ((nm >> k) & 1ull), ksc);
+        // without the controller and the kNN candidates every iterated bit is a neighbour
+        pair_terms(me, j0, (w << 6) + k, (!CTRL && KN == 0) || ((am >> k) & 1ull), CTRL && ((nm >> k) & 1ull), ksc);
       }
     }
   };
@@ -939,7 +969,7 @@ void flock_step_kernel(StepArgs a) {
         rx32 = static_cast<float>(ri.px);
         ry32 = static_cast<float>(ri.py);
         if (wid == 0) rxy[lane] = make_float2(rx32, ry32);
-      } else if (!CTRL && wid == 0 && lane < ((nrows + 3) & ~3)) {
+      } else if ((!CTRL || kOuter) && wid == 0 && lane < ((nrows + 3) & ~3)) {
         rxy[lane] = make_float2(-1.0e18f, -1.0e18f);  // pass 1's padding rows (far away)
       }
       Pr = wave_max(fmaxf(fabsf(rx32), fabsf(ry32)));
@@ -1037,6 +1067,22 @@ void flock_step_kernel(StepArgs a) {
         } else {
           for (int r = 0; r < nrows; ++r) frow(r, row_pos(r));
         }
+      } else if (kOuter) {
+        // every pair within float32 reach of either threshold (r2 < cr^2 or r2 <= cr):
+        // one compare per column, no band sweep; the feature pass decides them exactly.
+        // Rows in pairs as the plain step; the rows past nrows sit far away in rxy.
+        const float ho = uniform_f(fmaxf(ba.hi, bn.hi));
+        auto orow = [&](int r, float2 pr) {
+          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
+          put_lane(wa0, wa1, __ballot(!(d2.x > ho)), r);
+          put_lane(wb0, wb1, __ballot(!(d2.y > ho)), r);
+        };
+        const int nr4 = (nrows + 3) & ~3;
+        for (int r = 0; r < nr4; r += 2) {
+          const float2 p0 = rxy[r], p1 = rxy[r + 1];
+          orow(r, p0);
+          orow(r + 1, p1);
+        }
       } else {
         auto row1 = [&](int r, float2 pr) {
           const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
@@ -1119,7 +1165,7 @@ void flock_step_kernel(StepArgs a) {
         uint64_t* arow = adj + (size_t)lane * Wn + (j0 >> 6) + ca;
         arow[0] = ((static_cast<uint64_t>(wa1) << 32) | wa0) & ka;
         if (has_b) arow[1] = ((static_cast<uint64_t>(wb1) << 32) | wb0) & kb;
-        if constexpr (CTRL) {
+        if constexpr (CTRL && !kOuter) {
           uint64_t* nrow = nearb + (size_t)lane * Wt + ca;
           nrow[0] = ((static_cast<uint64_t>(na1) << 32) | na0) & ka;
           if (has_b) nrow[1] = ((static_cast<uint64_t>(nb1) << 32) | nb0) & kb;
@@ -1161,8 +1207,9 @@ void flock_step_kernel(StepArgs a) {
     if (ti < 2) GF_STAMP(3 + 3 * ti);
 
     // pass 2 (features) of every tile but the last runs here; the last tile's runs
-    // after the network stores are issued, so the stores drain under it.
-    if (j0 + T < N) {
+    // after the network stores are issued, so the stores drain under it (kOuter: the
+    // stores need the exact adjacency this pass writes, so every tile's runs here)
+    if (kOuter || j0 + T < N) {
       feature_pass(j0, nch);
       if (ti < 1) GF_STAMP(4);
     }
@@ -1177,6 +1224,7 @@ void flock_step_kernel(StepArgs a) {
   }
   const int jl = ((N - 1) / T) * T;  // first column of the last tile (still in LDS)
   const int nchl = (N - jl + 63) >> 6;
+  if constexpr (kOuter) __syncthreads();  // the last feature pass's adjacency words
 
   // degree of each row -> 1/deg for the mean-pooled network (:120-122)
   {
@@ -1203,7 +1251,7 @@ void flock_step_kernel(StepArgs a) {
   if (a.network) store_network_rows(a, adj, inv, stab, Wn, env0 + i0, nrows, wid, lane);
 
   GF_STAMP(8);
-  feature_pass(jl, nchl);
+  if constexpr (!kOuter) feature_pass(jl, nchl);
   GF_STAMP(9);
 
   [[maybe_unused]] RawState<UF64> kraw{};
@@ -1688,7 +1736,7 @@ int step_tile(int N) {
 size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   const size_t Wn = (N + 63) / 64, Wt = T / 64;
   size_t s = (size_t)T * sizeof(St) + (size_t)R * sizeof(St);
-  s += (size_t)R * Wn * 8 + (ctrl ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
+  s += (size_t)R * Wn * 8 + ((ctrl && knn) ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   // inv (R floats); kNN: rthr (R), the waves' candidate-bound tables (4R), prow (R ints)
   s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 7 : 1) + 15) / 16) * 16;
   s += 4 * kStoreTab * 16 + (((size_t)R * 8 + 31) & ~size_t(31));  // row table, rows' float32 positions

@@ -85,6 +85,7 @@ SIGNATURES = {
     "fe_set_actions": [_P, _P, _I],
     "fe_compute_helpers": [_P, _I],
     "fe_step": [_P, _P, _I],
+    "fe_step_host": [_P, _P, _P, _P, _P, _P, _I],
     "fe_controller": [_P, _I, _P],
     "fe_get_stats": [_P, _I, _P, _P],
     "fe_get_stats_ex": [_P, _I, _P, _P, _P],
@@ -203,7 +204,7 @@ class HostPool:
         import collections
         import threading
         self.cap = int(cap_bytes)
-        self.live = 0
+        self._live = 0  # page-locked bytes handed out and not yet drained back
         self.free = {}
         self.lock = threading.Lock()
         # released buffers, queued without a lock: _release runs from weakref finalizers,
@@ -218,35 +219,47 @@ class HostPool:
                 p, nbytes = self.released.popleft()
             except IndexError:
                 return
-            self.live -= nbytes
+            self._live -= nbytes
             self.free.setdefault(nbytes, []).append(p)
 
+    @property
+    def live(self):
+        """Page-locked bytes held by live arrays (released ones are drained first)."""
+        with self.lock:
+            self._drain()
+            return self._live
+
     def array(self, shape, dtype):
+        return self.array_addr(shape, dtype)[0]
+
+    def array_addr(self, shape, dtype):
+        """(array, its address): a page-locked array from the pool, or past the cap (or if
+        page-locked memory runs out) an ordinary numpy array and None."""
         import weakref
         dtype = np.dtype(dtype)
         nbytes = int(np.prod(shape)) * dtype.itemsize
         if nbytes == 0:
-            return np.empty(shape, dtype)
+            return np.empty(shape, dtype), None
         with self.lock:
             self._drain()
             lst = self.free.get(nbytes)
             p = lst.pop() if lst else None
-            if p is None and self.live + nbytes > self.cap:
-                return np.empty(shape, dtype)
-            self.live += nbytes
+            if p is None and self._live + nbytes > self.cap:
+                return np.empty(shape, dtype), None
+            self._live += nbytes
         if p is None:
             out = ctypes.c_void_p()
             try:
                 check(load().fe_host_alloc(nbytes, ctypes.byref(out)))
             except GymFlockError:
                 with self.lock:
-                    self.live -= nbytes
-                return np.empty(shape, dtype)
+                    self._live -= nbytes
+                return np.empty(shape, dtype), None
             p = out.value
         buf = (ctypes.c_uint8 * nbytes).from_address(p)
         fin = weakref.finalize(buf, self._release, p, nbytes)
         fin.atexit = False  # the process's exit frees page-locked memory
-        return np.frombuffer(buf, dtype=dtype).reshape(shape)
+        return np.frombuffer(buf, dtype=dtype).reshape(shape), p
 
     def _release(self, p, nbytes):
         self.released.append((p, nbytes))  # no lock, no allocation beyond the tuple
@@ -270,6 +283,34 @@ def host_pool():
     if _host_pool is None:
         _host_pool = HostPool()
     return _host_pool
+
+
+class PinnedArray:
+    """A page-locked host array owned by one object (fe_host_alloc / fe_host_free), e.g.
+    the drop-in env's action buffer, which the step kernel reads in place."""
+
+    def __init__(self, shape, dtype):
+        dtype = np.dtype(dtype)
+        nbytes = max(1, int(np.prod(shape)) * dtype.itemsize)
+        out = ctypes.c_void_p()
+        check(load().fe_host_alloc(nbytes, ctypes.byref(out)))
+        self.addr = out.value
+        self.a = np.frombuffer((ctypes.c_uint8 * nbytes).from_address(self.addr), dtype=dtype,
+                               count=int(np.prod(shape))).reshape(shape)
+
+    def close(self):
+        if getattr(self, "addr", None):
+            self.a = None
+            load().fe_host_free(ctypes.c_void_p(self.addr))
+            self.addr = None
+
+    __del__ = close
+
+
+def u_is_f64(u):
+    """Whether the reference's `u * action_scalar` (flocking_relative.py:95) computes in
+    float64 for this action array (NumPy's promotion: float32/float16 stay float32)."""
+    return np.result_type(u.dtype, 10.0) != np.float32
 
 
 def check_shard_sizes(n_envs):
@@ -359,28 +400,39 @@ class FlockHandle:
     def set_actions(self, u):
         """Upload (B,N,2) actions to the resident buffer used by FE_U_RESIDENT."""
         u = np.asarray(u)
-        f64 = u.dtype == np.float64
+        f64 = u_is_f64(u)
         u = np.ascontiguousarray(u, dtype=np.float64 if f64 else np.float32)
         assert u.shape == (self.n_envs, self.n_agents, 2), u.shape
         check(self.lib.fe_set_actions(self.h, ptr(u), int(f64)))
 
     def step(self, u=None, flags=0):
-        """u: host ndarray (B,N,2) float32/float64, or a device pointer (int) with
-        FE_U_DEVICE, or None with FE_U_EXPERT / FE_U_RESIDENT."""
+        """u: host ndarray (B,N,2) (float32 arithmetic for float32/float16 actions, else
+        float64, as NumPy promotes u * 10.0), or a device pointer (int) with FE_U_DEVICE,
+        or None with FE_U_EXPERT / FE_U_RESIDENT."""
         if flags & (FE_U_EXPERT | FE_U_RESIDENT):
             check(self.lib.fe_step(self.h, None, int(flags)))
         elif flags & FE_U_DEVICE:
             check(self.lib.fe_step(self.h, ctypes.c_void_p(int(u)), int(flags)))
         else:
             u = np.asarray(u)
-            if u.dtype == np.float64:
+            if u_is_f64(u):
                 flags |= FE_U_F64
+                u = u.astype(np.float64, copy=False)
             else:
                 u = u.astype(np.float32, copy=False)
                 flags &= ~FE_U_F64
             u = np.ascontiguousarray(u)
             assert u.shape == (self.n_envs, self.n_agents, 2), u.shape
             check(self.lib.fe_step(self.h, ptr(u), int(flags)))
+
+    def step_host(self, u_addr, f64, sv, net, rew, ctrl):
+        """fe_step_host: one launch and one wait. u_addr: address of (B,N,2) host actions
+        (page-locked ones are read in place) or None (compute_helpers); sv / net / rew /
+        ctrl: addresses of host destinations or None (page-locked ones are written by the
+        kernel directly). Addresses are ints (the drop-in env passes pool addresses)."""
+        rc = self.lib.fe_step_host(self.h, u_addr, sv, net, rew, ctrl, FE_U_F64 if f64 else 0)
+        if rc:
+            check(rc)
 
     def controller(self, centralized=None):
         out = np.empty((self.n_envs, self.n_agents, 2))

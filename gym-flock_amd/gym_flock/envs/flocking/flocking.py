@@ -25,6 +25,7 @@ class FlockingEnv(FlockingRelativeEnv):
         assert u.shape == (self.n_agents, self.nu)
         self.u = u * self.action_scalar
         self._handle().step(u[None], flags=nat.FE_WITH_KNN)
+        self._ctrl_cache = None
         self._fetch_obs()
         return (self.get_observation(), self.state_network), self.instant_cost(), False, {}
 

@@ -57,11 +57,18 @@ class FlockingRelativeEnv(Env):
         self.n_neighbors = 0
         self.reset_mode = "reference"
         self.reset_max_attempts = 1000
-        # how step() brings (state_values, network, reward) to the host: "pooled" = one
-        # fe_get_outputs call into page-locked arrays from the process's HostPool (fresh
-        # arrays to the caller, recycled once released); "batched" = the same call into
-        # ordinary numpy arrays; "getters" = three synchronous getters (bench.py's dropin)
-        self.fetch_mode = "pooled"
+        # how step() brings (state_values, network, reward) to the host: "direct" = one
+        # fe_step_host call: the kernel reads the actions from a page-locked buffer and
+        # writes the outputs straight into page-locked arrays from the process's HostPool
+        # (fresh arrays to the caller, recycled once released), one launch and one wait;
+        # "pooled" = fe_step, then one fe_get_outputs call into pool arrays; "batched" =
+        # the same into ordinary numpy arrays; "getters" = three synchronous getters
+        self.fetch_mode = "direct"
+        # controller() once asked for, every later step also computes the expert action of
+        # its resulting state in the same launch, and controller() returns it
+        self._want_ctrl = False
+        self._ctrl_cache = None
+        self._ubuf = None
 
         self._make_spaces()
         self.fig = None
@@ -106,6 +113,8 @@ class FlockingRelativeEnv(Env):
         if self._h is None or key != self._hkey:
             if self._h is not None:
                 self._h.close()
+            self._invalidate()
+            self._ubuf = None
             self._h = nat.FlockHandle(self.n_agents, 1, self.comm_radius, self.dt,
                                       self.action_scalar, self.mean_pooling, self.centralized,
                                       self.n_neighbors, self.device)
@@ -131,8 +140,57 @@ class FlockingRelativeEnv(Env):
         value = np.asarray(value, dtype=np.float64)
         assert value.shape == (self.n_agents, self.nx_system), value.shape
         self._handle().set_state(value, env=0)
+        self._invalidate()
+
+    def _invalidate(self):
+        """The state changed outside step(): the cached expert action is stale."""
+        self._ctrl_cache = None
 
     # ---------------------------------------------------------------- hot path
+    def _device_step(self, u):
+        """step(u) (u None: compute_helpers) on the device, observations to the host."""
+        if self.fetch_mode != "direct":
+            h = self._handle()
+            if u is None:
+                h.compute_helpers()
+            else:
+                h.step(u[None])
+            self._ctrl_cache = None
+            self._fetch_obs()
+            return
+        h = self._handle()
+        n = self.n_agents
+        f64 = False
+        uaddr = None
+        if u is not None:
+            f64 = nat.u_is_f64(u)
+            dt = np.float64 if f64 else np.float32
+            if self._ubuf is None or self._ubuf.a.dtype != dt:
+                self._ubuf = nat.PinnedArray((n, 2), dt)  # read by the kernel in place
+            self._ubuf.a[...] = u
+            uaddr = self._ubuf.addr
+        # one page-locked block per step: network, controls, reward, state_values (64-byte
+        # aligned parts, so the network rows get 16-byte stores); the caller's arrays are
+        # views of it, and it returns to the pool once all of them are released
+        ctrl = self._want_ctrl
+        o_ct = (4 * n * n + 63) & ~63
+        o_rw = o_ct + ((16 * n + 63) & ~63 if ctrl else 0)
+        o_sv = o_rw + 64
+        size = o_sv + 24 * n
+        blk, base = nat.host_pool().array_addr((size,), np.uint8)
+        net = blk[:4 * n * n].view(np.float32).reshape(n, n)
+        rw = blk[o_rw:o_rw + 8].view(np.float64)
+        sv = blk[o_sv:o_sv + 24 * n].view(np.float32).reshape(n, 6)
+        ct = blk[o_ct:o_ct + 16 * n].view(np.float64).reshape(n, 2) if ctrl else None
+        if base is None:  # not page-locked (pool cap): the library copies after the launch
+            h.step_host(uaddr, f64, sv.ctypes.data, net.ctypes.data, rw.ctypes.data,
+                        ct.ctypes.data if ctrl else None)
+        else:
+            h.step_host(uaddr, f64, base + o_sv, base, base + o_rw, base + o_ct if ctrl else None)
+        self.state_values, self.state_network = sv, net
+        self._reward = float(rw[0])
+        self._ctrl_cache = ct
+
     def _fetch_obs(self):
         h = self._h
         if self.fetch_mode == "getters":
@@ -140,23 +198,22 @@ class FlockingRelativeEnv(Env):
             self.state_network = h.network(0)
             self._reward = float(h.rewards()[0])
             return
-        pool = nat.host_pool() if self.fetch_mode == "pooled" else None
+        pool = nat.host_pool() if self.fetch_mode in ("pooled", "direct") else None
         self.state_values, self.state_network, rw = h.outputs(0, pool=pool)
         self._reward = float(rw[0])
 
     def step(self, u):
-        """:91-109 — dynamics, compute_helpers and instant_cost in one device launch."""
+        """:91-109 — dynamics, compute_helpers and instant_cost in one device launch (with
+        controller() of the new state fused in, once the caller uses the expert)."""
         u = np.asarray(u)
         assert u.shape == (self.n_agents, self.nu)
         self.u = u * self.action_scalar
-        self._handle().step(u[None])
-        self._fetch_obs()
+        self._device_step(u)
         return (self.state_values, self.state_network), self._reward, False, {}
 
     def compute_helpers(self):
         """:111-134 on the current state."""
-        self._handle().compute_helpers()
-        self._fetch_obs()
+        self._device_step(None)
 
     def instant_cost(self):
         """:145-147 — reward of the current state (computed with the observations)."""
@@ -176,9 +233,17 @@ class FlockingRelativeEnv(Env):
         return {'vel_diffs': vd, 'min_dists': md}
 
     def controller(self, centralized=None):
-        """:194-212 — Turner-2003 expert action (N,2) float64 for the current state."""
+        """:194-212 — Turner-2003 expert action (N,2) float64 for the current state. After
+        a step (or reset) the action was computed in that launch already: it is returned
+        as is (a fresh array; a second call for the same state gets a copy). Otherwise, or
+        for the other `centralized` setting, one launch."""
         if centralized is None:
             centralized = self.centralized
+        self._want_ctrl = True
+        c = self._ctrl_cache
+        if c is not None and bool(centralized) == bool(self.centralized):
+            self._ctrl_cache = c.copy()  # later calls for this state get their own array
+            return c
         return self._handle().controller(centralized)[0]
 
     def potential_grad(self, pos_diff, r2):

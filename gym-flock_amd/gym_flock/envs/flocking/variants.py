@@ -75,8 +75,7 @@ class FlockingLeaderEnv(FlockingRelativeEnv):
         _frozen_prefix(self.mask, self.n_agents, strict=True)
         self.u = u
         self._helpers_x = None
-        self._handle().step(u[None])
-        self._fetch_obs()
+        self._device_step(u)
         return (self.state_values, self.state_network), self._reward, False, {}
 
     def reset(self):
@@ -139,8 +138,7 @@ class FlockingObstacleEnv(FlockingRelativeEnv):
         assert u.shape == (self.n_agents, self.nu)
         _frozen_prefix(self.mask, self.n_agents, strict=True)
         self.u = u
-        self._handle().step(u[None])
-        self._fetch_obs()
+        self._device_step(u)
         return (self.state_values, self.state_network), self._reward, False, {}
 
     def reset(self):
@@ -194,10 +192,8 @@ class FlockingStochasticEnv(FlockingRelativeEnv):
         u = np.clip(u, a_min=-self.max_accel, a_max=self.max_accel)
         self.u = u * self.scale
         self.dt = np.random.normal(self.dt_mean, self.dt_sigma)
-        h = self._handle()
-        h.set_dt(self.dt)
-        h.step(u[None])
-        self._fetch_obs()
+        self._handle().set_dt(self.dt)
+        self._device_step(u)
         return (self.state_values, self.state_network), self._reward, False, {}
 
 

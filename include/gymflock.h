@@ -138,6 +138,20 @@ int fe_compute_helpers(fe_handle* h, int flags);
  * optionally fused controller() (:194-226) and Flocking-v0 kNN (flocking.py:20-25).
  * u: (B,N,2) float32 or float64 (FE_U_F64), host or device (FE_U_DEVICE). Async. */
 int fe_step(fe_handle* h, const void* u, int flags);
+/* The drop-in env's step(u) (:91-109) as one launch and one wait, for small batches
+ * where latency, not bandwidth, counts (FlockingRelativeEnv.step, N ~ 100-1000, B = 1).
+ * u: (B,N,2) host actions, float32 or float64 (FE_U_F64); if page-locked (fe_host_alloc)
+ * the kernel reads them in place, else they are copied first. u == NULL: no dynamics,
+ * compute_helpers (:111-134) on the current state (reset's observation). Outputs, any of
+ * them NULL (not computed): state_values (B,N,6) f32, network (B,N,N) f32, rewards (B)
+ * f64 and controls (B,N,2) f64 = controller() (:194-212) of the resulting state (fused,
+ * FE_WITH_CONTROLLER implied). Page-locked destinations are written by the kernel
+ * through their mapped addresses; others by a copy after it. Returns when all are in
+ * place. Observations written to host arrays are not kept on the device (the device
+ * getters then return GF_ESTATE); rewards also go to the ring (fe_get_rewards, metrics
+ * path). flags: FE_U_F64, FE_WITH_CONTROLLER. */
+int fe_step_host(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                 double* controls, int flags);
 /* controller(centralized) (:194-212) on the current state; centralized < 0 means the
  * config default. Writes (B,N,2) float64 to u_out (host) if non-NULL. */
 int fe_controller(fe_handle* h, int centralized, double* u_out);

@@ -110,6 +110,98 @@ def test_n10_episode_trajectory_bit_exact():
     h.close()
 
 
+@pytest.mark.parametrize("mode", ["direct", "pooled"])
+def test_dropin_expert_loop_episode(mode):
+    """The reference's 40-step N=10 episode (20 expert steps u = env.controller(), then 20
+    float32 random actions) through the drop-in env API. In "direct" mode every step is
+    one fe_step_host launch that also computes the next expert action, which the next
+    controller() returns without a launch. State bit-exact every step; observations,
+    reward and controller as the fixture (tolerances of the module docstring)."""
+    from gym_flock.envs.flocking.flocking_relative import FlockingRelativeEnv
+    f = np.load(os.path.join(GOLDEN, "flock_n10_episode.npz"))
+    env = FlockingRelativeEnv()
+    env.n_agents = 10
+    env._make_spaces()
+    env.fetch_mode = mode
+    env.x = f["x0"]
+    env.compute_helpers()
+    close_sv(env.state_values, f["sv0"])
+    np.testing.assert_array_equal(env.state_network, f["net0"].astype(np.float32))
+    for t in range(40):
+        if not f["u_is_f32"][t]:
+            got = env.controller()
+            np.testing.assert_allclose(got, f["u"][t], rtol=1e-9, atol=1e-12)
+            if t > 0 and mode == "direct":
+                assert env._ctrl_cache is not None  # the fused result, no extra launch
+            np.testing.assert_array_equal(env.controller(), got)  # same state, same answer
+            u = f["u"][t]
+        else:
+            u = f["u"][t].astype(np.float32)
+        (sv, net), r, done, info = env.step(u)
+        assert not done and info == {}
+        np.testing.assert_array_equal(env.x, f["x"][t])
+        close_sv(sv, f["sv"][t])
+        np.testing.assert_array_equal(net, f["net"][t].astype(np.float32))
+        np.testing.assert_allclose(r, f["reward"][t], rtol=1e-12)
+        if mode == "direct" and t >= 1:
+            np.testing.assert_allclose(env._ctrl_cache, f["ctrl"][t], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(env.controller(), f["ctrl"][t], rtol=1e-9, atol=1e-12)
+    # the arrays a step returned stay valid after later steps (fresh arrays per call)
+    (sv_a, net_a), _, _, _ = env.step(np.zeros((10, 2), np.float32))
+    keep = (sv_a.copy(), net_a.copy())
+    env.step(np.ones((10, 2), np.float32))
+    np.testing.assert_array_equal(sv_a, keep[0])
+    np.testing.assert_array_equal(net_a, keep[1])
+    env.close()
+
+
+def test_step_host_pageable_and_pinned_destinations():
+    """fe_step_host with pageable destinations (device buffers, copied after the launch)
+    and with page-locked ones (written by the kernel through their mapped addresses)
+    equals the device-buffer step. After a page-locked step the device observation
+    getters refuse (their buffers were not written) while rewards and state stay
+    readable; a device step makes them readable again."""
+    B, N = 2, 40
+    x0 = synthetic_batch(B, N, seed0=9)
+    u = np.random.RandomState(4).uniform(-1, 1, size=(B, N, 2))
+    ha, hb = nat.FlockHandle(N, B), nat.FlockHandle(N, B)
+    ha.set_state(x0)
+    hb.set_state(x0)
+    ha.step(u, nat.FE_WITH_CONTROLLER)
+    sv = np.empty((B, N, 6), np.float32)
+    net = np.empty((B, N, N), np.float32)
+    rw = np.empty(B)
+    ct = np.empty((B, N, 2))
+    hb.step_host(u.ctypes.data, True, sv.ctypes.data, net.ctypes.data, rw.ctypes.data, ct.ctypes.data)
+    np.testing.assert_array_equal(hb.get_state(), ha.get_state())
+    np.testing.assert_array_equal(sv, ha.state_values())
+    np.testing.assert_array_equal(net, ha.network())
+    np.testing.assert_array_equal(rw, ha.rewards())
+    np.testing.assert_array_equal(ct, ha.controls())
+    np.testing.assert_array_equal(hb.network(), net)  # pageable: the device copy is current
+    # page-locked actions and destinations: read and written in place by the kernel
+    pu = nat.PinnedArray((B, N, 2), np.float64)
+    pu.a[...] = u
+    ps = [nat.PinnedArray(shape, dt) for shape, dt in (((B, N, 6), np.float32), ((B, N, N), np.float32),
+                                                        ((B,), np.float64), ((B, N, 2), np.float64))]
+    ha.step(u, nat.FE_WITH_CONTROLLER)
+    hb.step_host(pu.addr, True, *[p.addr for p in ps])
+    np.testing.assert_array_equal(hb.get_state(), ha.get_state())
+    for p, want in zip(ps, (ha.state_values(), ha.network(), ha.rewards(), ha.controls())):
+        np.testing.assert_array_equal(p.a, want)
+    np.testing.assert_array_equal(hb.rewards(), ha.rewards())
+    with pytest.raises(nat.GymFlockError) as e:
+        hb.network()
+    assert e.value.code == nat.GF_ESTATE
+    hb.step(u, 0)  # a device step makes them readable again
+    ha.step(u, 0)
+    np.testing.assert_array_equal(hb.network(), ha.network())
+    for p in ps + [pu]:
+        p.close()
+    ha.close()
+    hb.close()
+
+
 @pytest.mark.parametrize("n", [7, 10, 63, 100, 130, 1000, 1030, 2049])
 def test_sizes_vs_oracle(n):
     """Ragged N (scalar network path when N % 4 != 0, partial ballot words, several LDS
