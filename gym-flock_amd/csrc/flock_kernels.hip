@@ -24,6 +24,7 @@
 #include <float.h>
 #include <limits.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include <type_traits>
@@ -1071,11 +1072,13 @@ void flock_step_kernel(StepArgs a) {
         // every pair within float32 reach of either threshold (r2 < cr^2 or r2 <= cr):
         // one compare per column, no band sweep; the feature pass decides them exactly.
         // Rows in pairs as the plain step; the rows past nrows sit far away in rxy.
+        // (columns past the tile are masked: at huge coordinates ho is +inf)
         const float ho = uniform_f(fmaxf(ba.hi, bn.hi));
+        const uint64_t vma = __ballot(va), vmb = __ballot(vb);
         auto orow = [&](int r, float2 pr) {
           const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
-          put_lane(wa0, wa1, __ballot(!(d2.x > ho)), r);
-          put_lane(wb0, wb1, __ballot(!(d2.y > ho)), r);
+          put_lane(wa0, wa1, __ballot(!(d2.x > ho)) & vma, r);
+          put_lane(wb0, wb1, __ballot(!(d2.y > ho)) & vmb, r);
         };
         const int nr4 = (nrows + 3) & ~3;
         for (int r = 0; r < nr4; r += 2) {
@@ -1326,9 +1329,9 @@ void flock_step_kernel(StepArgs a) {
   step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
                                       frow && fs == 0, S, tid);
   if constexpr (KN > 0) {
-    if (kgo) {  // Flocking-v0 observation x_i - x_j of this lane's neighbour (flocking.py:24)
-      const St o = state_from_raw<DYN, UF64>(a, kraw);
-      if (fs == KN - 1 && a.knn_r2) {  // the row's k-th nearest r2: candidate radius two steps on
+    // Flocking-v0 observation x_i - x_j of this lane's neighbour(s) (flocking.py:24)
+    auto knn_out = [&](const St& o, int m) {
+      if (m == KN - 1 && a.knn_r2) {  // the row's k-th nearest r2: candidate radius two steps on
         const double dx = me.px - o.px, dy = me.py - o.py;
         a.knn_r2[env0 + i_row] = static_cast<float>(dx * dx + dy * dy);
       }
@@ -1337,8 +1340,9 @@ void flock_step_kernel(StepArgs a) {
       ob.y = static_cast<float>(me.py - o.py);
       ob.z = static_cast<float>(me.vx - o.vx);
       ob.w = static_cast<float>(me.vy - o.vy);
-      if (!GF_ABLATE(a, 0x20000000)) reinterpret_cast<float4*>(a.knn_obs)[(env0 + i_row) * KN + fs] = ob;
-    }
+      if (!GF_ABLATE(a, 0x20000000)) reinterpret_cast<float4*>(a.knn_obs)[(env0 + i_row) * KN + m] = ob;
+    };
+    if (kgo) knn_out(state_from_raw<DYN, UF64>(a, kraw), fs);
     // inline rim: the wave's remaining rows, each scanned by the whole wave over every
     // agent's post-update position (recomputed from x_in and u, bit-identical to the
     // step's), with the rim kernel's ranking and outputs (knn_wave_scan, knn_write_row)
