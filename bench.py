@@ -417,14 +417,41 @@ def bench_greedy(v, targets, R, M, B, K, args):
     v.h.controller_greedy(fetch=False)
     v.sync()
     build = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    for _ in range(K):
+    def loop(step, k):
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        v.sync()
+        return time.perf_counter() - t0
+
+    def separate():
         v.h.controller_greedy(fetch=False)
         v.step(resident=True)
-    v.sync()
-    el = time.perf_counter() - t0
+
+    # the fused form: greedy actions from the per-node greedy lists inside the step launch
+    # (COV_ACTIONS_GREEDY), the default expert step; then the two-launch form beside it
+    state = v.h.robots(0)  # (a sync point: the steps below start from the same batch)
+    loop(lambda: v.step(greedy=True), 20)
+    el = loop(lambda: v.step(greedy=True), K)
+    el_sep = loop(separate, K)
+    # in episodes: reset every 75 steps (the reference's EPISODE_LENGTH), resets untimed,
+    # so most steps see unvisited targets nearby (the long run above is mostly the
+    # all-visited tail, where every robot falls back)
+    ep_t, ep_k = 0.0, 0
+    for e in range(4):
+        v.reset(seed=100 + e)
+        v.sync()
+        ep_t += loop(lambda: v.step(greedy=True), 75)
+        ep_k += 75
+    del state
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
-           "expert_step_ms": 1e3 * el / K, "expert_robot_steps_per_s": R * B * K / el}
+           "expert_step_ms": 1e3 * el / K, "expert_robot_steps_per_s": R * B * K / el,
+           "expert_step_ms_two_launches": 1e3 * el_sep / K,
+           "expert_step_ms_in_episodes": 1e3 * ep_t / ep_k,
+           "note": "expert step = controller(greedy=True) + step for every env; fused: the greedy actions "
+                   "come from per-node greedy lists inside the step's own launch (COV_ACTIONS_GREEDY); "
+                   "two_launches: cov_greedy kernel then the resident step; fallback robots take action 0 "
+                   "(no host round trip)"}
     if not args.no_cpu_baseline:
         from oracle import coverage as oc
         o = oc.CoverageOracle(targets, R, M)

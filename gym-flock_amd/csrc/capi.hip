@@ -4,7 +4,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <atomic>
 #include <deque>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -287,14 +289,28 @@ int dalloc(T** p, size_t count) {
 // Tear down the metrics path: the communicator (aborted when a collective may never
 // complete, else destroyed once the side stream has drained) and everything fe_comm_init
 // made for it, so that a later fe_comm_init starts from scratch.
+//
+// abort: a collective (or the initialisation) may never finish because a peer is gone.
+// The communicator is then aborted on a detached thread, and its side stream, events and
+// buffers are abandoned rather than synchronised or freed (a kernel of the aborted
+// collective may still touch them), so that this call cannot hang; the step streams never
+// wait on the side stream's collectives (only on its staging copies, which complete).
 void comm_release(fe_handle* h, bool abort) {
-  if (h->comm) {
-    if (abort) {
-      ncclCommAbort(h->comm);  // a collective stuck on a missing peer exits
-    } else {
-      if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
-      ncclCommDestroy(h->comm);
+  if (abort) {
+    if (h->comm) {
+      ncclComm_t c = h->comm;
+      std::thread([c] { ncclCommAbort(c); }).detach();
     }
+    h->comm = nullptr;
+    h->comm_stream = nullptr;
+    h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = nullptr;
+    h->ring_reads.clear();
+    h->ev_free.clear();
+    h->gsend = h->gather = h->ssend = h->stats_gather = nullptr;
+  }
+  if (h->comm) {
+    if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
+    ncclCommDestroy(h->comm);
     h->comm = nullptr;
   }
   if (h->comm_stream) {
@@ -957,7 +973,13 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
   h->has_obs = true;
   h->obs_on_host = sv_m || net_m;
   h->has_knn = false;
-  GF_HIP(hipStreamSynchronize(h->stream));
+  // spin on the stream: the drop-in step is latency-bound (tens of us), and a blocking
+  // wait's wake-up costs a sizeable part of that
+  for (;;) {
+    const hipError_t q = hipStreamQuery(h->stream);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return fail_hip("fe_step_host", q);
+  }
   return GF_OK;
 }
 
@@ -1486,9 +1508,34 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
   h->comm_timeout = timeout_s;
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
-  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
-  config.blocking = 0;
-  const ncclResult_t r = ncclCommInitRankConfig(&h->comm, nranks, uid, rank, &config);
+  // RCCL's non-blocking init still connects to the bootstrap root inside the call, which
+  // waits for every rank: with a rank missing it never returns. The call therefore runs
+  // on a thread of its own; past the deadline it is left behind (with whatever it
+  // creates) and this rank fails with GF_ECOMM, its handle still usable.
+  struct InitJob {
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclInProgress;
+    std::atomic<bool> done{false};
+  };
+  auto job = std::make_shared<InitJob>();
+  const int dev = h->cfg.device;
+  std::thread([job, nranks, uid, rank, dev]() {
+    hipSetDevice(dev);
+    ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+    config.blocking = 0;
+    ncclComm_t c = nullptr;
+    const ncclResult_t rr = ncclCommInitRankConfig(&c, nranks, uid, rank, &config);
+    job->comm = c;
+    job->r = rr;
+    job->done.store(true, std::memory_order_release);
+  }).detach();
+  while (!job->done.load(std::memory_order_acquire)) {
+    if (Clock::now() > deadline)
+      return fail(GF_ECOMM, "ncclCommInitRankConfig: timed out (a rank did not join); the initialisation is left behind");
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  h->comm = job->comm;
+  const ncclResult_t r = job->r;
   if (r != ncclSuccess && r != ncclInProgress) {
     comm_release(h, true);
     return fail(GF_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));

@@ -68,6 +68,9 @@ struct cov_handle {
   uint8_t* tm_wide = nullptr;    // (B) 1: the env's matrix needed uint16 entries
   std::vector<uint8_t> tm_wide_host;
   int16_t* tm_prevT = nullptr;
+  uint16_t* tm_glist = nullptr;  // greedy lists (B,Tmax,gstride), Tmax <= kGreedyListMaxT
+  uint16_t* tm_glen = nullptr;   // (B,Tmax)
+  int gstride = 0;
   uint8_t* tm_flags = nullptr;
   uint8_t* needs_random = nullptr;
   int32_t* tm_envsel = nullptr;
@@ -77,6 +80,7 @@ struct cov_handle {
   uint8_t* tm_overflow = nullptr;
   std::vector<int> n_motion_host;
   std::vector<char> tm_valid;
+  bool tm_ready = false;           // every env's time matrix (and greedy lists) is current
   int64_t tm_wide_envs = 0;  // envs whose matrix needed uint16 entries (diagnostics)
   // wire formats: scratch for host-bound outputs, graph-tuple offsets
   unsigned char* scratch = nullptr;
@@ -119,7 +123,7 @@ void cov_release(cov_handle* h) {
   gf::CovArgs& a = h->a;
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
-                  a.receivers, a.obs_step, a.axy, a.nrec, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT,
+                  a.receivers, a.obs_step, a.axy, a.nrec, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT, h->tm_glist, h->tm_glen,
                   h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
                   h->goff};
   for (void* p : bufs)
@@ -169,6 +173,11 @@ int ensure_time_matrix(cov_handle* h) {
         (rc = calloc_dev(&h->tm_nlev, (size_t)B)) || (rc = calloc_dev(&h->tm_overflow, (size_t)B)) ||
         (rc = calloc_dev(&h->tm_cost8, (size_t)B * Tm * Tm)) || (rc = calloc_dev(&h->tm_wide, (size_t)B)))
       return rc;
+    if (Tm <= gf::kGreedyListMaxT) {  // rows padded to 16 bytes (greedy_from_list's loads)
+      h->gstride = (Tm + 7) & ~7;
+      if ((rc = calloc_dev(&h->tm_glist, (size_t)B * Tm * h->gstride)) || (rc = calloc_dev(&h->tm_glen, (size_t)B * Tm)))
+        return rc;
+    }
     h->tm_wide_host.assign(B, 0);
   }
   std::vector<int32_t> sel;
@@ -179,7 +188,10 @@ int ensure_time_matrix(cov_handle* h) {
     t_lds = std::max(t_lds, h->ntg_host[b]);
     e_max = std::max(e_max, h->n_motion_host[b]);
   }
-  if (sel.empty()) return GF_OK;
+  if (sel.empty()) {
+    h->tm_ready = true;
+    return GF_OK;
+  }
   if (gf::cov_time_matrix_lds_bytes(t_lds, false) > 160 * 1024 ||
       gf::cov_tm_schedule_lds_bytes(t_lds, e_max) > 160 * 1024)
     return cfail(GF_EINVAL, "time matrix: (n_targets + 1) * 64 bytes exceed the 160 KB LDS of a CU");
@@ -235,8 +247,20 @@ int ensure_time_matrix(cov_handle* h) {
   for (int b : sel) h->tm_wide_host[b] = 0;
   for (int b : wide) h->tm_wide_host[b] = 1;
   CV_HIP(hipMemcpyAsync(h->tm_wide, h->tm_wide_host.data(), B, hipMemcpyHostToDevice, h->stream));
+  if (h->tm_glist) {  // every selected env's greedy lists, from its final matrix
+    t.wide = h->tm_wide;
+    t.nbr = h->a.nbr;
+    t.cnt = h->a.cnt;
+    t.glist = h->tm_glist;
+    t.glen = h->tm_glen;
+    t.gstride = h->gstride;
+    CV_HIP(hipMemcpyAsync(h->tm_envsel, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+    e = gf::launch_cov_greedy_lists(t, (int)sel.size(), h->stream);
+    if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_greedy_list_kernel: ") + hipGetErrorString(e));
+  }
   CV_HIP(hipStreamSynchronize(h->stream));
   for (int b : sel) h->tm_valid[b] = 1;
+  h->tm_ready = true;
   return GF_OK;
 }
 
@@ -358,6 +382,7 @@ int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets
   if (int rc = check_err(h)) return rc;
   CV_HIP(hipMemcpy(h->n_motion_host.data(), h->a.n_motion, B * sizeof(int32_t), hipMemcpyDeviceToHost));
   for (int b = b0; b < b1; ++b) h->tm_valid[b] = 0;
+  h->tm_ready = false;
   h->has_graph = true;
   for (int b = 0; b < B; ++b) h->has_graph = h->has_graph && h->ntg_host[b] > 0;
   return GF_OK;
@@ -398,7 +423,23 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
   if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
   CV_HIP(hipSetDevice(h->cfg.device));
   gf::CovArgs a = h->a;
-  if (flags & COV_ACTIONS_DEVICE) {
+  if (flags & COV_ACTIONS_GREEDY) {
+    // controller(greedy=True) in the step's own launch, from the greedy lists
+    if (!h->tm_ready || !h->tm_glist) {
+      if (int rc = use(h)) return rc;
+      if (int rc = ensure_time_matrix(h)) return rc;
+    }
+    if (!h->tm_glist) {  // Tmax > kGreedyListMaxT: the row-scan greedy kernel, then the step
+      if (int rc = cov_controller_greedy(h, nullptr, nullptr, nullptr)) return rc;
+      return cov_step(h, nullptr, COV_ACTIONS_RESIDENT);
+    }
+    a.actions = nullptr;
+    a.glist = h->tm_glist;
+    a.glen = h->tm_glen;
+    a.gstride = h->gstride;
+    a.gactions = h->actions;
+    a.needs_random = h->needs_random;
+  } else if (flags & COV_ACTIONS_DEVICE) {
     if (!actions) return cfail(GF_EINVAL, "null action pointer");
     a.actions = actions;
   } else if (flags & COV_ACTIONS_RESIDENT) {
@@ -430,7 +471,8 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
     h->s2_pending = true;
     if (h->timing) h->tw_steps++;
-    if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT))) CV_HIP(hipStreamSynchronize(h->stream));
+    if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT | COV_ACTIONS_GREEDY)))
+      CV_HIP(hipStreamSynchronize(h->stream));
     return GF_OK;
   }
   if (int rc = join_s2(h)) return rc;
@@ -453,7 +495,8 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     CV_HIP(hipEventRecord(h->ev[h->ev_used + 1], h->stream));
     h->ev_used += 2;
   }
-  if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT))) CV_HIP(hipStreamSynchronize(h->stream));
+  if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT | COV_ACTIONS_GREEDY)))
+    CV_HIP(hipStreamSynchronize(h->stream));
   return GF_OK;
 }
 
@@ -589,6 +632,9 @@ int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random
   g.actions = h->actions;
   g.needs_random = h->needs_random;
   g.err = h->err;
+  g.glist = h->tm_glist;
+  g.glen = h->tm_glen;
+  g.gstride = h->gstride;
   hipError_t e = gf::launch_cov_greedy(g, h->stream);
   if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_greedy_kernel: ") + hipGetErrorString(e));
   if (!actions && !needs_random && !n_random) return GF_OK;
@@ -608,6 +654,22 @@ int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random
     *n_random = cnt;
   }
   return check_err(h);
+}
+
+int cov_get_actions(cov_handle* h, int32_t* actions, uint8_t* needs_random) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (int rc = use(h)) return rc;
+  const size_t n = (size_t)h->cfg.n_envs * h->cfg.n_robots;
+  if (int rc = copy_out(h, actions, h->actions, n * 4)) return rc;
+  if (needs_random) {
+    if (h->needs_random) {
+      if (int rc = copy_out(h, needs_random, h->needs_random, n)) return rc;
+    } else {
+      std::memset(needs_random, 0, n);
+    }
+  }
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
 }
 
 int cov_get_time_matrix(cov_handle* h, int env, int32_t* cost, int32_t* prev) {

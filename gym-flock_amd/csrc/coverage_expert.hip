@@ -455,7 +455,139 @@ hipError_t launch_cov_time_matrix(const CovTmArgs& a, int n_envs_sel, bool wide,
   return wide ? launch_tm_passes<uint16_t>(a, n_envs_sel, s) : launch_tm_passes<uint8_t>(a, n_envs_sel, s);
 }
 
+
+namespace {
+
+// One wave per source node c of a selected env: its greedy list (coverage_internal.h).
+// The row's hop counts and entries sit in registers (Tmax <= 1024: 16 per lane); the
+// distinct counts are visited in ascending order and each count's targets are appended
+// in t order by ballot, which is np.argmin's (min value, then first index) order.
+constexpr int kListChunks = kGreedyListMaxT / 64;
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void cov_greedy_list_kernel(CovTmArgs a) {
+  const int b = a.envs[blockIdx.x];
+  const int c = blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int T = a.ntg[b], Tm = a.Tmax;
+  if (c >= T) return;  // wave-uniform
+  const size_t row = (size_t)b * Tm + c;
+  const uint16_t* cost = a.cost + row * Tm;
+  const int16_t* prev = a.prevT + row * Tm;  // graph_previous[t, c] at t
+  const int32_t* nb = a.nbr + row * 4;
+  const int n = a.cnt[row];
+  const int nb0 = nb[0], nb1 = nb[1], nb2 = nb[2], nb3 = nb[3];
+  uint32_t vv[kListChunks], ee[kListChunks];
+#pragma unroll
+  for (int k = 0; k < kListChunks; ++k) {
+    const int t = 64 * k + lane;
+    vv[k] = 0xFFFFu;
+    ee[k] = 0;
+    if (t < T) {
+      const uint32_t v = cost[t];
+      if (v != kInf && v < (uint32_t)kMaxCost) vv[k] = v;  // inf -> MAX_COST: never argmin-chosen
+      const int p = prev[t];
+      uint32_t flag = 0, act = 0;
+      if (p < 0) {
+        flag = kGreedyRnd;  // :863
+      } else {  // the first of the node's action targets equal to the next hop (:869)
+        act = (n > 3 && nb3 == p) ? 3u : 4u;
+        act = (n > 2 && nb2 == p) ? 2u : act;
+        act = (n > 1 && nb1 == p) ? 1u : act;
+        act = (n > 0 && nb0 == p) ? 0u : act;
+        if (act == 4u) {
+          flag = kGreedyErr;
+          act = 0;
+        }
+      }
+      ee[k] = (uint32_t)t | act << 10 | flag << 12;
+    }
+  }
+  uint16_t* out = a.glist + row * a.gstride;
+  int len = 0;
+  uint32_t lo = 0xFFFFu;
+#pragma unroll
+  for (int k = 0; k < kListChunks; ++k) lo = min(lo, vv[k]);
+  uint32_t v = wave_min_u32(lo);
+  while (v != 0xFFFFu) {
+    uint32_t nxt = 0xFFFFu;
+#pragma unroll
+    for (int k = 0; k < kListChunks; ++k) {
+      if (64 * k < T) {  // wave-uniform
+        const bool hit = vv[k] == v;
+        const uint64_t m = __ballot(hit);
+        if (hit)
+          out[len + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
+              (uint16_t)ee[k];
+        len += __popcll(m);
+        if (vv[k] > v) nxt = min(nxt, vv[k]);
+      }
+    }
+    v = wave_min_u32(nxt);
+  }
+  if (lane == 0) a.glen[row] = (uint16_t)len;
+}
+
+// controller(greedy=True) from the greedy lists: one workgroup per env, one thread per
+// robot; the env's visited flags staged in LDS as bits.
+__global__ __launch_bounds__(256) void cov_greedy_list_step_kernel(CovGreedyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* vbits = reinterpret_cast<uint32_t*>(smem);
+  const int b = blockIdx.x;
+  const int R = a.R, Tm = a.Tmax;
+  const int T = a.ntg[b];
+  const uint8_t* vis = a.visited + (size_t)b * Tm;
+  for (int w = threadIdx.x; w < (Tm + 31) / 32; w += 256) vbits[w] = 0u;
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += 256)
+    if (vis[t]) atomicOr(&vbits[t >> 5], 1u << (t & 31));
+  __syncthreads();
+  const bool any_vis = a.nvisited[b] > 0;
+  const bool dirty = a.dirty[b] != 0;
+  for (int i = threadIdx.x; i < R; i += 256) {
+    int c;
+    if (dirty) {  // robots were placed externally: closest_targets (:427-432)
+      const double* tg = a.tgt + (size_t)b * Tm * 2;
+      const double px = a.xr[((size_t)b * R + i) * 2], py = a.xr[((size_t)b * R + i) * 2 + 1];
+      double best = __builtin_inf();
+      c = 0;
+      for (int t = 0; t < T; ++t) {
+        const double dx = px - tg[2 * t], dy = py - tg[2 * t + 1];
+        const double d = sqrt(dx * dx + dy * dy);
+        if (d < best) {
+          best = d;
+          c = t;
+        }
+      }
+    } else {
+      c = a.cur[(size_t)b * R + i] - R;
+    }
+    const size_t row = (size_t)b * Tm + c;
+    const int g = greedy_from_list(a.glist + row * a.gstride, a.glen[row], vbits, any_vis, a.nvisited[b] >= T);
+    const uint32_t flag = (uint32_t)g >> 2;
+    if (flag & kGreedyErr) atomicOr(a.err, 8);
+    a.actions[(size_t)b * R + i] = (flag & kGreedyRnd) ? 0 : (g & 3);
+    a.needs_random[(size_t)b * R + i] = (flag & kGreedyRnd) ? 1 : 0;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_cov_greedy_lists(const CovTmArgs& a, int n_envs_sel, hipStream_t s) {
+  hipLaunchKernelGGL(cov_greedy_list_kernel, dim3(n_envs_sel, (a.Tmax + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s) {
+  if (a.glist) {
+    hipLaunchKernelGGL(cov_greedy_list_step_kernel, dim3(a.B), dim3(256), ((a.Tmax + 31) / 32) * 4, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(cov_greedy_kernel, dim3(a.B, (a.R + kGreedyRobotsPerBlock - 1) / kGreedyRobotsPerBlock),
                      dim3(256), 0, s, a);
   return hipGetLastError();

@@ -35,7 +35,48 @@ struct CovArgs {
                           // with itself; int4), the 4 action-edge features of a robot on it
                           // (float4), its position (double2), 16 B pad
   int* err;               // device error bits: 1 degree > 4, 2 edges overflow, 4 bad action
+  // fused greedy expert (cov_step with COV_ACTIONS_GREEDY): the step's actions are
+  // controller(greedy=True)'s, taken from each node's greedy list (below)
+  const uint16_t* glist;  // (B,Tmax,gstride) or nullptr: actions come from `actions`
+  const uint16_t* glen;   // (B,Tmax)
+  int gstride;
+  int32_t* gactions;      // (B,R) the greedy actions taken (written)
+  uint8_t* needs_random;  // (B,R) robots the reference hands to np_random.choice (action 0 here)
 };
+
+// Greedy lists (built with the time matrix, cov_greedy_list_kernel): for every source
+// node c of an env, the targets t with a finite hop count cost[c][t] < MAX_COST, in
+// (cost, t) order, i.e. the order of controller(greedy=True)'s np.argmin over the
+// masked row (coverage.py:817-819). Entry = t | action << 10 | flag << 12: the index of
+// the first hop (graph_previous[t, c], :863-869) among the node's action targets, flag
+// 1 when the predecessor is -1 (the reference draws a random action), 2 when it is not
+// among them (the reference raises IndexError). Needs Tmax <= 1024.
+constexpr int kGreedyListMaxT = 1024;
+constexpr uint32_t kGreedyRnd = 1, kGreedyErr = 2;
+
+// The greedy action of a robot on target-local node c from its list row: the first
+// entry whose target is unvisited (and is not target 0 once anything is visited: the
+// reference masks visited targets through np.where on its (N,1) visited column, which
+// also hits column 0). vbits: the env's visited flags as bits (LDS). Returns
+// action | flag << 2; flag kGreedyRnd also when every listed target is masked (at once
+// when the env has no unvisited target left: nv == T).
+__device__ __forceinline__ int greedy_from_list(const uint16_t* row, int len, const uint32_t* vbits, bool any_vis,
+                                                bool none_left) {
+  if (none_left) len = 0;
+  for (int k0 = 0; k0 < len; k0 += 8) {
+    const uint4 q = *reinterpret_cast<const uint4*>(row + k0);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (k0 + j >= len) break;
+      const uint32_t e = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      const int t = static_cast<int>(e & 1023u);
+      const bool masked = ((vbits[t >> 5] >> (t & 31)) & 1u) || (t == 0 && any_vis);
+      if (!masked) return static_cast<int>(e >> 10);
+    }
+  }
+  return static_cast<int>(kGreedyRnd << 2);
+}
 
 // Greedy expert (coverage_expert.hip).
 struct CovTmArgs {
@@ -58,6 +99,13 @@ struct CovTmArgs {
   int32_t* nlev;             // (B) schedule levels
   uint8_t* overflow;         // (B) the uint8 pass could not bound an entry: rerun wide
   int sched_stride;
+  // greedy lists (cov_greedy_list_kernel), when Tmax <= kGreedyListMaxT
+  const uint8_t* wide;       // (B) which cost form holds the env's matrix
+  const int32_t* nbr;        // (B,Tmax,4)
+  const int32_t* cnt;        // (B,Tmax)
+  uint16_t* glist;           // (B,Tmax,gstride)
+  uint16_t* glen;            // (B,Tmax)
+  int gstride;
 };
 
 struct CovGreedyArgs {
@@ -78,6 +126,9 @@ struct CovGreedyArgs {
   int32_t* actions;        // (B,R)
   uint8_t* needs_random;   // (B,R)
   int* err;                // 8: next hop not among the robot's actions
+  const uint16_t* glist;   // greedy lists (or nullptr: scan the cost rows)
+  const uint16_t* glen;
+  int gstride;
 };
 
 size_t cov_time_matrix_lds_bytes(int t_lds, bool wide);
@@ -87,6 +138,8 @@ hipError_t launch_cov_tm_schedule(const CovTmArgs& a, int n_envs_sel, int e_max,
 // overflow[b] for envs it cannot bound).
 hipError_t launch_cov_time_matrix(const CovTmArgs& a, int n_envs_sel, bool wide, hipStream_t s);
 hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s);
+// the greedy lists of the selected envs (after their time matrices)
+hipError_t launch_cov_greedy_lists(const CovTmArgs& a, int n_envs_sel, hipStream_t s);
 
 size_t cov_step_lds_bytes(int R, int M);
 // Observation wire formats: the flat FlattenDictWrapper rows (B, 15M+1) and the

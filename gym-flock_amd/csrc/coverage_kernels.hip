@@ -177,6 +177,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
   unsigned* seen = claim + (M + 31) / 32;                      // visited-this-step bits
   int* counter = reinterpret_cast<int*>(seen + (M + 31) / 32);
   int* first = counter + 4;                                    // M: first claimer of each node
+  uint32_t* gvis = reinterpret_cast<uint32_t*>(first + M);     // greedy: visited bits, 64 per 2 words
   const int W = (M + 31) / 32;
   const int tid = threadIdx.x;
   const double* tg = a.tgt + (size_t)b * Tm * 2;
@@ -195,11 +196,14 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     claim[k] = 0u;
     seen[k] = 0u;
   }
-  if (a.actions)
+  if (a.actions || a.glist)
     for (int k = tid; k < M; k += NT) first[k] = INT_MAX;
   if (tid == 0) *counter = 0;
   GF_COV_STAMP(0);
   const int32_t* act = a.actions ? a.actions + (size_t)b * R : nullptr;
+  // COV_ACTIONS_GREEDY: controller(greedy=True) picks each robot's action in this launch
+  const bool greedy = a.glist != nullptr;
+  const bool has_act = act || greedy;
   // One robot per thread (R <= NT): the data of the node a robot will end on
   // (if it moves: the chosen node; in a full pass: its node) is loaded right after the
   // chosen node is known, so that round trip runs under the claim resolution.
@@ -235,7 +239,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     Ld l;
     l.c = cur[i];
     l.ai = act ? act[i] : 0;
-    l.offer = act ? *reinterpret_cast<const int4*>(snd + base + 4 * i) : make_int4(0, 0, 0, 0);
+    l.offer = has_act ? *reinterpret_cast<const int4*>(snd + base + 4 * i) : make_int4(0, 0, 0, 0);
     return l;
   };
   Ld ld[RPT];  // R <= kCovThreads: every slot's loads issued first, before the env's words
@@ -247,7 +251,22 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
   // the env's words, loaded up front so none of them costs a round trip of its own
   const bool dirty = a.dirty[b] != 0;
   const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
-  const bool full = dirty || !a.actions;  // recompute every robot's action edges
+  const bool full = dirty || !has_act;  // recompute every robot's action edges
+  const bool any_vis = nv0 > 0;
+  if (greedy) {
+    // the env's visited flags as bits, before this step marks any (ballots, no atomics),
+    // read after the robots' loads are in flight
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int t0 = wv * 64; t0 < Tm; t0 += NT) {
+      const int t = t0 + lane;
+      const uint64_t m = __ballot(t < T && vis[t]);
+      if (lane == 0) {
+        gvis[t0 >> 5] = static_cast<uint32_t>(m);
+        gvis[(t0 >> 5) + 1] = static_cast<uint32_t>(m >> 32);
+      }
+    }
+    __syncthreads();
+  }
   // robot i: its node c and the node n its action points at (claiming c if n == c)
   auto pick = [&](int i, const Ld& l, int& c) {
     c = l.c;
@@ -269,7 +288,16 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     }
     cur_s[i] = c;
     int n = c;
-    if (act) {
+    if (greedy) {  // :814-869 from the node's greedy list; fallbacks take action 0 here
+      const size_t row = (size_t)b * Tm + (c - R);
+      const int g = greedy_from_list(a.glist + row * a.gstride, a.glen[row], gvis, any_vis, nv0 >= T);
+      const uint32_t flag = static_cast<uint32_t>(g) >> 2;
+      if (flag & kGreedyErr) atomicOr(a.err, 8);
+      ai = (flag & kGreedyRnd) ? 0 : (g & 3);
+      a.gactions[(size_t)b * R + i] = ai;
+      a.needs_random[(size_t)b * R + i] = (flag & kGreedyRnd) ? 1 : 0;
+    }
+    if (has_act) {
       // step (:184-200): the node the action points at; robots that stay claim first
       if (ai < 0 || ai >= 4) {
         atomicOr(a.err, 4);
@@ -313,7 +341,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
   __syncthreads();
   GF_COV_STAMP(1);
 
-  if (act) {
+  if (has_act) {
     // then, in robot order, a move succeeds unless its node is already claimed; a
     // blocked robot stays and its node joins the claims. The reference walks the robots
     // serially; here every robot's outcome is re-evaluated in parallel from the current
@@ -609,7 +637,7 @@ hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all
 }
 
 size_t cov_step_lds_bytes(int R, int M) {
-  return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16 + (size_t)M * 4;
+  return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16 + (size_t)M * 4 + (size_t)((M - R + 63) / 64) * 8;
 }
 
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {

@@ -60,6 +60,7 @@ class CovConfig(ctypes.Structure):
 
 COV_ACTIONS_DEVICE = 0x1
 COV_ACTIONS_RESIDENT = 0x2
+COV_ACTIONS_GREEDY = 0x20
 COV_OUT_DEVICE = 0x4
 COV_FLAT_F32 = 0x8
 COV_MASK_ALL = 0x10
@@ -135,6 +136,7 @@ SIGNATURES = {
     "cov_set_streams": [_P, _I],
     "cov_controller_greedy": [_P, _P, _P, _P],
     "cov_get_time_matrix": [_P, _I, _P, _P],
+    "cov_get_actions": [_P, _P, _P],
     "cov_get_flat_obs": [_P, _P, _I],
     "cov_graphs_tuple_sizes": [_P, _P, _P, _I],
     "cov_get_graphs_tuple": [_P, _P, _P, _P, _P, _P, _P, _P, _I],
@@ -204,29 +206,32 @@ class HostPool:
         import collections
         import threading
         self.cap = int(cap_bytes)
-        self._live = 0  # page-locked bytes handed out and not yet drained back
+        self._live = 0  # page-locked bytes handed out and not yet reclaimed
         self.free = {}
         self.lock = threading.Lock()
-        # released buffers, queued without a lock: _release runs from weakref finalizers,
-        # which the cyclic GC may fire inside any allocation, including one made while
-        # self.lock is held by this very thread (deque.append is atomic)
-        self.released = collections.deque()
+        # buffers handed out, oldest first, as (weak reference to the ctypes buffer every
+        # array and view of it keeps alive, address, bytes). A buffer is reclaimed once its
+        # reference is dead; each allocation looks at a few of the oldest entries (a step's
+        # arrays are usually released within a step or two). No finalizer callbacks: they
+        # cost more than the step's own launch overhead and can fire inside any allocation.
+        self.out = collections.deque()
 
-    def _drain(self):
-        # caller holds self.lock
-        while True:
-            try:
-                p, nbytes = self.released.popleft()
-            except IndexError:
-                return
-            self._live -= nbytes
-            self.free.setdefault(nbytes, []).append(p)
+    def _reclaim(self, budget):
+        # caller holds self.lock; checks at most `budget` of the oldest entries (all: -1)
+        n = len(self.out) if budget < 0 else min(budget, len(self.out))
+        for _ in range(n):
+            ref, p, nbytes = self.out.popleft()
+            if ref() is None:
+                self._live -= nbytes
+                self.free.setdefault(nbytes, []).append(p)
+            else:
+                self.out.append((ref, p, nbytes))
 
     @property
     def live(self):
-        """Page-locked bytes held by live arrays (released ones are drained first)."""
+        """Page-locked bytes held by live arrays (every released one reclaimed first)."""
         with self.lock:
-            self._drain()
+            self._reclaim(-1)
             return self._live
 
     def array(self, shape, dtype):
@@ -241,8 +246,11 @@ class HostPool:
         if nbytes == 0:
             return np.empty(shape, dtype), None
         with self.lock:
-            self._drain()
+            self._reclaim(4)
             lst = self.free.get(nbytes)
+            if not lst:
+                self._reclaim(-1)
+                lst = self.free.get(nbytes)
             p = lst.pop() if lst else None
             if p is None and self._live + nbytes > self.cap:
                 return np.empty(shape, dtype), None
@@ -257,17 +265,14 @@ class HostPool:
                 return np.empty(shape, dtype), None
             p = out.value
         buf = (ctypes.c_uint8 * nbytes).from_address(p)
-        fin = weakref.finalize(buf, self._release, p, nbytes)
-        fin.atexit = False  # the process's exit frees page-locked memory
+        with self.lock:
+            self.out.append((weakref.ref(buf), p, nbytes))
         return np.frombuffer(buf, dtype=dtype).reshape(shape), p
-
-    def _release(self, p, nbytes):
-        self.released.append((p, nbytes))  # no lock, no allocation beyond the tuple
 
     def trim(self):
         """Free the recycled (unused) buffers."""
         with self.lock:
-            self._drain()
+            self._reclaim(-1)
             ps = [p for lst in self.free.values() for p in lst]
             self.free = {}
         for p in ps:
@@ -310,7 +315,10 @@ class PinnedArray:
 def u_is_f64(u):
     """Whether the reference's `u * action_scalar` (flocking_relative.py:95) computes in
     float64 for this action array (NumPy's promotion: float32/float16 stay float32)."""
-    return np.result_type(u.dtype, 10.0) != np.float32
+    d = u.dtype
+    if d == np.float32 or d == np.float16:
+        return False
+    return d == np.float64 or np.result_type(d, 10.0) != np.float32
 
 
 def check_shard_sizes(n_envs):
@@ -628,8 +636,10 @@ class CoverageHandle:
         h = ctypes.c_void_p()
         check(self.lib.cov_create(ctypes.byref(self.cfg), ctypes.byref(h)))
         self.h = h
-        # the resident-action step with its arguments bound: a step is ~7 us, host-bound
+        # the resident-action and fused greedy steps with their arguments bound: a step is
+        # ~7 us, host-bound
         self._step_resident = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_RESIDENT)
+        self._step_greedy = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_GREEDY)
 
     def close(self):
         h = getattr(self, "h", None)
@@ -664,9 +674,12 @@ class CoverageHandle:
         assert vi.shape == (self.n_envs, self.t_max), vi.shape
         check(self.lib.cov_reset(self.h, ptr(st), ptr(vi)))
 
-    def step(self, actions=None, resident=False):
-        if resident:
-            rc = self._step_resident()
+    def step(self, actions=None, resident=False, greedy=False):
+        """actions (B,R) host ints; or resident=True (the last set/greedy actions); or
+        greedy=True: controller(greedy=True)'s actions computed inside the step's launch
+        (fallback robots take action 0, needs_random flags them)."""
+        if resident or greedy:
+            rc = self._step_greedy() if greedy else self._step_resident()
             if rc:
                 check(rc)
             return
@@ -676,6 +689,14 @@ class CoverageHandle:
     def set_actions(self, actions):
         a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
         check(self.lib.cov_set_actions(self.h, ptr(a)))
+
+    def actions(self):
+        """(resident actions (B,R) int32, needs_random (B,R) bool) of the last greedy call or
+        set_actions."""
+        a = np.empty((self.n_envs, self.n_robots), np.int32)
+        r = np.empty((self.n_envs, self.n_robots), np.uint8)
+        check(self.lib.cov_get_actions(self.h, ptr(a), ptr(r)))
+        return a, r.astype(bool)
 
     def set_robot_positions(self, env, xr):
         x = np.ascontiguousarray(xr, dtype=np.float64)

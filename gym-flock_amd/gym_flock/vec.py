@@ -169,13 +169,16 @@ class VecCoverage:
         self.h.reset(start, visited)
         return start, visited
 
-    def step(self, actions=None, resident=False):
-        if resident:
-            rc = self.h._step_resident()
+    def step(self, actions=None, resident=False, greedy=False):
+        """actions (B,R); or resident=True (the last set/greedy actions); or greedy=True
+        (the greedy expert's actions computed in the step's own launch; fallback robots
+        take action 0, see include/gymflock.h COV_ACTIONS_GREEDY)."""
+        if resident or greedy:
+            rc = self.h._step_greedy() if greedy else self.h._step_resident()
             if rc:
                 nat.check(rc)
             return
-        self.h.step(actions, resident)
+        self.h.step(actions)
 
     def set_actions(self, actions):
         self.h.set_actions(actions)

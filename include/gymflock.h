@@ -261,6 +261,12 @@ typedef struct cov_handle cov_handle;
 
 #define COV_ACTIONS_DEVICE   0x1 /* actions is a device pointer                          */
 #define COV_ACTIONS_RESIDENT 0x2 /* use the actions last given to cov_set_actions        */
+#define COV_ACTIONS_GREEDY   0x20 /* the step's actions are controller(greedy=True)'s (:800-872),
+                                    computed in the same launch from per-node greedy lists
+                                    built with the time matrix; robots the reference hands to
+                                    np_random.choice(4) take action 0 (needs_random flags them:
+                                    for the reference's draws use cov_controller_greedy). The
+                                    actions taken stay resident (COV_ACTIONS_RESIDENT). */
 
 int cov_create(const cov_config* cfg, cov_handle** out);        /* CoverageEnv.__init__ :83 */
 int cov_destroy(cov_handle* h);
@@ -297,6 +303,10 @@ int cov_set_streams(cov_handle* h, int n);
  * the patched array with cov_set_actions. actions[B][R], needs_random[B][R] and
  * n_random may be NULL; with all three NULL the call does not synchronise. */
 int cov_controller_greedy(cov_handle* h, int32_t* actions, uint8_t* needs_random, int64_t* n_random);
+/* The resident actions (B,R) (the last cov_set_actions, cov_controller_greedy or
+ * COV_ACTIONS_GREEDY step) and the needs_random flags (B,R) of the last greedy call;
+ * either pointer may be NULL. */
+int cov_get_actions(cov_handle* h, int32_t* actions, uint8_t* needs_random);
 /* One env's graph_cost (inf -> MAX_COST=1000, as :651) and graph_previous, each
  * (T,T) row-major, T = that env's target count; builds the matrix if needed. */
 int cov_get_time_matrix(cov_handle* h, int env, int32_t* cost, int32_t* prev);

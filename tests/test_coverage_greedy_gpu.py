@@ -224,3 +224,69 @@ def test_mixed_width_batch_greedy_vs_oracle():
         v.set_targets(maps[b], env=b)
     _greedy_phase(v, maps, R, M, seed=5, steps=15)
     v.close()
+
+
+def test_fused_greedy_step_equals_separate():
+    """cov_step(COV_ACTIONS_GREEDY): the greedy actions computed inside the step's launch
+    from the per-node greedy lists, against controller_greedy (its own kernel) followed
+    by a resident step, fallback robots taking action 0 in both. A batch of different
+    maps over a whole episode (robots placed off-node in one env at step 10): the actions
+    taken, needs_random, robots, rewards and observations are equal at every step."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, R, M = 4, 20, 800
+    maps = []
+    for b in range(B):
+        np.random.seed(700 + b)
+        maps.append(generate_targets())
+    va, vb = VecCoverage(B, R, max_nodes=M), VecCoverage(B, R, max_nodes=M)
+    for v in (va, vb):
+        for b in range(B):
+            v.set_targets(maps[b], env=b)
+        v.reset(seed=21)
+    n_rand = 0
+    for t in range(75):
+        if t == 10:
+            xr = va.h.robots(1)[0] + np.random.RandomState(8).uniform(-2.0, 2.0, size=(R, 2))
+            va.h.set_robot_positions(1, xr)
+            vb.h.set_robot_positions(1, xr)
+        ea, er = va.h.controller_greedy()
+        va.step(resident=True)
+        vb.step(greedy=True)
+        ga, gr = vb.h.actions()
+        np.testing.assert_array_equal(ga, ea)
+        np.testing.assert_array_equal(gr, er)
+        n_rand += int(er.sum())
+        ra, da = va.rewards()
+        rb, db = vb.rewards()
+        np.testing.assert_array_equal(ra, rb)
+        np.testing.assert_array_equal(da, db)
+        for b in range(B):
+            np.testing.assert_array_equal(va.h.robots(b)[1], vb.h.robots(b)[1])
+        if t % 15 == 0:
+            oa, ob = va.obs(t % B), vb.obs(t % B)
+            for k in oa:
+                np.testing.assert_array_equal(oa[k], ob[k])
+    print("fallback robots over the episode:", n_rand)
+    va.close()
+    vb.close()
+
+
+def test_fused_greedy_step_vs_oracle():
+    """The fused greedy step against the oracle's greedy actions (fallbacks as action 0)
+    on the recorded r20 map, 30 steps: robots' nodes equal every step."""
+    f = np.load(GREEDY[-1])
+    h, R, T, M = _handle_for(f)
+    o = oc.CoverageOracle(f["targets"], R, M)
+    cost, prev = oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R)
+    start = np.arange(R) * (T // R)
+    h.reset(start[None], np.zeros((1, M - R), np.uint8))
+    o.reset(start, np.arange(T) + R)
+    for t in range(30):
+        cur = o.closest()
+        ea, er = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+        ea[er] = 0
+        h.step(greedy=True)
+        np.testing.assert_array_equal(h.actions()[0][0], ea)
+        o.step(ea)
+        np.testing.assert_array_equal(h.robots(0)[1], o.closest())
+    h.close()
