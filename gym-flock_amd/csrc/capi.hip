@@ -412,12 +412,6 @@ int packed_outputs(fe_handle* h, bool bits, gf::StepArgs& a, int* bw) {
 int knn_mode(const fe_handle* h, int flags, bool dyn) {
   if (!(flags & FE_WITH_KNN) || h->cfg.n_neighbors <= 0) return 0;
   const bool variant = h->has_variant || h->dt_per_env;
-#ifndef GF_EXP_KNN_V2  // (round-4 experiment: the step writes bits, flock_knn_rank_kernel + rim rank)
-#define GF_EXP_KNN_V2 0
-#endif
-  if (GF_EXP_KNN_V2 && dyn && h->cfg.n_neighbors == gf::kStepFusedK && !variant &&
-      h->cfg.n_agents <= gf::kKnnRankMaxN)
-    return 1;
   if (dyn && gf::step_fused_knn_ok(h->cfg.n_agents, h->R, h->cfg.n_neighbors, variant, h->prefetch != 0)) return 2;
   return 1;
 }
@@ -647,17 +641,7 @@ int launch_knn_cur(fe_handle* h, int mode) {
     GF_HIP(hipEventRecord(h->ev_kin[1], h->stream2));
     GF_HIP(hipStreamWaitEvent(h->kstream, h->ev_kin[1], 0));
   }
-  hipError_t e = hipSuccess;
-  if (GF_EXP_KNN_V2 && mode == 1 && k.K == gf::kStepFusedK && k.N <= gf::kKnnRankMaxN) {
-    // the rows with >= k neighbours ranked from the bits, the rest exactly by the rim pass
-    e = gf::launch_knn_rank(k, h->cfg.comm_radius * h->cfg.comm_radius, h->kstream);
-    k.rim = 1;
-    k.adj_bits = nullptr;
-    k.degree = nullptr;
-    if (e == hipSuccess) e = gf::launch_knn(k, h->kstream);
-  } else {
-    e = gf::launch_knn(k, h->kstream);
-  }
+  hipError_t e = gf::launch_knn(k, h->kstream);
   if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
   GF_HIP(hipEventRecord(r.ev, h->kstream));
   r.live = true;

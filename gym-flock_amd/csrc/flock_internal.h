@@ -124,11 +124,6 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 // kStepFusedK, no variant, no tile prefetch, at least K word-slices per row).
 bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
-// k = kStepFusedK nearest of rows with >= k neighbours from the step's adjacency bits and
-// degrees (N <= kKnnRankMaxN); the others get idx = -1 and their block flagged in
-// rimflag for launch_knn in rim mode.
-constexpr int kKnnRankMaxN = 2048;
-hipError_t launch_knn_rank(const KnnArgs& a, double cr2, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
 // per env: mean vel_diffs, mean min_dists of launch_stats' outputs -> out (B,2)
 hipError_t launch_stats_summary(const StatsArgs& a, double* out, hipStream_t s);

@@ -1630,84 +1630,6 @@ __device__ __forceinline__ void knn_block(const KnnArgs& a, const int L, unsigne
   knn_write_row<K>(a, xb, g, i, N, kr, kj);
 }
 
-// Flocking-v0 k nearest from the step's adjacency (kNN after a step that wrote its bits,
-// N <= kKnnRankMaxN): one lane per row. A row with at least K neighbours has its K
-// nearest among them (every other agent has r2 >= comm_radius^2), so only its set bits
-// are ranked, by integer keys (q << jbits) | j with q = min(floor(r2 * 2^qbits / cr2),
-// qmax) kept as a sorted list of K + 1 by v_med3 insertion (the fused step's keys). The
-// row is written when the K + 1 smallest keys have distinct q (the top K are then
-// strictly closer than everyone else and strictly ordered, the reference's argsort
-// order); rows with fewer neighbours or such ties get idx = -1 and their 256-row block
-// flagged for the rim kernel (exact float64 (r2, j) ranking). The env's state is staged in
-// LDS (32 B per agent); the observation is x_i - x_j from it.
-template <int K>
-__global__ __launch_bounds__(kThreads) void flock_knn_rank_kernel(KnnArgs a, double ksc, unsigned qmax, int jb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  St* lst = reinterpret_cast<St*>(smem);
-  const int N = a.N;
-  const int bpe = (N + kThreads - 1) / kThreads;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = L / bpe;
-  const int i = (L - b * bpe) * kThreads + threadIdx.x;
-  const St* xb = reinterpret_cast<const St*>(a.x) + (size_t)b * N;
-  for (int t = threadIdx.x; t < N; t += kThreads) lst[t] = xb[t];
-  __syncthreads();
-  if (i >= N) return;
-  const size_t g = (size_t)b * N + i;
-  const int Wn = (N + 63) >> 6;
-  const double2 pi = *reinterpret_cast<const double2*>(&lst[i]);
-  bool slow = a.degree[g] < K;
-  unsigned kk[K + 1];
-#pragma unroll
-  for (int m = 0; m <= K; ++m) kk[m] = 0xFFFFFFFFu;
-  if (!slow) {
-    const uint64_t* bits = a.adj_bits + g * Wn;
-    const double qm = static_cast<double>(qmax);
-    for (int w0 = 0; w0 < Wn; w0 += 8) {  // eight words in flight per lane
-      uint64_t wv[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) wv[q] = w0 + q < Wn ? bits[w0 + q] : 0ull;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        uint64_t m = wv[q];
-        while (m) {
-          const int j = ((w0 + q) << 6) + __builtin_ctzll(m);
-          m &= m - 1;
-          const double2 pj = *reinterpret_cast<const double2*>(&lst[j]);
-          const double dx = pi.x - pj.x, dy = pi.y - pj.y;
-          const unsigned qv = static_cast<unsigned>(fmin((dx * dx + dy * dy) * ksc, qm));
-          knn_list_insert<K + 1>(kk, (qv << jb) | static_cast<unsigned>(j));
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 1; m <= K; ++m) slow |= kk[m] != 0xFFFFFFFFu && (kk[m] >> jb) == (kk[m - 1] >> jb);
-  }
-  if (slow) {  // the rim kernel ranks it exactly
-    a.idx[g * K] = -1;
-    a.rimflag[L] = 1;
-    return;
-  }
-  const St me = lst[i];
-  const unsigned jm = (1u << jb) - 1u;
-#pragma unroll
-  for (int m = 0; m < K; ++m) {
-    const int j = static_cast<int>(kk[m] & jm);
-    a.idx[g * K + m] = j;
-    const St o = lst[j];
-    float4 ob;
-    ob.x = static_cast<float>(me.px - o.px);
-    ob.y = static_cast<float>(me.py - o.py);
-    ob.z = static_cast<float>(me.vx - o.vx);
-    ob.w = static_cast<float>(me.vy - o.vy);
-    reinterpret_cast<float4*>(a.obs)[g * K + m] = ob;
-    if (m == K - 1 && a.r2k) {
-      const double dx = me.px - o.px, dy = me.py - o.py;
-      a.r2k[g] = static_cast<float>(dx * dx + dy * dy);
-    }
-  }
-}
-
 // Rim mode runs a small grid that walks the blocks (kKnnRimGrid workgroups): it is
 // enqueued beside the next step, whose workgroups hold most CU slots, and a full grid of
 // mostly idle workgroups took ~150 us to drain between them. Other modes: one
@@ -1907,23 +1829,6 @@ hipError_t launch_knn(const KnnArgs& a, hipStream_t s) {
 #undef GF_KNN_CASE
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_knn_rank(const KnnArgs& a, double cr2, hipStream_t s) {
-  if (a.K != kStepFusedK || a.N > kKnnRankMaxN || !a.adj_bits || !a.degree || !a.rimflag) return hipErrorInvalidValue;
-  int jb = 1;
-  while ((1 << jb) < a.N) ++jb;
-  const unsigned qmax = (1u << (32 - jb)) - 2u;
-  const double ksc = std::ldexp(1.0, 32 - jb) / cr2;
-  const size_t bytes = (size_t)a.N * sizeof(St);
-  static std::atomic<uint64_t> attr{0};
-  if (const hipError_t e = max_lds_once(reinterpret_cast<const void*>(&flock_knn_rank_kernel<kStepFusedK>), attr,
-                                        (int)(kKnnRankMaxN * sizeof(St)));
-      e != hipSuccess)
-    return e;
-  const int grid = a.B * ((a.N + kThreads - 1) / kThreads);
-  hipLaunchKernelGGL((flock_knn_rank_kernel<kStepFusedK>), dim3(grid), dim3(kThreads), bytes, s, a, ksc, qmax, jb);
   return hipGetLastError();
 }
 
