@@ -104,7 +104,6 @@ struct fe_handle {
   int R = 0, T = 0, bpe = 0;
   size_t BN = 0;
   int diag = 0;                         // ablation switches (diagnostic build only, fe_diag)
-  int R_ctrl = 0;                       // rows per block of the step + controller kernel
   int prefetch = 0;                     // tile loads one tile ahead (N >= 16 tiles)
   int store_fast[2] = {0, 1};           // fast network store loop: plain step / with controller
   // kernel timing (bench roofline)
@@ -507,10 +506,6 @@ gf::StepArgs env_range(const fe_handle* h, const gf::StepArgs& a, int b0, int nb
 
 int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bool ctrl) {
   gf::StepArgs a = a_in;
-  if (ctrl && !a.variant && !a.knn_idx && h->R_ctrl != a.R) {  // fused kNN keeps R (slices >= k)
-    a.R = h->R_ctrl;
-    a.bpe = (a.N + a.R - 1) / a.R;
-  }
   a.store_fast = h->store_fast[ctrl ? 1 : 0];
   const bool split = split_next(h, a.B);
   h->other_work = false;
@@ -704,9 +699,9 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   // tile loads issued a tile ahead: 1604 -> 1527 us at N=8192 (16 tiles); no gain at 2-8
   // tiles, where its registers cost occupancy instead
   h->prefetch = (cfg->n_agents + h->T - 1) / h->T >= 16 ? 1 : 0;
-  // step + controller: 64-row blocks at 513..1024 agents (194.7 vs 200.1 us at config 2;
-  // the plain step stays at 32: 198 vs 184)
-  h->R_ctrl = (h->R == 32 && cfg->n_agents > 512 && cfg->n_agents <= 1024) ? 64 : h->R;
+  // the step + controller uses the plain step's rows per block: with one superset pass 1
+  // (kOuter) 32-row blocks beat the 64 of round 3, 169.3 vs 174.4 us at config 2
+  // (profiles/r04/ab_ctrl_rows32.txt)
   h->bpe = (cfg->n_agents + h->R - 1) / h->R;
   if ((size_t)h->bpe * B > 0x7fffffff) {
     delete h;

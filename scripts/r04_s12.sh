@@ -2,7 +2,8 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/r04; mkdir -p $O
 GYMFLOCK_LIB=$PWD/build/lib_w6/libgymflock.so timeout -k 10 400 python -u -m pytest tests/test_flock_gpu.py -k "knn or v0" -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/s12_knn_w6.log 2>&1; echo "knn w6 tests rc=$?"; tail -2 $O/s12_knn_w6.log
-ROUNDS=3 OUT=gpurun_out/r04/ab_w6 timeout -k 10 700 python scripts/ab_multi.py base=gym-flock_amd/lib/libgymflock.so w6=build/lib_w6/libgymflock.so -- --no-other-configs --no-packed-line --no-controller-line
+GYMFLOCK_LIB=$PWD/build/lib_c32/libgymflock.so timeout -k 10 400 python -u -m pytest tests/test_flock_gpu.py -k "controller or ctrl or expert or closed" -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/s12_ctrl_c32.log 2>&1; echo "ctrl c32 tests rc=$?"; tail -2 $O/s12_ctrl_c32.log
+ROUNDS=3 OUT=gpurun_out/r04/ab_w6 timeout -k 10 900 python scripts/ab_multi.py base=gym-flock_amd/lib/libgymflock.so w6=build/lib_w6/libgymflock.so c32=build/lib_c32/libgymflock.so -- --no-other-configs --no-packed-line
 echo "== knn instruction mix by part"
 P=$PWD/gpurun_out/r04/pmc_knn; mkdir -p $P
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD"
