@@ -174,7 +174,7 @@ int ensure_time_matrix(cov_handle* h) {
         (rc = calloc_dev(&h->tm_cost8, (size_t)B * Tm * Tm)) || (rc = calloc_dev(&h->tm_wide, (size_t)B)))
       return rc;
     if (Tm <= gf::kGreedyListMaxT) {  // rows padded to 16 bytes (greedy_from_list's loads)
-      h->gstride = (Tm + 7) & ~7;
+      h->gstride = (Tm + gf::kGreedyListPad - 1) & ~(gf::kGreedyListPad - 1);
       if ((rc = calloc_dev(&h->tm_glist, (size_t)B * Tm * h->gstride)) || (rc = calloc_dev(&h->tm_glen, (size_t)B * Tm)))
         return rc;
     }

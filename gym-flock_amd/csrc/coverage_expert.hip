@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void cov_greedy_list_step_kernel(CovGreedyArgs
       c = a.cur[(size_t)b * R + i] - R;
     }
     const size_t row = (size_t)b * Tm + c;
-    const int g = greedy_from_list(a.glist + row * a.gstride, a.glen[row], vbits, any_vis, a.nvisited[b] >= T);
+    const int g = greedy_from_list(a.glist + row * a.gstride, a.glen + row, vbits, any_vis, a.nvisited[b] >= T);
     const uint32_t flag = (uint32_t)g >> 2;
     if (flag & kGreedyErr) atomicOr(a.err, 8);
     a.actions[(size_t)b * R + i] = (flag & kGreedyRnd) ? 0 : (g & 3);

@@ -59,20 +59,34 @@ constexpr uint32_t kGreedyRnd = 1, kGreedyErr = 2;
 // reference masks visited targets through np.where on its (N,1) visited column, which
 // also hits column 0). vbits: the env's visited flags as bits (LDS). Returns
 // action | flag << 2; flag kGreedyRnd also when every listed target is masked (at once
-// when the env has no unvisited target left: nv == T).
-__device__ __forceinline__ int greedy_from_list(const uint16_t* row, int len, const uint32_t* vbits, bool any_vis,
-                                                bool none_left) {
-  if (none_left) len = 0;
-  for (int k0 = 0; k0 < len; k0 += 8) {
-    const uint4 q = *reinterpret_cast<const uint4*>(row + k0);
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+// when the env has no unvisited target left: nv == T). The row's length and its first
+// kGreedyListPad entries are loaded together, and each later round trip brings the next
+// kGreedyListPad (four 16-byte loads): late in an episode, when most targets near a robot
+// are visited, its scan runs deep into the list, and one 16-byte load per round trip made
+// such robots' dependent loads the step's longest phase. Rows are padded to a multiple
+// of kGreedyListPad entries (gstride).
+constexpr int kGreedyListPad = 32;
+__device__ __forceinline__ int greedy_from_list(const uint16_t* row, const uint16_t* lenp, const uint32_t* vbits,
+                                                bool any_vis, bool none_left) {
+  const uint4* r4 = reinterpret_cast<const uint4*>(row);
+  int len = *lenp;
+  uint4 q[kGreedyListPad / 8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (k0 + j >= len) break;
-      const uint32_t e = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+  for (int c = 0; c < kGreedyListPad / 8; ++c) q[c] = r4[c];
+  if (none_left) len = 0;
+  for (int k0 = 0; k0 < len; k0 += kGreedyListPad) {
+    if (k0 > 0) {
+#pragma unroll
+      for (int c = 0; c < kGreedyListPad / 8; ++c) q[c] = r4[k0 / 8 + c];
+    }
+#pragma unroll
+    for (int j = 0; j < kGreedyListPad; ++j) {
+      const uint4 v = q[j >> 3];
+      const uint32_t w = (j & 7) < 2 ? v.x : (j & 7) < 4 ? v.y : (j & 7) < 6 ? v.z : v.w;
+      const uint32_t e = (w >> (16 * (j & 1))) & 0xFFFFu;
       const int t = static_cast<int>(e & 1023u);
       const bool masked = ((vbits[t >> 5] >> (t & 31)) & 1u) || (t == 0 && any_vis);
-      if (!masked) return static_cast<int>(e >> 10);
+      if (k0 + j < len && !masked) return static_cast<int>(e >> 10);
     }
   }
   return static_cast<int>(kGreedyRnd << 2);

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
     int n = c;
     if (greedy) {  // :814-869 from the node's greedy list; fallbacks take action 0 here
       const size_t row = (size_t)b * Tm + (c - R);
-      const int g = greedy_from_list(a.glist + row * a.gstride, a.glen[row], gvis, any_vis, nv0 >= T);
+      const int g = greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, any_vis, nv0 >= T);
       const uint32_t flag = static_cast<uint32_t>(g) >> 2;
       if (flag & kGreedyErr) atomicOr(a.err, 8);
       ai = (flag & kGreedyRnd) ? 0 : (g & 3);

@@ -290,3 +290,39 @@ def test_fused_greedy_step_vs_oracle():
         o.step(ea)
         np.testing.assert_array_equal(h.robots(0)[1], o.closest())
     h.close()
+
+
+def test_fused_greedy_deep_list_scans_vs_oracle():
+    """Late-episode shape: every target visited but a few, so each robot's greedy list is
+    scanned far past its first load of entries (the list loader fetches 32 entries per
+    round trip). The fused greedy step against the oracle for 25 steps on the r20 map, with
+    the remaining targets at depths 7..213 of the robots' lists; the robots reach all six
+    within the 25 steps, after which every robot falls back."""
+    f = np.load(GREEDY[-1])
+    h, R, T, M = _handle_for(f)
+    o = oc.CoverageOracle(f["targets"], R, M)
+    cost, prev = oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R)
+    rs = np.random.RandomState(3)
+    start = rs.choice(T, R, replace=False)
+    left = rs.choice(np.setdiff1d(np.arange(T), start), size=6, replace=False)
+    vis = np.ones((1, M - R), np.uint8)
+    vis[0, left] = 0
+    h.reset(start[None], vis)
+    o.reset(start, left + R)
+    depths = []
+    for t in range(25):
+        cur = o.closest()
+        if t == 0:  # how deep the first unvisited target sits in each robot's list
+            for c in cur - R:
+                order = np.lexsort((np.arange(T), cost[c]))
+                depths.append(int(np.nonzero(np.isin(order, left))[0][0]))
+        ea, er = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+        ea[er] = 0
+        h.step(greedy=True)
+        ga, gr = h.actions()
+        np.testing.assert_array_equal(gr[0], er)
+        np.testing.assert_array_equal(ga[0], ea)
+        o.step(ea)
+        np.testing.assert_array_equal(h.robots(0)[1], o.closest())
+    assert max(depths) > 64, depths  # scans past two round trips of the loader
+    h.close()
