@@ -432,6 +432,7 @@ int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a, int xw) {
     a.knn_rimflag = h->knn_rimflag[xw];
     a.knn_jbits = jb;
     a.knn_qmax = (1u << (32 - jb)) - 2u;  // below the all-ones empty-slot key
+    a.knn_qmaxd = static_cast<double>(a.knn_qmax);
     a.knn_qscale = std::ldexp(1.0, 32 - jb);
   }
   if (int rc = wait_knn_readers(h, xw, bw)) return rc;

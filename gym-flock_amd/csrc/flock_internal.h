@@ -84,6 +84,7 @@ struct StepArgs {
                           // left to the rim kNN (its workgroups read only this byte)
   double knn_qscale;      // 2^qbits
   unsigned knn_qmax;      // 2^qbits - 2
+  double knn_qmaxd;       // the same as a double (compared with r2 * scale)
   int knn_jbits;          // bits of the agent index (qbits = 32 - jbits)
 };
 

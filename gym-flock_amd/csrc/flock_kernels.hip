@@ -467,6 +467,14 @@ __device__ __forceinline__ float uniform_f(float v) {
 // v_writelane_b32 through the LLVM intrinsic (this clang has no __builtin for it), so
 // the compiler applies the constant-bus and lane-select hazard rules itself.
 extern "C" __device__ int gf_writelane_i32(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+// float64 -> uint32, saturating (negative and NaN -> 0, >= 2^32 -> 2^32 - 1): the
+// hardware conversion itself (a plain cast is undefined outside the range, and the
+// compiler's saturating form adds two compares and two selects)
+__device__ __forceinline__ unsigned gf_cvt_u32_sat(double v) {
+  unsigned r;
+  asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
 
 // Minimum over aligned groups of S lanes (S a power of two): DPP lane swaps inside rows
 // of 16 (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), shuffles beyond.
@@ -554,7 +562,8 @@ __device__ __forceinline__ void put_lane(unsigned& w0, unsigned& w1, uint64_t m,
 // stores (1 KiB per wave instruction); the block's rows are one contiguous range
 // starting at global row grow0.
 __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint64_t* adj, const float* inv,
-                                                   f4v* stab, int Wn, size_t grow0, int nrows, int wid, int lane) {
+                                                   f4v* stab, int Wn, size_t grow0, int nrows, int wid, int lane,
+                                                   bool knn) {
   const int N = a.N;
   const bool vec4 = (N & 3) == 0;
   // wave w writes the contiguous rows [w*R/4, (w+1)*R/4): the 4 waves' concurrent
@@ -563,8 +572,11 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
   // fast form (N % 1024 == 0): every lane owns float4 columns lane + 64m of a row, so
   // its nibble sits at a fixed bit offset of 32-bit words 8 apart; four words are read
   // ahead and each nibble selects a float4 from the row's table (below).
-  // The host picks it per kernel (StepArgs.store_fast; diag 64 / 128 force it off / on).
-  const bool fast = (N & 1023) == 0 && !GF_ABLATE(a, (4 | 64)) && (a.store_fast || GF_ABLATE(a, 128));
+  // The host picks it per kernel (StepArgs.store_fast; diag 64 / 128 force it off / on);
+  // the fused-kNN step always takes it: 10 VALU per 4 KiB of a wave instead of ~64 (the
+  // kNN step is bound by its VALU issue more than the plain step, which measured the
+  // fast loop slower: 164.1 vs 161.5 us, the kNN step 195 vs 207, profiles/r04)
+  const bool fast = (N & 1023) == 0 && !GF_ABLATE(a, (4 | 64)) && (a.store_fast || knn || GF_ABLATE(a, 128));
   const unsigned* bits32 = reinterpret_cast<const unsigned*>(adj);
   const int hl = lane & 15;
   const int wsel = 2 * (lane >> 4) + (hl >> 3);  // 32-bit word of column block m = 0
@@ -772,6 +784,12 @@ void flock_step_kernel(StepArgs a) {
   // exactly in float64 (it computes every such pair's r2 anyway), writing the exact
   // adjacency words back; the fused-kNN controller keeps separate near bits
   constexpr bool kOuter = CTRL && KN == 0;
+  // Flocking-v0 without the controller (kSupK): pass 1 leaves the float32 superset of the
+  // adjacency (one compare per pair, no band sweep); the feature pass, which computes
+  // every such pair's float64 r2 to rank it, decides the adjacency exactly and writes the
+  // exact words back, so every tile's feature pass runs before the network stores
+  constexpr bool kSupK = KN > 0 && !CTRL;
+  constexpr bool kSup = kOuter || kSupK;
   uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits (KN && CTRL)
   uint64_t* candb = nearb + ((CTRL && !kOuter) ? (size_t)R * Wt : 0);  // (predicted rows) x Wt kNN candidates
   double* red = reinterpret_cast<double*>(candb + (KN ? (size_t)R * Wt : 0));
@@ -854,7 +872,6 @@ void flock_step_kernel(StepArgs a) {
 #pragma unroll
     for (int m = 0; m < KL; ++m) kk[m] = 0xFFFFFFFFu;
   }
-  [[maybe_unused]] const double qmaxd = static_cast<double>(a.knn_qmax);
   // one neighbour pair (row fr = me, tile column c): features and controller gradient.
   // The row's state is read from LDS per feature pass, so it holds no registers
   // through pass 1.
@@ -867,10 +884,13 @@ void flock_step_kernel(StepArgs a) {
       isnear = r2 <= a.cr;
       if (!isadj && !isnear) return isadj;
     }
+    if constexpr (kSupK) isadj = r2 < a.cr2;  // a superset or candidate bit: decided here (:117)
     if constexpr (KN > 0) {
       if (!GF_ABLATE(a, 0x200000)) {  // diag 0x200000: no insertion (timing only)
-        // q = min(floor(r2 * ksc), qmax); fmin returns qmax for a NaN r2 (ranked last)
-        const unsigned q = static_cast<unsigned>(fmin(r2 * ksc, qmaxd));
+        // q = min(ceil(r2 * ksc), qmax): qmax - (qmax - r2 * ksc truncated; negative or
+        // NaN converts to 0), so a NaN r2 ranks last. ceil or floor, q never decreases as
+        // r2 grows, and q <= qmax - 2 still means r2 < Tr (the merge's test (a)).
+        const unsigned q = a.knn_qmax - gf_cvt_u32_sat(fma(-r2, ksc, a.knn_qmaxd));
         knn_list_insert<KL>(kk, (q << a.knn_jbits) | static_cast<unsigned>(j0 + c));
       }
       if (!isadj && !(CTRL && isnear)) return isadj;  // a candidate only: no features
@@ -932,8 +952,22 @@ void flock_step_kernel(StepArgs a) {
         *aw = ex;
         continue;
       }
-      const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
       const uint64_t cm = (KN && crow) ? crow[w] : 0ull;
+      if constexpr (kSupK) {  // superset and candidates in, the exact adjacency word out
+        // am covers the adjacency, so clearing the bit of every pair found not adjacent
+        // (the rare float32 superset pairs past comm_radius, and a predicted row's
+        // candidates, whose bits may not be set) leaves the exact word; an LDS atomic
+        // keeps it a branch that no wave enters unless one of its lanes has such a pair
+        uint64_t m = am | cm;
+        while (m) {
+          const int k = __builtin_ctzll(m);
+          m &= m - 1;
+          if (!pair_terms(me, j0, (w << 6) + k, false, false, ksc))
+            __hip_atomic_fetch_and(aw, ~(1ull << k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        continue;
+      }
+      const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
       uint64_t m = am | nm | cm;
       while (m) {
         const int k = __builtin_ctzll(m);
@@ -1036,7 +1070,30 @@ void flock_step_kernel(StepArgs a) {
           if (lane < nrows) ptc[lane] = tcr_l;  // read back by this wave only (in-order LDS)
         }
       }
-      if (fused) {
+      if constexpr (kSupK) {
+        // one compare per column: the float32 superset of the adjacency (the feature pass
+        // decides it exactly), plus the predicted rows' candidates when most rows are
+        // predicted. Rows in pairs; the rows past nrows sit far away in rxy (columns past
+        // the tile are masked: at huge coordinates ba.hi is +inf)
+        const uint64_t vma = __ballot(va), vmb = __ballot(vb);
+        auto srow = [&](int r, float2 pr) {
+          const f2v d2 = d2_f32(pr.x, pr.y, qx, qy);
+          put_lane(wa0, wa1, __ballot(!(d2.x >= ba.hi)) & vma, r);
+          put_lane(wb0, wb1, __ballot(!(d2.y >= ba.hi)) & vmb, r);
+          if (fused && ((predm >> r) & 1)) {  // wave-uniform
+            const float tc = ptc[r];
+            put_lane(fca0, fca1, __ballot(d2.x < tc), fp);
+            put_lane(fcb0, fcb1, __ballot(d2.y < tc), fp);
+            ++fp;
+          }
+        };
+        const int nr4 = (nrows + 3) & ~3;
+        for (int r = 0; r < nr4; r += 2) {
+          const float2 p0 = rxy[r], p1 = rxy[r + 1];
+          srow(r, p0);
+          srow(r + 1, p1);
+        }
+      } else if (fused) {
         // rows in pairs (their LDS reads issued together), as the plain step; rows past
         // nrows sit far away in rxy and are never predicted
         auto frow = [&](int r, float2 pr) {
@@ -1214,7 +1271,7 @@ void flock_step_kernel(StepArgs a) {
     // pass 2 (features) of every tile but the last runs here; the last tile's runs
     // after the network stores are issued, so the stores drain under it (kOuter: the
     // stores need the exact adjacency this pass writes, so every tile's runs here)
-    if (kOuter || j0 + T < N) {
+    if (kSup || j0 + T < N) {
       feature_pass(j0, nch);
       if (ti < 1) GF_STAMP(4);
     }
@@ -1229,7 +1286,7 @@ void flock_step_kernel(StepArgs a) {
   }
   const int jl = ((N - 1) / T) * T;  // first column of the last tile (still in LDS)
   const int nchl = (N - jl + 63) >> 6;
-  if constexpr (kOuter) __syncthreads();  // the last feature pass's adjacency words
+  if constexpr (kSup) __syncthreads();  // the last feature pass's adjacency words
 
   // degree of each row -> 1/deg for the mean-pooled network (:120-122)
   {
@@ -1253,10 +1310,10 @@ void flock_step_kernel(StepArgs a) {
   __syncthreads();
   GF_STAMP(7);
 
-  if (a.network) store_network_rows(a, adj, inv, stab, Wn, env0 + i0, nrows, wid, lane);
+  if (a.network) store_network_rows(a, adj, inv, stab, Wn, env0 + i0, nrows, wid, lane, KN > 0);
 
   GF_STAMP(8);
-  if constexpr (!kOuter) feature_pass(jl, nchl);
+  if constexpr (!kSup) feature_pass(jl, nchl);
   GF_STAMP(9);
 
   [[maybe_unused]] RawState<UF64> kraw{};

@@ -19,7 +19,10 @@ from gym_flock.init_states import synthetic_batch  # noqa: E402
 
 N, B = int(os.environ.get("N", 1024)), int(os.environ.get("B", 256))  # N=8192 B=16: a config-5 half batch
 flags = int(os.environ.get("FLAGS", "0"), 0)
-h = nat.FlockHandle(N, B)
+KNN = os.environ.get("KNN") == "1"  # the Flocking-v0 step (fused 7-NN)
+h = nat.FlockHandle(N, B, n_neighbors=7 if KNN else 0)
+if KNN:
+    flags |= nat.FE_WITH_KNN
 h.set_streams(1)  # one launch per step: every workgroup of the step has its stamp slots
 if os.environ.get("DIAG"):
     h.diag_switches(int(os.environ["DIAG"]))

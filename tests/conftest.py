@@ -11,3 +11,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+
+
+def pytest_runtest_setup(item):
+    if os.environ.get("GF_ABORT_BT") == "1":  # debug aid: native backtrace on SIGABRT
+        import ctypes  # (re)installed before every test: the runtimes may install their own
+        ctypes.CDLL(os.path.join(ROOT, "scripts", "dbg", "libabort_bt.so")).gf_install_abort_bt()
