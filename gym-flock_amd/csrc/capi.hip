@@ -1506,12 +1506,17 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
   std::memcpy(&uid, id, 128);
   // RCCL's non-blocking init still connects to the bootstrap root inside the call, which
   // waits for every rank: with a rank missing it never returns. The call therefore runs
-  // on a thread of its own; past the deadline it is left behind (with whatever it
-  // creates) and this rank fails with GF_ECOMM, its handle still usable.
+  // on a thread of its own, which also waits for the communicator to leave
+  // ncclInProgress before it ends (RCCL's own init thread works on the creating thread's
+  // HIP state: with torch's HIP runtime bound, a creating thread that exited first left
+  // a corrupted heap). It hands the communicator over through `state`: 0 running,
+  // 1 handed over, 2 abandoned by this call at the deadline (the helper then aborts what
+  // it created), so exactly one side owns the communicator. This rank then fails with
+  // GF_ECOMM, its handle still usable.
   struct InitJob {
     ncclComm_t comm = nullptr;
     ncclResult_t r = ncclInProgress;
-    std::atomic<bool> done{false};
+    std::atomic<int> state{0};
   };
   auto job = std::make_shared<InitJob>();
   const int dev = h->cfg.device;
@@ -1520,14 +1525,29 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
     ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
     config.blocking = 0;
     ncclComm_t c = nullptr;
-    const ncclResult_t rr = ncclCommInitRankConfig(&c, nranks, uid, rank, &config);
+    ncclResult_t rr = ncclCommInitRankConfig(&c, nranks, uid, rank, &config);
+    if (c && (rr == ncclSuccess || rr == ncclInProgress)) {
+      for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+        rr = q != ncclSuccess ? q : st;
+        if (rr != ncclInProgress || job->state.load(std::memory_order_acquire) == 2) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+    }
     job->comm = c;
     job->r = rr;
-    job->done.store(true, std::memory_order_release);
+    int running = 0;
+    if (!job->state.compare_exchange_strong(running, 1, std::memory_order_acq_rel) && c)
+      ncclCommAbort(c);  // abandoned: nobody else will release it
   }).detach();
-  while (!job->done.load(std::memory_order_acquire)) {
-    if (Clock::now() > deadline)
-      return fail(GF_ECOMM, "ncclCommInitRankConfig: timed out (a rank did not join); the initialisation is left behind");
+  while (job->state.load(std::memory_order_acquire) != 1) {
+    if (Clock::now() > deadline) {
+      int running = 0;
+      if (job->state.compare_exchange_strong(running, 2, std::memory_order_acq_rel))
+        return fail(GF_ECOMM, "ncclCommInitRankConfig: timed out (a rank did not join); the initialisation is aborted behind");
+      break;  // handed over just now
+    }
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
   h->comm = job->comm;
