@@ -6,6 +6,7 @@ __graft_entry__.build()); if it is missing or no GPU is present, every call that
 needs it raises — there is no CPU fallback in the product path.
 """
 import ctypes
+import math
 import functools
 import os
 
@@ -240,11 +241,21 @@ class HostPool:
     def array_addr(self, shape, dtype):
         """(array, its address): a page-locked array from the pool, or past the cap (or if
         page-locked memory runs out) an ordinary numpy array and None."""
-        import weakref
         dtype = np.dtype(dtype)
-        nbytes = int(np.prod(shape)) * dtype.itemsize
+        nbytes = math.prod(shape) * dtype.itemsize
         if nbytes == 0:
             return np.empty(shape, dtype), None
+        buf, p = self.block_addr(nbytes)
+        if p is None:
+            return np.empty(shape, dtype), None
+        return np.frombuffer(buf, dtype=dtype).reshape(shape), p
+
+    def block_addr(self, nbytes):
+        """(ctypes byte buffer, its address) of `nbytes` page-locked bytes from the pool, or
+        (None, None) past the cap or when page-locked memory runs out. Arrays made over the
+        buffer (np.ndarray(buffer=...)) keep it alive; it returns to the pool once all of
+        them are released."""
+        import weakref
         with self.lock:
             self._reclaim(4)
             lst = self.free.get(nbytes)
@@ -253,7 +264,7 @@ class HostPool:
                 lst = self.free.get(nbytes)
             p = lst.pop() if lst else None
             if p is None and self._live + nbytes > self.cap:
-                return np.empty(shape, dtype), None
+                return None, None
             self._live += nbytes
         if p is None:
             out = ctypes.c_void_p()
@@ -262,12 +273,12 @@ class HostPool:
             except GymFlockError:
                 with self.lock:
                     self._live -= nbytes
-                return np.empty(shape, dtype), None
+                return None, None
             p = out.value
         buf = (ctypes.c_uint8 * nbytes).from_address(p)
         with self.lock:
             self.out.append((weakref.ref(buf), p, nbytes))
-        return np.frombuffer(buf, dtype=dtype).reshape(shape), p
+        return buf, p
 
     def trim(self):
         """Free the recycled (unused) buffers."""

@@ -69,6 +69,7 @@ class FlockingRelativeEnv(Env):
         self._want_ctrl = False
         self._ctrl_cache = None
         self._ubuf = None
+        self._layout = None  # ((n, ctrl), offsets of the step's page-locked output block)
 
         self._make_spaces()
         self.fig = None
@@ -171,22 +172,25 @@ class FlockingRelativeEnv(Env):
             uaddr = self._ubuf.addr
         # one page-locked block per step: network, controls, reward, state_values (64-byte
         # aligned parts, so the network rows get 16-byte stores); the caller's arrays are
-        # views of it, and it returns to the pool once all of them are released
+        # made over it, and it returns to the pool once all of them are released
         ctrl = self._want_ctrl
-        o_ct = (4 * n * n + 63) & ~63
-        o_rw = o_ct + ((16 * n + 63) & ~63 if ctrl else 0)
-        o_sv = o_rw + 64
-        size = o_sv + 24 * n
-        blk, base = nat.host_pool().array_addr((size,), np.uint8)
-        net = blk[:4 * n * n].view(np.float32).reshape(n, n)
-        rw = blk[o_rw:o_rw + 8].view(np.float64)
-        sv = blk[o_sv:o_sv + 24 * n].view(np.float32).reshape(n, 6)
-        ct = blk[o_ct:o_ct + 16 * n].view(np.float64).reshape(n, 2) if ctrl else None
-        if base is None:  # not page-locked (pool cap): the library copies after the launch
-            h.step_host(uaddr, f64, sv.ctypes.data, net.ctypes.data, rw.ctypes.data,
-                        ct.ctypes.data if ctrl else None)
-        else:
-            h.step_host(uaddr, f64, base + o_sv, base, base + o_rw, base + o_ct if ctrl else None)
+        lay = self._layout
+        if lay is None or lay[0] != (n, ctrl):
+            o_ct = (4 * n * n + 63) & ~63
+            o_rw = o_ct + ((16 * n + 63) & ~63 if ctrl else 0)
+            o_sv = o_rw + 64
+            lay = self._layout = ((n, ctrl), o_ct, o_rw, o_sv, o_sv + 24 * n)
+        _, o_ct, o_rw, o_sv, size = lay
+        buf, base = nat.host_pool().block_addr(size)
+        if buf is None:  # not page-locked (pool cap): the library copies after the launch
+            buf = np.empty(size, np.uint8)
+        net = np.ndarray((n, n), np.float32, buf)
+        rw = np.ndarray((1,), np.float64, buf, o_rw)
+        sv = np.ndarray((n, 6), np.float32, buf, o_sv)
+        ct = np.ndarray((n, 2), np.float64, buf, o_ct) if ctrl else None
+        if base is None:
+            base = buf.ctypes.data
+        h.step_host(uaddr, f64, base + o_sv, base, base + o_rw, base + o_ct if ctrl else None)
         self.state_values, self.state_network = sv, net
         self._reward = float(rw[0])
         self._ctrl_cache = ct

@@ -15,6 +15,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.txt
 timeout -k 10 500 python bench.py --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err || { tail $O/bench20.err; exit 1; }
 timeout -k 10 500 python bench.py > $O/bench200.json 2> $O/bench200.err || { tail $O/bench200.err; exit 1; }
+timeout -k 10 300 python bench.py --workload coverage --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_cov.json 2> $O/bench_cov.err || { tail $O/bench_cov.err; exit 1; }
+timeout -k 10 300 python scripts/dropin_probe.py > $O/dropin_probe.txt 2>&1 || { tail $O/dropin_probe.txt; exit 1; }
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o trace -- python3 $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $O/rocprof_trace.log 2>&1 || { tail $O/rocprof_trace.log; exit 1; }
 pmc() {  # pmc <name> <script> [env...]
