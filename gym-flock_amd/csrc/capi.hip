@@ -926,7 +926,14 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
   if (int rc = use_dev(h)) return rc;
   const bool dyn = u != nullptr, ctrl = flags & FE_WITH_CONTROLLER, uf64 = dyn && (flags & FE_U_F64);
   const void* up = nullptr;
-  if (dyn) {
+  // one env of one tile: the actions travel in the kernel arguments (no read over the
+  // link inside the kernel); otherwise page-locked actions are read in place, others
+  // copied to the device first
+  const bool uin = dyn && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
+                   h->BN * 2 * (uf64 ? 8 : 4) <= (size_t)gf::kUInlineBytes;
+  if (uin) {
+    up = u;
+  } else if (dyn) {
     up = mapped_ptr(const_cast<void*>(u));  // page-locked: the kernel reads it in place
     if (!up) {
       GF_HIP(hipMemcpyAsync(h->u, u, h->BN * 2 * (uf64 ? 8 : 4), hipMemcpyHostToDevice, h->stream));
@@ -946,6 +953,7 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
   if (dyn) {
     a.x_out = h->x[h->cur ^ 1];
     a.u = up;
+    a.u_inline = uin ? 1 : 0;
   }
   a.state_values = state_values ? (sv_m ? sv_m : h->sv) : nullptr;
   a.network = network ? (net_m ? net_m : h->net) : nullptr;

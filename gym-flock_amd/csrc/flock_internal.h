@@ -52,6 +52,8 @@ struct StepArgs {
   int mean_pooling, centralized;
   int prefetch;           // tiled step issues each tile's loads one tile ahead (T <= 512)
   int store_fast;         // network rows by the fast bit-extract loop (N % 1024 == 0)
+  int u_inline;           // u is a host pointer: its B*N actions travel in the kernel arguments
+                          // (StepArgsU; one env of one tile, <= kUInlineBytes)
   int diag;               // ablation switches, read only by the diagnostic build (GF_ABLATE):
                           // 2 skip feature pass,
                           // 4 non-temporal network stores, 8 skip pass 1 (bits are left
@@ -86,6 +88,14 @@ struct StepArgs {
   unsigned knn_qmax;      // 2^qbits - 2
   double knn_qmaxd;       // the same as a double (compared with r2 * scale)
   int knn_jbits;          // bits of the agent index (qbits = 32 - jbits)
+};
+
+// The drop-in step's actions passed in the kernel arguments (fe_step_host, one env of up
+// to kUInlineBytes of actions: 384 agents in float32, 192 in float64)
+constexpr int kUInlineBytes = 3072;
+struct StepArgsU {
+  StepArgs a;
+  alignas(16) unsigned char u[kUInlineBytes];
 };
 
 constexpr int kStepFusedK = 7;  // Flocking-v0's n_neighbors (flocking.py:9)

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <atomic>
 
 #include <type_traits>
@@ -758,12 +759,24 @@ __device__ unsigned long long gf_stamp_buf[8192 * 16];
 // KN > 0 (Flocking-v0, flocking.py:20-25): each (row, slice) thread also keeps the KN
 // smallest keys of its neighbours, the S slices of a row are merged after the last
 // feature pass, and the row's k nearest indices and observation are written (below).
-template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
+// UIN: the drop-in step of a small env with its actions in the kernel arguments
+// (StepArgsU): they arrive with the dispatch instead of being read over the link from
+// page-locked host memory, one dependent round trip per workgroup fewer.
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0, bool UIN = false>
 __global__ __launch_bounds__(kThreads, VAR ? 1
                                            : (PF ? kWavesPf
                                                  : (KN ? (CTRL ? kWavesKnnCtrl : kWavesKnn)
                                                        : (CTRL ? kWavesCtrl : kWavesPlain))))
-void flock_step_kernel(StepArgs a) {
+void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type p) {
+  [[maybe_unused]] StepArgs uargs;
+  if constexpr (UIN) {
+    uargs = p.a;
+    uargs.u = p.u;
+  }
+  const StepArgs& a = *[&]() -> const StepArgs* {
+    if constexpr (UIN) return &uargs;
+    else return &p;
+  }();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = a.N, R = a.R, T = a.T;
   const int Wn = (N + 63) >> 6;  // adjacency words per row (whole env)
@@ -789,6 +802,9 @@ void flock_step_kernel(StepArgs a) {
   // every such pair's float64 r2 to rank it, decides the adjacency exactly and writes the
   // exact words back, so every tile's feature pass runs before the network stores
   constexpr bool kSupK = KN > 0 && !CTRL;
+#ifndef GF_AB_CANDLOOP
+#define GF_AB_CANDLOOP 0
+#endif
   constexpr bool kSup = kOuter || kSupK;
   uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits (KN && CTRL)
   uint64_t* candb = nearb + ((CTRL && !kOuter) ? (size_t)R * Wt : 0);  // (predicted rows) x Wt kNN candidates
@@ -836,8 +852,12 @@ void flock_step_kernel(StepArgs a) {
     if (lane < nrows && a.knn_r2) khist = a.knn_r2[env0 + i0 + lane];
   }
 
-  // rows owned by this workgroup (post-update state)
-  for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
+  // rows owned by this workgroup (post-update state). An env of one tile takes them from
+  // the tile's staging instead (below): one dependent round trip fewer, which the
+  // drop-in step pays over the link when its actions are read from page-locked host memory
+  const bool one_tile = N <= T;
+  if (!one_tile)
+    for (int r = tid; r < nrows; r += kThreads) rows[r] = load_state<DYN, UF64, VAR>(a, env0 + i0 + r);
 
   // feature-pass thread mapping: S word-slices per row
   const int S = kThreads / R;
@@ -958,13 +978,28 @@ void flock_step_kernel(StepArgs a) {
         // (the rare float32 superset pairs past comm_radius, and a predicted row's
         // candidates, whose bits may not be set) leaves the exact word; an LDS atomic
         // keeps it a branch that no wave enters unless one of its lanes has such a pair
+#if GF_AB_CANDLOOP
+        uint64_t m = am;
+#else
         uint64_t m = am | cm;
+#endif
         while (m) {
           const int k = __builtin_ctzll(m);
           m &= m - 1;
           if (!pair_terms(me, j0, (w << 6) + k, false, false, ksc))
             __hip_atomic_fetch_and(aw, ~(1ull << k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+#if GF_AB_CANDLOOP
+        // a predicted row's candidates outside the superset: never adjacent, only ranked
+        for (uint64_t mc = cm & ~am; mc; mc &= mc - 1) {
+          const int c = (w << 6) + __builtin_ctzll(mc);
+          const double2 o = *reinterpret_cast<const double2*>(&tile[c]);
+          const double dx = me.px - o.x, dy = me.py - o.y;
+          const double r2 = dx * dx + dy * dy;
+          const unsigned q = a.knn_qmax - gf_cvt_u32_sat(fma(-r2, ksc, a.knn_qmaxd));
+          knn_list_insert<KL>(kk, (q << a.knn_jbits) | static_cast<unsigned>(j0 + c));
+        }
+#endif
         continue;
       }
       const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
@@ -986,6 +1021,7 @@ void flock_step_kernel(StepArgs a) {
     float pt = 0.f;
     auto stage = [&](int t, const St& s) {
       tile[t] = s;
+      if (one_tile && static_cast<unsigned>(t - i0) < static_cast<unsigned>(nrows)) rows[t - i0] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
       pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
       svx += s.vx;
@@ -1001,6 +1037,7 @@ void flock_step_kernel(StepArgs a) {
         stage(t, load_state<DYN, UF64, VAR>(a, env0 + j0 + t));
     }
     if (j0 == 0) {
+      if (one_tile) __syncthreads();  // rows[] written by the staging threads
       if (lane < nrows) {
         const St ri = rows[lane];
         rx32 = static_cast<float>(ri.px);
@@ -1835,6 +1872,28 @@ static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// the drop-in step with its actions copied from the host into the kernel arguments
+template <bool UF64, bool CTRL>
+static hipError_t launch_step_uin(const StepArgs& a, hipStream_t s) {
+  const size_t bytes = (size_t)a.B * a.N * 2 * (UF64 ? 8 : 4);
+  if (bytes > (size_t)kUInlineBytes || a.N > a.T) return hipErrorInvalidValue;
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, false);
+  if (!CTRL && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
+  static std::atomic<uint64_t> attr{0};
+  if (const hipError_t e = max_lds_once(
+          reinterpret_cast<const void*>(&flock_step_kernel<true, UF64, CTRL, false, 0, 0, true>), attr, 160 * 1024);
+      e != hipSuccess)
+    return e;
+  StepArgsU p;
+  p.a = a;
+  p.a.u = nullptr;
+  p.a.u_inline = 0;
+  std::memcpy(p.u, a.u, bytes);
+  hipLaunchKernelGGL((flock_step_kernel<true, UF64, CTRL, false, 0, 0, true>), dim3(a.B * a.bpe), dim3(kThreads), lds,
+                     s, p);
+  return hipGetLastError();
+}
+
 bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch) {
   return K == kStepFusedK && !variant && !prefetch && kThreads / R >= K && N <= 65536;
 }
@@ -1842,6 +1901,10 @@ bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch) {
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if constexpr (DYN) {
+    if (a.u_inline) {
+      if (a.knn_idx || a.variant) return hipErrorInvalidValue;
+      return launch_step_uin<UF64, CTRL>(a, s);
+    }
     if (a.knn_idx) {
       if (a.variant || (a.prefetch && a.T <= 2 * kThreads && a.N > a.T) || kThreads / a.R < kStepFusedK)
         return hipErrorInvalidValue;

@@ -140,8 +140,10 @@ int fe_compute_helpers(fe_handle* h, int flags);
 int fe_step(fe_handle* h, const void* u, int flags);
 /* The drop-in env's step(u) (:91-109) as one launch and one wait, for small batches
  * where latency, not bandwidth, counts (FlockingRelativeEnv.step, N ~ 100-1000, B = 1).
- * u: (B,N,2) host actions, float32 or float64 (FE_U_F64); if page-locked (fe_host_alloc)
- * the kernel reads them in place, else they are copied first. u == NULL: no dynamics,
+ * u: (B,N,2) host actions, float32 or float64 (FE_U_F64). One env of at most one tile
+ * (N <= 512) whose actions fit 3 KiB (N <= 384 in float32, 192 in float64) passes them in
+ * the kernel arguments; otherwise page-locked ones (fe_host_alloc) are read by the kernel
+ * in place, others copied first. Either way u may be reused on return. u == NULL: no dynamics,
  * compute_helpers (:111-134) on the current state (reset's observation). Outputs, any of
  * them NULL (not computed): state_values (B,N,6) f32, network (B,N,N) f32, rewards (B)
  * f64 and controls (B,N,2) f64 = controller() (:194-212) of the resulting state (fused,

@@ -107,6 +107,19 @@ def test_collisions_and_blocking_order():
     h.close()
 
 
+def test_step_after_close_is_refused():
+    """A closed handle's resident and greedy steps (bound to the C handle object) pass NULL
+    and are refused with GF_EINVAL, never the freed handle (advisor r03)."""
+    f = np.load(EPISODES[0])
+    R, M = int(f["n_robots"]), int(f["max_nodes"])
+    h = nat.CoverageHandle(R, 1, M)
+    h.set_targets(f["targets"], env=0)
+    h.close()
+    for kw in ({"resident": True}, {"greedy": True}):
+        with pytest.raises(nat.GymFlockError):
+            h.step(**kw)
+
+
 def test_external_robot_positions_recompute_closest():
     f = np.load(EPISODES[0])
     R, T, M = int(f["n_robots"]), int(f["n_targets"]), int(f["max_nodes"])
