@@ -802,9 +802,6 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   // every such pair's float64 r2 to rank it, decides the adjacency exactly and writes the
   // exact words back, so every tile's feature pass runs before the network stores
   constexpr bool kSupK = KN > 0 && !CTRL;
-#ifndef GF_AB_CANDLOOP
-#define GF_AB_CANDLOOP 0
-#endif
   constexpr bool kSup = kOuter || kSupK;
   uint64_t* nearb = adj + (size_t)R * Wn;                      // R x Wt controller bits (KN && CTRL)
   uint64_t* candb = nearb + ((CTRL && !kOuter) ? (size_t)R * Wt : 0);  // (predicted rows) x Wt kNN candidates
@@ -978,28 +975,13 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
         // (the rare float32 superset pairs past comm_radius, and a predicted row's
         // candidates, whose bits may not be set) leaves the exact word; an LDS atomic
         // keeps it a branch that no wave enters unless one of its lanes has such a pair
-#if GF_AB_CANDLOOP
-        uint64_t m = am;
-#else
         uint64_t m = am | cm;
-#endif
         while (m) {
           const int k = __builtin_ctzll(m);
           m &= m - 1;
           if (!pair_terms(me, j0, (w << 6) + k, false, false, ksc))
             __hip_atomic_fetch_and(aw, ~(1ull << k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-#if GF_AB_CANDLOOP
-        // a predicted row's candidates outside the superset: never adjacent, only ranked
-        for (uint64_t mc = cm & ~am; mc; mc &= mc - 1) {
-          const int c = (w << 6) + __builtin_ctzll(mc);
-          const double2 o = *reinterpret_cast<const double2*>(&tile[c]);
-          const double dx = me.px - o.x, dy = me.py - o.y;
-          const double r2 = dx * dx + dy * dy;
-          const unsigned q = a.knn_qmax - gf_cvt_u32_sat(fma(-r2, ksc, a.knn_qmaxd));
-          knn_list_insert<KL>(kk, (q << a.knn_jbits) | static_cast<unsigned>(j0 + c));
-        }
-#endif
         continue;
       }
       const uint64_t nm = CTRL ? nearb[(size_t)fr * Wt + w] : 0ull;
