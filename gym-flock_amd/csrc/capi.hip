@@ -573,7 +573,7 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
 // kNN of the current state (mode: knn_mode; 0 = a full kNN with no step behind it):
 // 1: the last launch wrote this state's adjacency (packed outputs), which lets agents
 // with >= k neighbours rank only those; 2: the last launch ranked the rows it could.
-int launch_knn_cur(fe_handle* h, int mode) {
+int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs_to = nullptr) {
 #ifdef GF_DIAG
   if (mode == 2 && (h->diag & 0x80000)) {  // ablation: no rim kNN launch (timing only)
     h->has_knn = true;
@@ -585,8 +585,8 @@ int launch_knn_cur(fe_handle* h, int mode) {
   k.x = h->x[h->cur];
   k.adj_bits = mode == 1 ? h->adj_bits[h->bits_cur] : nullptr;
   k.degree = mode == 1 ? h->pdeg[h->bits_cur] : nullptr;
-  k.idx = h->knn_idx[h->cur];
-  k.obs = h->knn_obs[h->cur];
+  k.idx = idx_to ? idx_to : h->knn_idx[h->cur];
+  k.obs = obs_to ? obs_to : h->knn_obs[h->cur];
   k.rim = mode == 2;
   k.r2k = h->knn_r2[h->cur];
   k.rimflag = h->knn_rimflag[h->cur];
@@ -916,11 +916,15 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   return GF_OK;
 }
 
-int fe_step_host(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
-                 double* controls, int flags) {
+// fe_step_host and fe_step_host_knn: knn_idx / knn_obs (either non-NULL) also rank the new
+// state's k nearest (the fused selection, or the kNN kernel) and bring them back.
+static int step_host_impl(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                          double* controls, int32_t* knn_idx, float* knn_obs, int flags) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->has_state) return fail(GF_ESTATE, "state not set (call fe_set_state first)");
   if (flags & ~(FE_U_F64 | FE_WITH_CONTROLLER)) return fail(GF_EINVAL, "flags: FE_U_F64 and FE_WITH_CONTROLLER only");
+  const bool knn = knn_idx || knn_obs;
+  if (knn && h->cfg.n_neighbors <= 0) return fail(GF_EINVAL, "handle created with n_neighbors = 0");
   if (controls) flags |= FE_WITH_CONTROLLER;
   // one launch on the handle's stream, after all of its outstanding work
   if (int rc = use_dev(h)) return rc;
@@ -929,7 +933,7 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
   // one env of one tile: the actions travel in the kernel arguments (no read over the
   // link inside the kernel); otherwise page-locked actions are read in place, others
   // copied to the device first
-  const bool uin = dyn && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
+  const bool uin = dyn && !(knn && ctrl) && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
                    h->BN * 2 * (uf64 ? 8 : 4) <= (size_t)gf::kUInlineBytes;
   if (uin) {
     up = u;
@@ -960,7 +964,18 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
   a.ctrl_out = ctrl ? (ct_m ? ct_m : h->ctrl[h->ccur ^ 1]) : nullptr;
   a.reward = cur_reward(h);
   a.reward2 = rw_m;
-  if (int rc = prepare_outputs(h, 0, a, dyn ? h->cur ^ 1 : -1)) return rc;
+  const int kflags = knn ? FE_WITH_KNN : 0, km = knn_mode(h, kflags, dyn);
+  if (int rc = prepare_outputs(h, kflags, a, dyn ? h->cur ^ 1 : -1)) return rc;
+  // fused selection with both destinations page-locked: the step and its rim kNN write
+  // the rows straight into them (the device's kNN buffers of this state are then not
+  // written: fe_get_knn recomputes them if asked)
+  int32_t* idx_m = knn_idx ? static_cast<int32_t*>(mapped_ptr(knn_idx)) : nullptr;
+  float* obs_m = knn_obs ? static_cast<float*>(mapped_ptr(knn_obs)) : nullptr;
+  const bool kdirect = km == 2 && idx_m && obs_m;
+  if (kdirect) {
+    a.knn_idx = idx_m;
+    a.knn_obs = obs_m;
+  }
   if (int rc = timed_launch(h, a, dyn, uf64, ctrl)) return rc;
   if (dyn) h->cur ^= 1;
   const size_t nsv = h->BN * 6, nnet = h->BN * (size_t)h->cfg.n_agents, nct = h->BN * 2;
@@ -977,6 +992,34 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
   h->has_obs = true;
   h->obs_on_host = sv_m || net_m;
   h->has_knn = false;
+  if (knn) {
+    // the rim (or whole) kNN of the new state, then its rows to the host: page-locked
+    // destinations by one copy kernel through their mapped addresses (a DMA copy costs
+    // ~12 us of latency each), others by copies
+    if (int rc = launch_knn_cur(h, km, kdirect ? idx_m : nullptr, kdirect ? obs_m : nullptr)) return rc;
+    if (int rc = join_s2(h)) return rc;
+    if (int rc = join_k(h)) return rc;
+    if (kdirect) {
+      h->has_knn = false;
+      knn_idx = nullptr;
+      knn_obs = nullptr;
+    }
+    const size_t nk = h->BN * (size_t)h->cfg.n_neighbors;
+    OutCopy c{};
+    c.src[0] = reinterpret_cast<const float*>(h->knn_idx[h->cur]);
+    c.src[1] = h->knn_obs[h->cur];
+    c.n[0] = nk;
+    c.n[1] = 4 * nk;
+    if (knn_idx && (c.dst[0] = static_cast<float*>(mapped_ptr(knn_idx)))) knn_idx = nullptr;
+    if (knn_obs && (c.dst[1] = static_cast<float*>(mapped_ptr(knn_obs)))) knn_obs = nullptr;
+    if (c.dst[0] || c.dst[1]) {
+      const int grid = static_cast<int>(std::min<size_t>((nk + 255) / 256, 1024));
+      hipLaunchKernelGGL(out_copy_kernel, dim3(grid), dim3(256), 0, h->stream, c);
+      GF_HIP(hipGetLastError());
+    }
+    if (knn_idx) GF_HIP(hipMemcpyAsync(knn_idx, h->knn_idx[h->cur], nk * 4, hipMemcpyDeviceToHost, h->stream));
+    if (knn_obs) GF_HIP(hipMemcpyAsync(knn_obs, h->knn_obs[h->cur], nk * 16, hipMemcpyDeviceToHost, h->stream));
+  }
   // spin on the stream: the drop-in step is latency-bound (tens of us), and a blocking
   // wait's wake-up costs a sizeable part of that
   for (;;) {
@@ -985,6 +1028,18 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
     if (q != hipErrorNotReady) return fail_hip("fe_step_host", q);
   }
   return GF_OK;
+}
+
+int fe_step_host(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                 double* controls, int flags) {
+  return step_host_impl(h, u, state_values, network, rewards, controls, nullptr, nullptr, flags);
+}
+
+int fe_step_host_knn(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                     int32_t* knn_idx, float* knn_obs, int flags) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!knn_idx && !knn_obs) return fail(GF_EINVAL, "knn_idx and knn_obs both NULL (use fe_step_host)");
+  return step_host_impl(h, u, state_values, network, rewards, nullptr, knn_idx, knn_obs, flags);
 }
 
 int fe_set_variant(fe_handle* h, const fe_variant* v) {

@@ -1855,15 +1855,15 @@ static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
 }
 
 // the drop-in step with its actions copied from the host into the kernel arguments
-template <bool UF64, bool CTRL>
+template <bool UF64, bool CTRL, int KN = 0>
 static hipError_t launch_step_uin(const StepArgs& a, hipStream_t s) {
   const size_t bytes = (size_t)a.B * a.N * 2 * (UF64 ? 8 : 4);
   if (bytes > (size_t)kUInlineBytes || a.N > a.T) return hipErrorInvalidValue;
-  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, false);
-  if (!CTRL && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
+  size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0);
+  if (!CTRL && KN == 0 && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
   static std::atomic<uint64_t> attr{0};
   if (const hipError_t e = max_lds_once(
-          reinterpret_cast<const void*>(&flock_step_kernel<true, UF64, CTRL, false, 0, 0, true>), attr, 160 * 1024);
+          reinterpret_cast<const void*>(&flock_step_kernel<true, UF64, CTRL, false, 0, KN, true>), attr, 160 * 1024);
       e != hipSuccess)
     return e;
   StepArgsU p;
@@ -1871,7 +1871,7 @@ static hipError_t launch_step_uin(const StepArgs& a, hipStream_t s) {
   p.a.u = nullptr;
   p.a.u_inline = 0;
   std::memcpy(p.u, a.u, bytes);
-  hipLaunchKernelGGL((flock_step_kernel<true, UF64, CTRL, false, 0, 0, true>), dim3(a.B * a.bpe), dim3(kThreads), lds,
+  hipLaunchKernelGGL((flock_step_kernel<true, UF64, CTRL, false, 0, KN, true>), dim3(a.B * a.bpe), dim3(kThreads), lds,
                      s, p);
   return hipGetLastError();
 }
@@ -1884,7 +1884,14 @@ template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if constexpr (DYN) {
     if (a.u_inline) {
-      if (a.knn_idx || a.variant) return hipErrorInvalidValue;
+      if (a.variant) return hipErrorInvalidValue;
+      if (a.knn_idx) {  // the drop-in Flocking-v0 step (fe_step_host_knn), no controller
+        if constexpr (CTRL) return hipErrorInvalidValue;
+        else {
+          if (kThreads / a.R < kStepFusedK) return hipErrorInvalidValue;
+          return launch_step_uin<UF64, CTRL, kStepFusedK>(a, s);
+        }
+      }
       return launch_step_uin<UF64, CTRL>(a, s);
     }
     if (a.knn_idx) {

@@ -88,6 +88,7 @@ SIGNATURES = {
     "fe_compute_helpers": [_P, _I],
     "fe_step": [_P, _P, _I],
     "fe_step_host": [_P, _P, _P, _P, _P, _P, _I],
+    "fe_step_host_knn": [_P, _P, _P, _P, _P, _P, _P, _I],
     "fe_controller": [_P, _I, _P],
     "fe_get_stats": [_P, _I, _P, _P],
     "fe_get_stats_ex": [_P, _I, _P, _P, _P],
@@ -450,6 +451,14 @@ class FlockHandle:
         ctrl: addresses of host destinations or None (page-locked ones are written by the
         kernel directly). Addresses are ints (the drop-in env passes pool addresses)."""
         rc = self.lib.fe_step_host(self.h, u_addr, sv, net, rew, ctrl, FE_U_F64 if f64 else 0)
+        if rc:
+            check(rc)
+
+    def step_host_knn(self, u_addr, f64, sv, net, rew, idx, obs):
+        """fe_step_host_knn: step_host plus the new state's k nearest (addresses of host
+        destinations, page-locked ones written in place; any may be None but not both
+        idx and obs)."""
+        rc = self.lib.fe_step_host_knn(self.h, u_addr, sv, net, rew, idx, obs, FE_U_F64 if f64 else 0)
         if rc:
             check(rc)
 

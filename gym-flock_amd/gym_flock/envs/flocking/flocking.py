@@ -18,16 +18,61 @@ class FlockingEnv(FlockingRelativeEnv):
         self.n_neighbors = 7
         self.n_f = self.nx_system * self.n_neighbors
         self.nearest = None
+        self._obs = None  # the last step's observation rows, fetched with it ("direct")
+        self._klayout = None
+
+    def _invalidate(self):
+        super(FlockingEnv, self)._invalidate()
+        self._obs = None
+
+    def _device_step(self, u):
+        super(FlockingEnv, self)._device_step(u)
+        self._obs = None
 
     def step(self, u):
-        """:12-14."""
+        """:12-14. In the default fetch mode ("direct") one library call with one wait
+        (fe_step_host_knn): the step with the k-nearest selection fused in, the rim kNN,
+        and every output (state_values, network, reward, the neighbour rows and indices)
+        written into one pooled page-locked block."""
         u = np.asarray(u)
         assert u.shape == (self.n_agents, self.nu)
         self.u = u * self.action_scalar
-        self._handle().step(u[None], flags=nat.FE_WITH_KNN)
+        if self.fetch_mode != "direct":
+            self._handle().step(u[None], flags=nat.FE_WITH_KNN)
+            self._ctrl_cache = None
+            self._fetch_obs()
+            return (self.get_observation(), self.state_network), self.instant_cost(), False, {}
+        h = self._handle()
+        n, k = self.n_agents, self.n_neighbors
+        f64 = nat.u_is_f64(u)
+        dt = np.float64 if f64 else np.float32
+        if self._ubuf is None or self._ubuf.a.dtype != dt:
+            self._ubuf = nat.PinnedArray((n, 2), dt)  # read by the kernel in place
+        self._ubuf.a[...] = u
+        lay = self._klayout
+        if lay is None or lay[0] != (n, k):
+            a64 = lambda b: (b + 63) & ~63  # noqa: E731
+            o_ix = a64(4 * n * n)
+            o_ob = o_ix + a64(4 * n * k)
+            o_rw = o_ob + a64(16 * n * k)
+            o_sv = o_rw + 64
+            lay = self._klayout = ((n, k), o_ix, o_ob, o_rw, o_sv, o_sv + 24 * n)
+        _, o_ix, o_ob, o_rw, o_sv, size = lay
+        buf, base = nat.host_pool().block_addr(size)
+        if buf is None:  # not page-locked (pool cap): the library copies after the launch
+            buf = np.empty(size, np.uint8)
+            base = buf.ctypes.data
+        net = np.ndarray((n, n), np.float32, buf)
+        idx = np.ndarray((n, k), np.int32, buf, o_ix)
+        obs = np.ndarray((n, 4 * k), np.float32, buf, o_ob)
+        rw = np.ndarray((1,), np.float64, buf, o_rw)
+        sv = np.ndarray((n, 6), np.float32, buf, o_sv)
+        h.step_host_knn(self._ubuf.addr, f64, base + o_sv, base, base + o_rw, base + o_ix, base + o_ob)
         self._ctrl_cache = None
-        self._fetch_obs()
-        return (self.get_observation(), self.state_network), self.instant_cost(), False, {}
+        self.state_values, self.state_network = sv, net
+        self._reward = float(rw[0])
+        self.nearest, self._obs = idx, obs
+        return (obs, net), self._reward, False, {}
 
     def reset(self):
         """:16-18."""
@@ -36,6 +81,8 @@ class FlockingEnv(FlockingRelativeEnv):
 
     def get_observation(self):
         """:20-25 — (N, 4*n_neighbors) float32: x_i - x_{nn_k(i)} for k < n_neighbors."""
+        if self._obs is not None:  # fetched with the step that made this state
+            return self._obs
         idx, obs = self._handle().knn(0)
         self.nearest = idx
         return obs

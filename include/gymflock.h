@@ -154,6 +154,16 @@ int fe_step(fe_handle* h, const void* u, int flags);
  * path). flags: FE_U_F64, FE_WITH_CONTROLLER. */
 int fe_step_host(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
                  double* controls, int flags);
+/* Flocking-v0's drop-in step(u) (flocking.py:12-25 over flocking_relative.py:91-109) as
+ * one call and one wait: fe_step_host (no controller) plus the new state's k nearest
+ * neighbours (the selection fused into the step, or the kNN kernel), written to knn_idx
+ * (B,N,K) int32 and knn_obs (B,N,4K) float32 (either may be NULL, not both): page-locked
+ * destinations through their mapped addresses (both page-locked: the step and its rim
+ * kNN write the rows there directly; otherwise one copy kernel or copies). Needs
+ * n_neighbors > 0. Afterwards fe_get_knn returns the same rows (recomputed on the device
+ * when they were written straight to the host). */
+int fe_step_host_knn(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                     int32_t* knn_idx, float* knn_obs, int flags);
 /* controller(centralized) (:194-212) on the current state; centralized < 0 means the
  * config default. Writes (B,N,2) float64 to u_out (host) if non-NULL. */
 int fe_controller(fe_handle* h, int centralized, double* u_out);

@@ -403,6 +403,49 @@ def test_flocking_v0_env_api():
     env.close()
 
 
+@pytest.mark.parametrize("n,f64", [(100, False), (300, True)])
+def test_flocking_v0_dropin_direct_matches_oracle(n, f64):
+    """Flocking-v0's drop-in step in the default fetch mode: one fe_step_host_knn call
+    returns the neighbour rows, indices, network and reward of the new state. Against the
+    oracle (indices bit-exact, observation rows as float32 of the float64 differences,
+    network bit-exact) over several steps, and equal to the pooled mode's getters."""
+    from gym_flock.envs.flocking.flocking import FlockingEnv
+    from gym_flock.init_states import synthetic_state
+    envs = []
+    for mode in ("direct", "pooled"):
+        env = FlockingEnv()
+        env.n_agents = n
+        env._make_spaces()
+        env.fetch_mode = mode
+        env.x = synthetic_state(n, 4)
+        env.compute_helpers()
+        envs.append(env)
+    rs = np.random.RandomState(12)
+    for t in range(5):
+        x = envs[0].x
+        u = rs.uniform(-1, 1, size=(n, 2))
+        u = u if f64 else u.astype(np.float32)
+        (obs, net), r, done, _ = envs[0].step(u)
+        (obs_p, net_p), r_p, _, _ = envs[1].step(u)
+        ref = orc.step(x, u)
+        ridx, robs = orc.knn_observation(ref["x"])
+        np.testing.assert_array_equal(envs[0].x, ref["x"])
+        np.testing.assert_array_equal(envs[0].nearest, ridx)
+        np.testing.assert_array_equal(obs, robs.astype(np.float32))
+        np.testing.assert_array_equal(net, ref["network"].astype(np.float32))
+        np.testing.assert_allclose(r, ref["reward"], rtol=1e-12)
+        np.testing.assert_array_equal(obs, obs_p)
+        np.testing.assert_array_equal(envs[0].nearest, envs[1].nearest)
+        np.testing.assert_array_equal(net, net_p)
+        assert r == r_p
+        np.testing.assert_array_equal(envs[0].get_observation(), obs)  # the fetched rows, no relaunch
+    idx, kobs = envs[0]._handle().knn(0)  # fe_get_knn after fe_step_host_knn: the same rows
+    np.testing.assert_array_equal(idx, envs[0].nearest)
+    np.testing.assert_array_equal(kobs, obs)
+    for env in envs:
+        env.close()
+
+
 def test_config5_size_sampled_rows():
     """N=8192 (BASELINE.json configs[4]'s agent count; 16-row blocks, 16 LDS tiles per
     row sweep): the whole state and reward, and 40 sampled rows of the network,
