@@ -23,6 +23,7 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 constexpr int kInlineRimU = 4;      // fused kNN inline rim scan: columns in flight per lane
 constexpr int kStoreTab = 16;      // network rows: float4 table entries per wave (one per nibble)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
+constexpr int kStepInlineRimSmallN = 128;  // ... and every unranked row in envs up to this size
 constexpr int kKnnRimGrid = 256;     // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnRimHalfGrid = kKnnRimGrid / 2;  // the same per half-batch launch
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are

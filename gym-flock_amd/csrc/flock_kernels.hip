@@ -1379,7 +1379,9 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
     // (an exact scan of the env, as the rim kernel's few-rows path); more go to the rim
     // kernel (idx = -1, block flagged)
     // diag 0x40000: every such row to the rim kernel (timing only)
-    const bool inl = __popcll(__ballot(frow && slow && fs == 0)) <= kStepInlineRim && !GF_ABLATE(a, 0x40000);
+    // (an env of at most kStepInlineRimSmallN agents: any number, its scans are short)
+    const int ilim = N <= kStepInlineRimSmallN ? 64 : kStepInlineRim;
+    const bool inl = __popcll(__ballot(frow && slow && fs == 0)) <= ilim && !GF_ABLATE(a, 0x40000);
     if (frow) {
       const size_t g = env0 + i_row;
       if (slow) {
