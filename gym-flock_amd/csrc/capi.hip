@@ -581,6 +581,14 @@ int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs
   }
 #endif
   auto& r = h->kread[h->cur];
+  if (mode == 2 && h->cfg.n_agents <= gf::kStepInlineRimSmallN && !(h->diag & 0x40000)) {
+    // envs this small: the fused step ranks every row itself (inline scans), none is
+    // left to the rim kernel, so it is not launched
+    r.live = false;
+    r.bmask = 0;
+    h->has_knn = true;
+    return GF_OK;
+  }
   gf::KnnArgs k{};
   k.x = h->x[h->cur];
   k.adj_bits = mode == 1 ? h->adj_bits[h->bits_cur] : nullptr;
