@@ -399,11 +399,29 @@ def bench_dropin(args):
             cpu.step(cpu.controller())
         t_ctrl = (time.perf_counter() - t0) / k
         row["cpu_ref_1core"] = {"step_ms": 1e3 * t_step, "controller_plus_step_ms": 1e3 * t_ctrl}
+        # Flocking-v0's drop-in step (flocking.py:12-25): the observation is the 7-nearest
+        # rows; "direct" (default) is one fe_step_host_knn call, "pooled" the older form
+        from gym_flock.envs.flocking.flocking import FlockingEnv
+        for mode in ("pooled", "direct"):
+            env = FlockingEnv()
+            env.n_agents = n
+            env._make_spaces()
+            env.fetch_mode = mode
+            env.x = x0
+            env.compute_helpers()
+            for _ in range(20):
+                env.step(u32)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                env.step(u32)
+            row["flocking_v0_" + mode] = {"step_ms": 1e3 * (time.perf_counter() - t0) / iters}
+            env.close()
         out["n%d" % n] = row
     out["note"] = ("one env per FlockingRelativeEnv object, float32 host actions for step_ms, float64 controller() "
                    "output for controller_plus_step_ms; outputs copied to fresh host arrays every call, as the "
                    "reference returns them; the env default is fetch_mode='direct' (one launch and one wait per "
-                   "step, the expert action of the new state fused into it)")
+                   "step, the expert action of the new state fused into it); flocking_v0_*: FlockingEnv.step(u) (Flocking-v0, "
+                   "7-nearest observation), 'direct' = one fe_step_host_knn call")
     return out
 
 
