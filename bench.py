@@ -402,6 +402,9 @@ def bench_dropin(args):
         # Flocking-v0's drop-in step (flocking.py:12-25): the observation is the 7-nearest
         # rows; "direct" (default) is one fe_step_host_knn call, "pooled" the older form
         from gym_flock.envs.flocking.flocking import FlockingEnv
+        w = int(np.ceil(np.sqrt(n)))
+        lattice = np.zeros((n, 4))  # an exact lattice at rest: every row's r2 tied, every step
+        lattice[:, :2] = np.stack(np.meshgrid(np.arange(w), np.arange(w)), -1).reshape(-1, 2)[:n] * 0.5
         for mode in ("pooled", "direct"):
             env = FlockingEnv()
             env.n_agents = n
@@ -409,19 +412,45 @@ def bench_dropin(args):
             env.fetch_mode = mode
             env.x = x0
             env.compute_helpers()
-            for _ in range(20):
-                env.step(u32)
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                env.step(u32)
-            row["flocking_v0_" + mode] = {"step_ms": 1e3 * (time.perf_counter() - t0) / iters}
+
+            def v0_plain(k):
+                for _ in range(k):
+                    env.step(u32)
+
+            def v0_expert(k):
+                for _ in range(k):
+                    env.step(env.controller())
+
+            r = {}
+            for name, fn in (("step_ms", v0_plain), ("controller_plus_step_ms", v0_expert)):
+                fn(20)
+                t0 = time.perf_counter()
+                fn(iters)
+                r[name] = 1e3 * (time.perf_counter() - t0) / iters
             env.close()
+            if mode == "direct":
+                env = FlockingEnv()
+                env.n_agents = n
+                env._make_spaces()
+                env.x = lattice
+                env.compute_helpers()
+                z = np.zeros((n, 2), np.float32)
+                for _ in range(20):
+                    env.step(z)
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    env.step(z)
+                r["lattice_at_rest_step_ms"] = 1e3 * (time.perf_counter() - t0) / iters
+                env.close()
+            row["flocking_v0_" + mode] = r
         out["n%d" % n] = row
     out["note"] = ("one env per FlockingRelativeEnv object, float32 host actions for step_ms, float64 controller() "
                    "output for controller_plus_step_ms; outputs copied to fresh host arrays every call, as the "
                    "reference returns them; the env default is fetch_mode='direct' (one launch and one wait per "
                    "step, the expert action of the new state fused into it); flocking_v0_*: FlockingEnv.step(u) (Flocking-v0, "
-                   "7-nearest observation), 'direct' = one fe_step_host_knn call")
+                   "7-nearest observation), 'direct' = one fe_step_host_knn(_ctrl) call (the expert action fused "
+                   "once controller() is in use); lattice_at_rest: an exact lattice (spacing 0.5) with zero "
+                   "velocities and actions, every row's r2 tied every step")
     return out
 
 
@@ -885,10 +914,15 @@ def main():
                                    % (N, B, CONFIG_TAG.get((N, B, world), "")),
                        "n_agents": N, "envs_per_gpu": B, "global_envs": world * B,
                        "outputs": "network (N,N) f32 + state_values (N,6) f32 + reward, in HBM",
-                       "parallelism": "env-sharded dp%d, RCCL reward all-gather" % world},
+                       "parallelism": (("env-sharded dp%d, RCCL reward all-gather of every step, one collective "
+                                        "per %d steps" % (world, args.metrics_every)) if gather is not None else
+                                       "env-sharded dp%d, no collective ran (one rank: the reward all-gather "
+                                       "runs at N>1 or with --force-dist)" % world)},
             "roofline": flock_roofline(N, B, kernel_ms, 2 if B >= 2 else 1),
         }
         line.update(extra)
+        from gym_flock import _native as nat
+        line["runtime"] = nat.runtime_info()  # the HIP runtime and RCCL this process measured on
         if world == 1 and not args.no_other_configs:
             log("config 4 (Coverage R=200 x 512)...")
             line["coverage_config4"] = bench_config4(args)
@@ -896,7 +930,9 @@ def main():
             line["n8192_config5"] = bench_config5(args)
             log("drop-in single-env path (N=100, 1024)...")
             line["dropin"] = bench_dropin(args)
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
+            # rank 0 after the timed region (the other ranks are done stepping): the same
+            # host-core baseline beside every world size's line
             log("cpu baseline (cpu_ref, 1 core, ~%.0fs)..." % args.cpu_seconds)
             line["cpu_baseline"] = flock_cpu_baseline(N, args.cpu_seconds, args.cpu_procs or None)
         print(json.dumps(line), flush=True)

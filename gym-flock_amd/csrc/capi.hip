@@ -2,11 +2,15 @@
 // stream-ordered launches, host transfers, RCCL metrics path and error reporting.
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <atomic>
+#include <condition_variable>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -119,13 +123,26 @@ struct fe_handle {
   int max_envs = 0;
   std::vector<int32_t> shard_sizes;     // every rank's n_envs (fe_comm_init's exchange)
   double comm_timeout = kCommInitTimeoutS;  // bound on every wait for a collective
-  double* gsend = nullptr;              // kRewardSlots x max_envs: the gathered steps, padded
+  // The staging copies into the send blocks run on stage_stream, which waits only for the
+  // step streams, never for a collective: the ring slots a step overwrites are therefore
+  // released by the steps' own progress, and a collective stuck on a dead peer cannot
+  // hold the step streams (they wait only on staging events). A send block is reused
+  // only after the host has seen (bounded, comm_event_wait) the collective that read it
+  // complete; the reward send block is double-buffered so that this is the collective
+  // two gathers back.
+  hipStream_t stage_stream = nullptr;
+  double* gsend[2] = {nullptr, nullptr};  // kRewardSlots x max_envs each: the gathered steps, padded
+  hipEvent_t ag_done[2] = {nullptr, nullptr};  // the reward collective that read gsend[k]
+  bool ag_live[2] = {false, false};
+  int64_t n_gathers = 0;                // reward gathers issued (send block = count % 2)
+  hipEvent_t stage_ev = nullptr;        // the latest staging copy (the collective waits for it)
   double* gather = nullptr;             // nranks x kRewardSlots x max_envs
   hipEvent_t step_ev = nullptr;
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
   hipEvent_t ag_ev = nullptr;           // completion of the latest reward all-gather
   // ring slots a reward gather's staging copy still reads: steps [first, ...) until ev
+  // (an event on stage_stream)
   struct RingRead {
     int64_t first;
     hipEvent_t ev;
@@ -140,6 +157,11 @@ struct fe_handle {
   double* stats_gather = nullptr;       // nranks x max_envs x 2 (fe_allgather_stats)
   hipEvent_t sg_ev = nullptr;           // completion of the latest stats all-gather
   bool sg_pending = false;
+  hipEvent_t ss_copy_ev = nullptr;      // stats_sum -> ssend staging copy (stage_stream)
+  bool ss_copy_pending = false;
+  // fe_debug_comm_gate: a bounded spin kernel on comm_stream, released by this page-locked
+  // flag, stands in for a collective whose peer stopped responding (tests only)
+  unsigned* gate_flag = nullptr;
   // flocking variant (fe_set_variant / fe_set_dt)
   bool has_variant = false;
   fe_variant var{};
@@ -285,39 +307,116 @@ int dalloc(T** p, size_t count) {
   return GF_OK;
 }
 
+// ---- the process's communicator worker
+// ncclCommAbort runs on one thread per process that lives until the process exits (never
+// on a short-lived thread: RCCL's own threads may keep using the HIP thread-local state of
+// the thread that called into it, and a thread that exited under them corrupted the heap
+// once torch's HIP runtime was bound). The worker and its queue are never
+// destroyed, so the thread outlives static destruction.
+struct CommWorker {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<ncclComm_t, int>> q;  // (communicator, device)
+};
+
+CommWorker* comm_worker() {
+  static CommWorker* w = [] {
+    auto* p = new CommWorker();
+    std::thread([p] {
+      for (;;) {
+        std::pair<ncclComm_t, int> job;
+        {
+          std::unique_lock<std::mutex> l(p->mu);
+          p->cv.wait(l, [p] { return !p->q.empty(); });
+          job = p->q.front();
+          p->q.pop_front();
+        }
+        hipSetDevice(job.second);
+        ncclCommAbort(job.first);
+      }
+    }).detach();
+    return p;
+  }();
+  return w;
+}
+
+void abort_comm_later(ncclComm_t c, int device) {
+  CommWorker* w = comm_worker();
+  {
+    std::lock_guard<std::mutex> l(w->mu);
+    w->q.emplace_back(c, device);
+  }
+  w->cv.notify_one();
+}
+
+// A thread that called into RCCL's initialisation parks here for the rest of the process
+// instead of exiting (the same thread-local-state reason as the worker above).
+[[noreturn]] void park_thread() {
+  static std::mutex* m = new std::mutex();
+  static std::condition_variable* cv = new std::condition_variable();
+  std::unique_lock<std::mutex> l(*m);
+  for (;;) cv->wait(l);
+}
+
+using Clock = std::chrono::steady_clock;
+
+Clock::time_point deadline_in(double seconds) {
+  return Clock::now() + std::chrono::microseconds(static_cast<int64_t>(seconds * 1e6));
+}
+
+// Every collective on the side stream complete, polled against the collective timeout and
+// the communicator's async error; false when it expired (a peer stopped responding).
+bool comm_stream_drained(fe_handle* h) {
+  if (!h->comm_stream) return true;
+  const auto deadline = deadline_in(h->comm_timeout);
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipStreamQuery(h->comm_stream);
+    if (q != hipErrorNotReady) return q == hipSuccess;
+    ncclResult_t st = ncclSuccess;
+    if (h->comm && (ncclCommGetAsyncError(h->comm, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)))
+      return false;
+    if (Clock::now() > deadline) return false;
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 // Tear down the metrics path: the communicator (aborted when a collective may never
 // complete, else destroyed once the side stream has drained) and everything fe_comm_init
 // made for it, so that a later fe_comm_init starts from scratch.
 //
 // abort: a collective (or the initialisation) may never finish because a peer is gone.
-// The communicator is then aborted on a detached thread, and its side stream, events and
-// buffers are abandoned rather than synchronised or freed (a kernel of the aborted
-// collective may still touch them), so that this call cannot hang; the step streams never
-// wait on the side stream's collectives (only on its staging copies, which complete).
+// The communicator is then aborted on the process's communicator worker, and the side
+// stream, the events it waits on and the buffers its collectives use are abandoned
+// rather than synchronised or freed (a kernel of the aborted collective may still touch
+// them), so that this call cannot hang. The staging stream is drained and released: it
+// waits only for the step streams, never for a collective. A non-abort release whose
+// side stream does not drain within the collective timeout becomes an abort.
 void comm_release(fe_handle* h, bool abort) {
+  if (!abort && h->comm && !comm_stream_drained(h)) abort = true;
   if (abort) {
-    if (h->comm) {
-      ncclComm_t c = h->comm;
-      std::thread([c] { ncclCommAbort(c); }).detach();
-    }
+    if (h->comm) abort_comm_later(h->comm, h->cfg.device);
     h->comm = nullptr;
     h->comm_stream = nullptr;
-    h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = nullptr;
-    h->ring_reads.clear();
-    h->ev_free.clear();
-    h->gsend = h->gather = h->ssend = h->stats_gather = nullptr;
+    h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = h->stage_ev = nullptr;
+    h->ag_done[0] = h->ag_done[1] = nullptr;
+    h->gsend[0] = h->gsend[1] = h->gather = h->ssend = h->stats_gather = nullptr;
   }
   if (h->comm) {
-    if (h->comm_stream) hipStreamSynchronize(h->comm_stream);
     ncclCommDestroy(h->comm);
     h->comm = nullptr;
   }
   if (h->comm_stream) {
-    hipStreamSynchronize(h->comm_stream);
+    hipStreamSynchronize(h->comm_stream);  // drained above
     hipStreamDestroy(h->comm_stream);
     h->comm_stream = nullptr;
   }
-  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev})
+  if (h->stage_stream) {
+    hipStreamSynchronize(h->stage_stream);  // behind the step streams only
+    hipStreamDestroy(h->stage_stream);
+    h->stage_stream = nullptr;
+  }
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev, &h->stage_ev, &h->ss_copy_ev,
+                        &h->ag_done[0], &h->ag_done[1]})
     if (*e) {
       hipEventDestroy(*e);
       *e = nullptr;
@@ -326,12 +425,14 @@ void comm_release(fe_handle* h, bool abort) {
   h->ring_reads.clear();
   for (hipEvent_t e : h->ev_free) hipEventDestroy(e);
   h->ev_free.clear();
-  for (double** p : {&h->gsend, &h->gather, &h->ssend, &h->stats_gather})
+  for (double** p : {&h->gsend[0], &h->gsend[1], &h->gather, &h->ssend, &h->stats_gather})
     if (*p) {
       hipFree(*p);
       *p = nullptr;
     }
-  h->ag_issued = h->sg_pending = false;
+  h->ag_issued = h->sg_pending = h->ss_copy_pending = false;
+  h->ag_live[0] = h->ag_live[1] = false;
+  h->n_gathers = 0;
   h->last_count = 0;
   h->nranks = 1;
   h->rank = 0;
@@ -371,7 +472,9 @@ double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h-
 
 // Advance the reward ring before a launch that writes rewards. The slot last held the
 // step kRewardSlots launches back; if a reward gather's staging copy may still read it,
-// both step streams wait for that copy first (a device-side wait, no host sync).
+// both step streams wait for that copy first (a device-side wait, no host sync). The copy
+// runs on the staging stream behind the steps it reads and nothing else, so this wait
+// can never be held by a collective.
 int next_reward_slot(fe_handle* h) {
   const int64_t s = h->steps_written;
   h->rslot = static_cast<int>(s % kRewardSlots);
@@ -581,9 +684,9 @@ int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs
   }
 #endif
   auto& r = h->kread[h->cur];
-  if (mode == 2 && h->cfg.n_agents <= gf::kStepInlineRimSmallN && !(h->diag & 0x40000)) {
-    // envs this small: the fused step ranks every row itself (inline scans), none is
-    // left to the rim kernel, so it is not launched
+  if (mode == 2 && gf::step_knn_exact(h->cfg.n_agents, h->T)) {
+    // envs this small: the fused step ranks every row exactly itself (KX), none is left
+    // to the rim kernel, so it is not launched
     r.live = false;
     r.bmask = 0;
     h->has_knn = true;
@@ -774,6 +877,25 @@ int fe_get_config(const fe_handle* h, fe_config* out) {
   return GF_OK;
 }
 
+int fe_set_params(fe_handle* h, const fe_config* cfg) {
+  if (!h || !cfg) return fail(GF_EINVAL, "null argument");
+  if (cfg->n_agents != h->cfg.n_agents || cfg->n_envs != h->cfg.n_envs || cfg->n_neighbors != h->cfg.n_neighbors ||
+      cfg->device != h->cfg.device)
+    return fail(GF_EINVAL, "fe_set_params: n_agents, n_envs, n_neighbors and device are fixed at fe_create");
+  if (!(cfg->comm_radius > 0) || !(cfg->action_scalar != 0)) return fail(GF_EINVAL, "bad comm_radius/action_scalar");
+  // every launch reads these from the handle's config; later steps (after the work already
+  // enqueued) use the new values. The kNN radius history was taken under the old radius:
+  // forgotten (it only steers which rows the fused step ranks beyond their neighbours)
+  if (int rc = use_dev(h)) return rc;
+  GF_HIP(clear_knn_history(h));
+  h->cfg.comm_radius = cfg->comm_radius;
+  h->cfg.dt = cfg->dt;
+  h->cfg.action_scalar = cfg->action_scalar;
+  h->cfg.mean_pooling = cfg->mean_pooling;
+  h->cfg.centralized = cfg->centralized;
+  return GF_OK;
+}
+
 int fe_set_state(fe_handle* h, const double* x) {
   if (!h || !x) return fail(GF_EINVAL, "null argument");
   if (int rc = use_dev(h)) return rc;
@@ -941,7 +1063,9 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
   // one env of one tile: the actions travel in the kernel arguments (no read over the
   // link inside the kernel); otherwise page-locked actions are read in place, others
   // copied to the device first
-  const bool uin = dyn && !(knn && ctrl) && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
+  // (the fused kNN step with the controller has an inline-actions form only for envs
+  // ranked exactly in the step, gf::step_knn_exact)
+  const bool uin = dyn && !(knn && ctrl && !gf::step_knn_exact(h->cfg.n_agents, h->T)) && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
                    h->BN * 2 * (uf64 ? 8 : 4) <= (size_t)gf::kUInlineBytes;
   if (uin) {
     up = u;
@@ -1050,6 +1174,13 @@ int fe_step_host_knn(fe_handle* h, const void* u, float* state_values, float* ne
   return step_host_impl(h, u, state_values, network, rewards, nullptr, knn_idx, knn_obs, flags);
 }
 
+int fe_step_host_knn_ctrl(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                          double* controls, int32_t* knn_idx, float* knn_obs, int flags) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!knn_idx && !knn_obs) return fail(GF_EINVAL, "knn_idx and knn_obs both NULL (use fe_step_host)");
+  return step_host_impl(h, u, state_values, network, rewards, controls, knn_idx, knn_obs, flags);
+}
+
 int fe_set_variant(fe_handle* h, const fe_variant* v) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!v) {
@@ -1132,8 +1263,9 @@ int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists,
 
 namespace {
 // get_stats (:136-143) on every env of the current state, then each env's means of the
-// two arrays into stats_sum (B,2), on the handle's stream. A pending stats all-gather
-// still reads stats_sum: the stream waits for it first.
+// two arrays into stats_sum (B,2), on the handle's stream. A pending stats gather's
+// staging copy still reads stats_sum: the stream waits for that copy first (on the
+// staging stream, behind the step streams only: never behind a collective).
 int stats_summary_dev(fe_handle* h) {
   if (!h->vel_diffs) {
     if (int rc = dalloc(&h->vel_diffs, h->BN)) return rc;
@@ -1142,7 +1274,10 @@ int stats_summary_dev(fe_handle* h) {
   }
   if (!h->stats_sum)
     if (int rc = dalloc(&h->stats_sum, (size_t)h->cfg.n_envs * 2)) return rc;
-  if (h->sg_pending) GF_HIP(hipStreamWaitEvent(h->stream, h->sg_ev, 0));
+  if (h->ss_copy_pending) {
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ss_copy_ev, 0));
+    h->ss_copy_pending = false;
+  }
   gf::StatsArgs s{h->x[h->cur], h->vel_diffs, h->min_dists, h->degree,
                   h->cfg.comm_radius * h->cfg.comm_radius, h->cfg.n_agents, h->cfg.n_envs};
   hipError_t e = gf::launch_stats(s, h->stream);
@@ -1308,8 +1443,10 @@ int fe_device_buffers(fe_handle* h, fe_buffers* out) {
   // second half waits for what the caller enqueues there
   if (int rc = use_dev(h)) return rc;
   out->x = h->x[h->cur];
-  out->state_values = h->sv;
-  out->network = h->net;
+  // fe_step_host wrote the last observation to host arrays only: the device copies are
+  // stale, so they are not handed out
+  out->state_values = h->obs_on_host ? nullptr : h->sv;
+  out->network = h->obs_on_host ? nullptr : h->net;
   out->controls = h->ctrl[h->ccur];
   out->rewards = cur_reward(h);
   out->knn_idx = h->knn_idx[h->cur];  // the current state's (they alternate with the state)
@@ -1324,7 +1461,12 @@ int fe_sync(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (int rc = use_dev(h)) return rc;
   GF_HIP(hipStreamSynchronize(h->stream));
-  if (h->comm_stream) GF_HIP(hipStreamSynchronize(h->comm_stream));
+  if (h->stage_stream) GF_HIP(hipStreamSynchronize(h->stage_stream));  // behind the steps only
+  if (h->comm && !comm_stream_drained(h)) {
+    comm_release(h, true);
+    return fail(GF_ECOMM, "fe_sync: a collective did not complete within the timeout (a rank stopped "
+                          "responding); communicator aborted, the handle keeps stepping");
+  }
   // both streams are idle now: the next step may split at once. main_dirty (set by
   // use_dev) stays: a zero-copy consumer may enqueue reads of the outputs on `stream`
   // after this call, and the next step's second half must wait for them
@@ -1446,12 +1588,6 @@ int fe_check_shard_sizes(int nranks, const int32_t* n_envs) {
 }  // extern "C"
 
 namespace {
-using Clock = std::chrono::steady_clock;
-
-Clock::time_point deadline_in(double seconds) {
-  return Clock::now() + std::chrono::microseconds(static_cast<int64_t>(seconds * 1e6));
-}
-
 // A non-blocking communicator's pending work: poll its async error until it leaves
 // ncclInProgress or the deadline passes; then the metrics path is torn down (the
 // communicator aborted), so no rank waits forever on a peer that never joined or died.
@@ -1549,11 +1685,12 @@ int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
   h->shard_sizes = sizes;
   h->max_envs = *std::max_element(sizes.begin(), sizes.end());
   const size_t W = h->max_envs;
-  GF_HIP(hipEventCreateWithFlags(&h->step_ev, hipEventDisableTiming));
-  GF_HIP(hipEventCreateWithFlags(&h->step_ev2, hipEventDisableTiming));
-  GF_HIP(hipEventCreateWithFlags(&h->ag_ev, hipEventDisableTiming));
-  GF_HIP(hipEventCreateWithFlags(&h->sg_ev, hipEventDisableTiming));
-  if ((rc = comm_alloc(h, &h->gsend, (size_t)kRewardSlots * W)) ||
+  GF_HIP(hipStreamCreateWithFlags(&h->stage_stream, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev, &h->stage_ev, &h->ss_copy_ev, &h->ag_done[0],
+                        &h->ag_done[1]})
+    GF_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if ((rc = comm_alloc(h, &h->gsend[0], (size_t)kRewardSlots * W)) ||
+      (rc = comm_alloc(h, &h->gsend[1], (size_t)kRewardSlots * W)) ||
       (rc = comm_alloc(h, &h->gather, (size_t)nranks * kRewardSlots * W)) || (rc = comm_alloc(h, &h->ssend, W * 2)) ||
       (rc = comm_alloc(h, &h->stats_gather, (size_t)nranks * W * 2)))
     return rc;
@@ -1578,12 +1715,13 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
   // RCCL's non-blocking init still connects to the bootstrap root inside the call, which
   // waits for every rank: with a rank missing it never returns. The call therefore runs
   // on a thread of its own, which also waits for the communicator to leave
-  // ncclInProgress before it ends (RCCL's own init thread works on the creating thread's
-  // HIP state: with torch's HIP runtime bound, a creating thread that exited first left
-  // a corrupted heap). It hands the communicator over through `state`: 0 running,
-  // 1 handed over, 2 abandoned by this call at the deadline (the helper then aborts what
-  // it created), so exactly one side owns the communicator. This rank then fails with
-  // GF_ECOMM, its handle still usable.
+  // ncclInProgress (RCCL's own init thread works on the creating thread's HIP state:
+  // with torch's HIP runtime bound, a creating thread that exited first left a corrupted
+  // heap) and then parks for the rest of the process instead of exiting. It hands the
+  // communicator over through `state`: 0 running, 1 handed over, 2 abandoned by this call
+  // at the deadline (the helper then queues what it created for the communicator
+  // worker's abort), so exactly one side owns the communicator. This rank then fails
+  // with GF_ECOMM, its handle still usable.
   struct InitJob {
     ncclComm_t comm = nullptr;
     ncclResult_t r = ncclInProgress;
@@ -1610,7 +1748,8 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
     job->r = rr;
     int running = 0;
     if (!job->state.compare_exchange_strong(running, 1, std::memory_order_acq_rel) && c)
-      ncclCommAbort(c);  // abandoned: nobody else will release it
+      abort_comm_later(c, dev);  // abandoned: nobody else will release it
+    park_thread();
   }).detach();
   while (job->state.load(std::memory_order_acquire) != 1) {
     if (Clock::now() > deadline) {
@@ -1681,20 +1820,30 @@ int fe_allgather_rewards(fe_handle* h) {
                                std::to_string(kRewardSlots) + " steps)");
   }
   const size_t B = h->cfg.n_envs, W = h->max_envs;
+  // the send block this gather stages into was read by the collective two gathers back:
+  // the host confirms it complete (bounded; normally long done) before overwriting it
+  const int k = static_cast<int>(h->n_gathers & 1);
+  if (h->ag_live[k]) {
+    if (int rc = comm_event_wait(h, h->ag_done[k], "reward all-gather (send block reuse)")) return rc;
+    h->ag_live[k] = false;
+  }
+  // the staging copy waits for both step streams' latest work (events only), on the
+  // staging stream: behind the steps it reads, never behind a collective
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
-  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
+  GF_HIP(hipStreamWaitEvent(h->stage_stream, h->step_ev, 0));
   if (h->stream2) {
     GF_HIP(hipEventRecord(h->step_ev2, h->stream2));
-    GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev2, 0));
+    GF_HIP(hipStreamWaitEvent(h->stage_stream, h->step_ev2, 0));
   }
   // the steps' ring slots (two runs when they wrap) into the padded send block
+  double* gs = h->gsend[k];
   const int s0 = static_cast<int>(first % kRewardSlots);
   const int n1 = static_cast<int>(std::min<int64_t>(count, kRewardSlots - s0));
-  GF_HIP(hipMemcpy2DAsync(h->gsend, W * 8, h->reward_ring + (size_t)s0 * B, B * 8, B * 8, n1,
-                          hipMemcpyDeviceToDevice, h->comm_stream));
+  GF_HIP(hipMemcpy2DAsync(gs, W * 8, h->reward_ring + (size_t)s0 * B, B * 8, B * 8, n1, hipMemcpyDeviceToDevice,
+                          h->stage_stream));
   if (n1 < count)
-    GF_HIP(hipMemcpy2DAsync(h->gsend + (size_t)n1 * W, W * 8, h->reward_ring, B * 8, B * 8, count - n1,
-                            hipMemcpyDeviceToDevice, h->comm_stream));
+    GF_HIP(hipMemcpy2DAsync(gs + (size_t)n1 * W, W * 8, h->reward_ring, B * 8, B * 8, count - n1,
+                            hipMemcpyDeviceToDevice, h->stage_stream));
   hipEvent_t rd = nullptr;  // the copy's completion: the slots are free again
   if (!h->ev_free.empty()) {
     rd = h->ev_free.back();
@@ -1703,12 +1852,16 @@ int fe_allgather_rewards(fe_handle* h) {
     GF_HIP(hipEventCreateWithFlags(&rd, hipEventDisableTiming));
   }
   h->ring_reads.push_back({first, rd});
-  GF_HIP(hipEventRecord(rd, h->comm_stream));
-  if (int rc = comm_enqueued(h, ncclAllGather(h->gsend, h->gather, (size_t)count * W, ncclFloat64, h->comm,
-                                              h->comm_stream),
+  GF_HIP(hipEventRecord(rd, h->stage_stream));
+  GF_HIP(hipEventRecord(h->stage_ev, h->stage_stream));
+  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->stage_ev, 0));
+  if (int rc = comm_enqueued(h, ncclAllGather(gs, h->gather, (size_t)count * W, ncclFloat64, h->comm, h->comm_stream),
                              "ncclAllGather (rewards)"))
     return rc;
   GF_HIP(hipEventRecord(h->ag_ev, h->comm_stream));
+  GF_HIP(hipEventRecord(h->ag_done[k], h->comm_stream));
+  h->ag_live[k] = true;
+  h->n_gathers++;
   h->ag_issued = true;
   h->last_count = static_cast<int>(count);
   h->gathered_upto = h->steps_written;
@@ -1735,12 +1888,19 @@ int fe_allgather_stats(fe_handle* h) {
   // the summaries are taken on the whole current state (both step halves joined); the
   // collective then runs on the side stream, like the reward all-gather
   if (int rc = use_dev(h)) return rc;
+  // the send block is still read by the previous stats collective: the host confirms it
+  // complete (bounded) before the staging copy overwrites it
+  if (h->sg_pending)
+    if (int rc = comm_event_wait(h, h->sg_ev, "stats all-gather (send block reuse)")) return rc;
   if (int rc = stats_summary_dev(h)) return rc;
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
-  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
-  // into the padded send block, on the side stream (after the previous stats gather)
+  GF_HIP(hipStreamWaitEvent(h->stage_stream, h->step_ev, 0));
+  // into the padded send block on the staging stream (behind the summary, no collective)
   GF_HIP(hipMemcpyAsync(h->ssend, h->stats_sum, (size_t)h->cfg.n_envs * 2 * sizeof(double), hipMemcpyDeviceToDevice,
-                        h->comm_stream));
+                        h->stage_stream));
+  GF_HIP(hipEventRecord(h->ss_copy_ev, h->stage_stream));
+  h->ss_copy_pending = true;
+  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->ss_copy_ev, 0));
   if (int rc = comm_enqueued(h, ncclAllGather(h->ssend, h->stats_gather, (size_t)h->max_envs * 2, ncclFloat64,
                                               h->comm, h->comm_stream),
                              "ncclAllGather (stats)"))
@@ -1764,6 +1924,80 @@ int fe_comm_destroy(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (int rc = use_dev(h)) return rc;
   comm_release(h, false);
+  return GF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// fe_debug_comm_gate's kernel: one wave that sleeps until the page-locked flag turns
+// non-zero or `ticks` of the device's wall clock pass (always bounded).
+__global__ __launch_bounds__(64) void comm_gate_kernel(const unsigned* flag, unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    if (wall_clock64() - t0 > ticks) break;
+    __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+// one process-wide gate flag (fine-grained page-locked memory), never freed: a gate
+// kernel abandoned with an aborted side stream may still read it
+unsigned* gate_flag() {
+  static unsigned* f = [] {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (unsigned*)nullptr;
+    *static_cast<unsigned*>(p) = 1u;
+    return static_cast<unsigned*>(p);
+  }();
+  return f;
+}
+
+// the path of the shared object that defines the function at `fn`
+void so_path(const void* fn, char* dst, int len) {
+  if (!dst || len <= 0) return;
+  Dl_info info{};
+  const char* p = (dladdr(fn, &info) && info.dli_fname) ? info.dli_fname : "";
+  std::snprintf(dst, (size_t)len, "%s", p);
+}
+}  // namespace
+
+extern "C" {
+
+int fe_debug_comm_gate(fe_handle* h, int close, double max_seconds) {
+  if (!h) return fail(GF_EINVAL, "null handle");
+  if (!h->comm || !h->comm_stream) return fail(GF_ESTATE, "no communicator (fe_comm_init first)");
+  unsigned* f = gate_flag();
+  if (!f) return fail(GF_ENOMEM, "gate flag: hipHostMalloc failed");
+  if (!close) {
+    __atomic_store_n(f, 1u, __ATOMIC_SEQ_CST);
+    return GF_OK;
+  }
+  if (!(max_seconds > 0) || max_seconds > 120) return fail(GF_EINVAL, "max_seconds must be in (0, 120]");
+  GF_HIP(hipSetDevice(h->cfg.device));
+  int khz = 0;
+  GF_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->cfg.device));
+  void* df = nullptr;
+  GF_HIP(hipHostGetDevicePointer(&df, f, 0));
+  __atomic_store_n(f, 0u, __ATOMIC_SEQ_CST);
+  const unsigned long long ticks = static_cast<unsigned long long>(max_seconds * 1000.0 * (khz > 0 ? khz : 100000));
+  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, h->comm_stream, static_cast<const unsigned*>(df), ticks);
+  GF_HIP(hipGetLastError());
+  return GF_OK;
+}
+
+int fe_runtime_info(int32_t* hip_runtime_version, int32_t* hip_driver_version, int32_t* rccl_version, char* hip_path,
+                    int hip_path_len, char* rccl_path, int rccl_path_len) {
+  int v = 0;
+  if (hip_runtime_version) *hip_runtime_version = hipRuntimeGetVersion(&v) == hipSuccess ? v : 0;
+  v = 0;
+  if (hip_driver_version) {
+    *hip_driver_version = hipDriverGetVersion(&v) == hipSuccess ? v : 0;
+    (void)hipGetLastError();
+  }
+  v = 0;
+  if (rccl_version) *rccl_version = ncclGetVersion(&v) == ncclSuccess ? v : 0;
+  so_path(reinterpret_cast<const void*>(&hipRuntimeGetVersion), hip_path, hip_path_len);
+  so_path(reinterpret_cast<const void*>(&ncclGetVersion), rccl_path, rccl_path_len);
   return GF_OK;
 }
 

@@ -23,7 +23,8 @@ constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (a
 constexpr int kInlineRimU = 4;      // fused kNN inline rim scan: columns in flight per lane
 constexpr int kStoreTab = 16;      // network rows: float4 table entries per wave (one per nibble)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
-constexpr int kStepInlineRimSmallN = 128;  // ... and every unranked row in envs up to this size
+constexpr int kStepExactKnnMax = 128;  // fused kNN: envs up to this size are ranked exactly in
+                                       // the step (KX: one tile in LDS, no rim kernel)
 constexpr int kKnnRimGrid = 256;     // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnRimHalfGrid = kKnnRimGrid / 2;  // the same per half-batch launch
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
@@ -135,6 +136,9 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 // Whether a step of this geometry can carry the fused k-nearest selection (K ==
 // kStepFusedK, no variant, no tile prefetch, at least K word-slices per row).
 bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch);
+// Whether the fused selection of an env of N agents (tile T) ranks every row exactly in
+// the step (the KX instantiation: one tile, N <= kStepExactKnnMax): no rim kernel follows.
+bool step_knn_exact(int N, int T);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
 // per env: mean vel_diffs, mean min_dists of launch_stats' outputs -> out (B,2)

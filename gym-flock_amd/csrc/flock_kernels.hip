@@ -526,6 +526,58 @@ __device__ __forceinline__ V group_sum_c(V v) {
   for (int o = 16; o < S; o <<= 1) v += __shfl_xor(v, o);
   return v;
 }
+// Exact (r2, j) order of the small-env kNN (KX): a pair's key is the bit pattern of its
+// float64 r2 (non-negative, so the bits order as the values; +inf for the diagonal, as
+// the reference's r2, and every NaN as one canonical NaN above +inf, where argsort puts
+// NaN), ties broken by the lower index.
+__device__ __forceinline__ unsigned long long r2_key(double r2) {
+  return r2 != r2 ? 0x7FF8000000000000ull : static_cast<unsigned long long>(__double_as_longlong(r2));
+}
+// Insert (key, j) into the ascending list (kk, kj) of L entries, keeping its L smallest;
+// columns arrive in ascending j, so an equal key keeps the listed (lower) index first.
+template <int L>
+__device__ __forceinline__ void key_insert_asc(unsigned long long (&kk)[L], int (&kj)[L], unsigned long long key, int j) {
+  if (key < kk[L - 1]) {
+    bool prev = false;
+    unsigned long long pk = 0;
+    int pj = 0;
+#pragma unroll
+    for (int m = 0; m < L; ++m) {
+      const bool sw = key < kk[m];
+      const unsigned long long ok = kk[m];
+      const int oj = kj[m];
+      kk[m] = sw ? (prev ? pk : key) : ok;
+      kj[m] = sw ? (prev ? pj : j) : oj;
+      prev = sw;
+      pk = ok;
+      pj = oj;
+    }
+  }
+}
+// (key, j) minimum over aligned groups of S lanes (S a power of two): DPP lane swaps
+// within rows of 16, shuffles beyond; every lane of a group ends with the group's minimum.
+template <int S>
+__device__ __forceinline__ void group_min_key(unsigned long long& k, int& j) {
+  auto take = [&](unsigned long long ok, int oj) {
+    if (ok < k || (ok == k && oj < j)) {
+      k = ok;
+      j = oj;
+    }
+  };
+  auto dstep = [&](int ctrl) {
+    const unsigned lo = dpp_u32(static_cast<unsigned>(k), ctrl), hi = dpp_u32(static_cast<unsigned>(k >> 32), ctrl);
+    take((static_cast<unsigned long long>(hi) << 32) | lo, static_cast<int>(dpp_u32(static_cast<unsigned>(j), ctrl)));
+  };
+  if constexpr (S > 1) dstep(0xB1);
+  if constexpr (S > 2) dstep(0x4E);
+  if constexpr (S > 4) dstep(0x141);
+  if constexpr (S > 8) dstep(0x140);
+#pragma unroll
+  for (int o = 16; o < S; o <<= 1) {
+    const unsigned long long ok = __shfl_xor(k, o);
+    take(ok, __shfl_xor(j, o));
+  }
+}
 // f(std::integral_constant<int, S>) for the runtime slice count S in {4, 8, 16, 32, 64}
 template <class F>
 __device__ __forceinline__ void with_slices(int S, F&& f) {
@@ -762,7 +814,10 @@ __device__ unsigned long long gf_stamp_buf[8192 * 16];
 // UIN: the drop-in step of a small env with its actions in the kernel arguments
 // (StepArgsU): they arrive with the dispatch instead of being read over the link from
 // page-locked host memory, one dependent round trip per workgroup fewer.
-template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0, bool UIN = false>
+// KX > 0 (Flocking-v0 in an env of one tile, N <= kStepExactKnnMax; KN == 0): after the
+// epilogue every row is ranked exactly against the whole env, staged in LDS as the tile
+// (below): no keys in the feature pass, no unranked rows, no rim kernel.
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0, bool UIN = false, int KX = 0>
 __global__ __launch_bounds__(kThreads, VAR ? 1
                                            : (PF ? kWavesPf
                                                  : (KN ? (CTRL ? kWavesKnnCtrl : kWavesKnn)
@@ -1379,9 +1434,8 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
     // (an exact scan of the env, as the rim kernel's few-rows path); more go to the rim
     // kernel (idx = -1, block flagged)
     // diag 0x40000: every such row to the rim kernel (timing only)
-    // (an env of at most kStepInlineRimSmallN agents: any number, its scans are short)
-    const int ilim = N <= kStepInlineRimSmallN ? 64 : kStepInlineRim;
-    const bool inl = __popcll(__ballot(frow && slow && fs == 0)) <= ilim && !GF_ABLATE(a, 0x40000);
+    // (envs of at most kStepExactKnnMax agents take the KX instantiation instead)
+    const bool inl = __popcll(__ballot(frow && slow && fs == 0)) <= kStepInlineRim && !GF_ABLATE(a, 0x40000);
     if (frow) {
       const size_t g = env0 + i_row;
       if (slow) {
@@ -1428,6 +1482,65 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
     // step's), with the rim kernel's ranking and outputs (knn_wave_scan, knn_write_row)
     const uint64_t todo = __ballot(kinl && fs == 0);
     if (todo) step_inline_rim<DYN, UF64, KN>(a, env0, todo, i_row, me);
+  }
+  if constexpr (KX > 0) {
+    // Flocking-v0 (flocking.py:20-25) in an env of one tile: the tile holds every agent's
+    // post-update state, so each (row, slice) thread ranks the columns fs, fs + S, ... of
+    // its row exactly (float64 r2 computed as the reference's, -ffp-contract=off; the
+    // diagonal +inf) into a sorted list of KX (key, j), and KX rounds of an S-lane (key, j)
+    // minimum leave winner m in the row's lane m: np.argsort's order with ties to the
+    // lower index. The observation x_i - x_j comes from the same LDS tile.
+    unsigned long long kk[KX];
+    int kj[KX];
+#pragma unroll
+    for (int m = 0; m < KX; ++m) {
+      kk[m] = ~0ull;
+      kj[m] = INT_MAX;
+    }
+    if (frow) {
+      for (int c = fs; c < N; c += S) {
+        const double2 p = *reinterpret_cast<const double2*>(&tile[c]);
+        const double dx = me.px - p.x, dy = me.py - p.y;
+        const double r2 = c == i_row ? __builtin_inf() : dx * dx + dy * dy;
+        key_insert_asc<KX>(kk, kj, r2_key(r2), c);
+      }
+    }
+    unsigned long long wk = ~0ull;
+    int wj = INT_MAX;
+    with_slices(S, [&](auto Sc) {
+      constexpr int SS = decltype(Sc)::value;
+#pragma unroll
+      for (int m = 0; m < KX; ++m) {
+        unsigned long long k0 = kk[0];
+        int j0 = kj[0];
+        group_min_key<SS>(k0, j0);
+        const bool pop = kj[0] == j0;  // j is unique among the group's listed entries
+#pragma unroll
+        for (int q = 0; q + 1 < KX; ++q) {
+          kk[q] = pop ? kk[q + 1] : kk[q];
+          kj[q] = pop ? kj[q + 1] : kj[q];
+        }
+        kk[KX - 1] = pop ? ~0ull : kk[KX - 1];
+        kj[KX - 1] = pop ? INT_MAX : kj[KX - 1];
+        if (fs == m) {
+          wk = k0;
+          wj = j0;
+        }
+      }
+    });
+    if (frow && fs < KX) {
+      const size_t g = env0 + i_row;
+      const int j = wj < N ? wj : i_row;  // (N >= KX: every winner is a real column)
+      a.knn_idx[g * KX + fs] = j;
+      const St o = tile[j];
+      float4 ob;
+      ob.x = static_cast<float>(me.px - o.px);
+      ob.y = static_cast<float>(me.py - o.py);
+      ob.z = static_cast<float>(me.vx - o.vx);
+      ob.w = static_cast<float>(me.vy - o.vy);
+      reinterpret_cast<float4*>(a.knn_obs)[g * KX + fs] = ob;
+      if (fs == KX - 1 && a.knn_r2) a.knn_r2[g] = static_cast<float>(__longlong_as_double(static_cast<long long>(wk)));
+    }
   }
   GF_STAMP(10);
 #if defined(GF_STAMPS) && GF_STAMPS >= 2
@@ -1840,7 +1953,7 @@ hipError_t max_lds_once(const void* f, std::atomic<uint64_t>& done, int bytes) {
   return e;
 }
 
-template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0>
+template <bool DYN, bool UF64, bool CTRL, bool VAR, int PF = 0, int KN = 0, int KX = 0>
 static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   size_t lds = step_lds_bytes(a.N, a.R, a.T, CTRL, KN > 0);
   // the plain step runs best at 6 workgroups per CU: 199 us vs 206 at the 7 its 21.2 KiB
@@ -1848,16 +1961,17 @@ static hipError_t launch_step_tiled(const StepArgs& a, hipStream_t s) {
   if (!CTRL && !VAR && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
   static std::atomic<uint64_t> attr{0};
   if (const hipError_t e = max_lds_once(
-          reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF, KN>), attr, 160 * 1024);
+          reinterpret_cast<const void*>(&flock_step_kernel<DYN, UF64, CTRL, VAR, PF, KN, false, KX>), attr, 160 * 1024);
       e != hipSuccess)
     return e;
   const int grid = a.B * a.bpe;
-  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR, PF, KN>), dim3(grid), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL((flock_step_kernel<DYN, UF64, CTRL, VAR, PF, KN, false, KX>), dim3(grid), dim3(kThreads), lds, s,
+                     a);
   return hipGetLastError();
 }
 
 // the drop-in step with its actions copied from the host into the kernel arguments
-template <bool UF64, bool CTRL, int KN = 0>
+template <bool UF64, bool CTRL, int KN = 0, int KX = 0>
 static hipError_t launch_step_uin(const StepArgs& a, hipStream_t s) {
   const size_t bytes = (size_t)a.B * a.N * 2 * (UF64 ? 8 : 4);
   if (bytes > (size_t)kUInlineBytes || a.N > a.T) return hipErrorInvalidValue;
@@ -1865,7 +1979,7 @@ static hipError_t launch_step_uin(const StepArgs& a, hipStream_t s) {
   if (!CTRL && KN == 0 && lds < kStepLdsPlainFloor) lds = kStepLdsPlainFloor;
   static std::atomic<uint64_t> attr{0};
   if (const hipError_t e = max_lds_once(
-          reinterpret_cast<const void*>(&flock_step_kernel<true, UF64, CTRL, false, 0, KN, true>), attr, 160 * 1024);
+          reinterpret_cast<const void*>(&flock_step_kernel<true, UF64, CTRL, false, 0, KN, true, KX>), attr, 160 * 1024);
       e != hipSuccess)
     return e;
   StepArgsU p;
@@ -1873,8 +1987,8 @@ static hipError_t launch_step_uin(const StepArgs& a, hipStream_t s) {
   p.a.u = nullptr;
   p.a.u_inline = 0;
   std::memcpy(p.u, a.u, bytes);
-  hipLaunchKernelGGL((flock_step_kernel<true, UF64, CTRL, false, 0, KN, true>), dim3(a.B * a.bpe), dim3(kThreads), lds,
-                     s, p);
+  hipLaunchKernelGGL((flock_step_kernel<true, UF64, CTRL, false, 0, KN, true, KX>), dim3(a.B * a.bpe), dim3(kThreads),
+                     lds, s, p);
   return hipGetLastError();
 }
 
@@ -1882,23 +1996,26 @@ bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch) {
   return K == kStepFusedK && !variant && !prefetch && kThreads / R >= K && N <= 65536;
 }
 
+bool step_knn_exact(int N, int T) { return N <= kStepExactKnnMax && N <= T; }
+
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if constexpr (DYN) {
+    const bool exact = a.knn_idx && step_knn_exact(a.N, a.T);
     if (a.u_inline) {
       if (a.variant) return hipErrorInvalidValue;
-      if (a.knn_idx) {  // the drop-in Flocking-v0 step (fe_step_host_knn), no controller
+      if (a.knn_idx) {  // the drop-in Flocking-v0 step (fe_step_host_knn*)
+        if (kThreads / a.R < kStepFusedK) return hipErrorInvalidValue;
+        if (exact) return launch_step_uin<UF64, CTRL, 0, kStepFusedK>(a, s);
         if constexpr (CTRL) return hipErrorInvalidValue;
-        else {
-          if (kThreads / a.R < kStepFusedK) return hipErrorInvalidValue;
-          return launch_step_uin<UF64, CTRL, kStepFusedK>(a, s);
-        }
+        else return launch_step_uin<UF64, CTRL, kStepFusedK>(a, s);
       }
       return launch_step_uin<UF64, CTRL>(a, s);
     }
     if (a.knn_idx) {
       if (a.variant || (a.prefetch && a.T <= 2 * kThreads && a.N > a.T) || kThreads / a.R < kStepFusedK)
         return hipErrorInvalidValue;
+      if (exact) return launch_step_tiled<DYN, UF64, CTRL, false, 0, 0, kStepFusedK>(a, s);
       return launch_step_tiled<DYN, UF64, CTRL, false, 0, kStepFusedK>(a, s);
     }
   }

@@ -80,6 +80,7 @@ SIGNATURES = {
     "fe_create": [ctypes.POINTER(FeConfig), ctypes.POINTER(_P)],
     "fe_destroy": [_P],
     "fe_get_config": [_P, ctypes.POINTER(FeConfig)],
+    "fe_set_params": [_P, ctypes.POINTER(FeConfig)],
     "fe_set_state": [_P, _P],
     "fe_set_state_env": [_P, _I, _P],
     "fe_get_state": [_P, _P],
@@ -89,6 +90,7 @@ SIGNATURES = {
     "fe_step": [_P, _P, _I],
     "fe_step_host": [_P, _P, _P, _P, _P, _P, _I],
     "fe_step_host_knn": [_P, _P, _P, _P, _P, _P, _P, _I],
+    "fe_step_host_knn_ctrl": [_P, _P, _P, _P, _P, _P, _P, _P, _I],
     "fe_controller": [_P, _I, _P],
     "fe_get_stats": [_P, _I, _P, _P],
     "fe_get_stats_ex": [_P, _I, _P, _P, _P],
@@ -120,6 +122,9 @@ SIGNATURES = {
     "fe_allgather_stats": [_P],
     "fe_get_gathered_stats": [_P, _P],
     "fe_comm_destroy": [_P],
+    "fe_debug_comm_gate": [_P, _I, ctypes.c_double],
+    "fe_runtime_info": [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                        ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, _I, ctypes.c_char_p, _I],
     "fe_set_variant": [_P, _P],
     "fe_set_dt": [_P, _P],
     "cov_create": [ctypes.POINTER(CovConfig), ctypes.POINTER(_P)],
@@ -326,11 +331,28 @@ class PinnedArray:
 
 def u_is_f64(u):
     """Whether the reference's `u * action_scalar` (flocking_relative.py:95) computes in
-    float64 for this action array (NumPy's promotion: float32/float16 stay float32)."""
+    float64 for this action array (NumPy's promotion: float32 stays float32, float64 and
+    integer arrays go to float64).
+
+    float16 actions are the exception: NumPy keeps `u * 10.0 * dt * dt * 0.5` in float16
+    (legacy value-based casting and NEP 50 alike), while the kernels have float32 and
+    float64 arithmetic only. They are cast to float32 and computed exactly as float32
+    actions of the same values are (tests/test_flock_gpu.py pins that); parity with the
+    reference's float16 rounding is unpinned."""
     d = u.dtype
     if d == np.float32 or d == np.float16:
         return False
     return d == np.float64 or np.result_type(d, 10.0) != np.float32
+
+
+def runtime_info():
+    """The HIP runtime and RCCL libgymflock is bound to in this process (fe_runtime_info):
+    {hip_runtime, hip_driver, rccl: versions; hip_lib, rccl_lib: shared-object paths}."""
+    rt, dv, rc = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    hp, rp = ctypes.create_string_buffer(512), ctypes.create_string_buffer(512)
+    check(load().fe_runtime_info(ctypes.byref(rt), ctypes.byref(dv), ctypes.byref(rc), hp, 512, rp, 512))
+    return {"hip_runtime": rt.value, "hip_driver": dv.value, "rccl": rc.value,
+            "hip_lib": hp.value.decode(errors="replace"), "rccl_lib": rp.value.decode(errors="replace")}
 
 
 def check_shard_sizes(n_envs):
@@ -369,6 +391,14 @@ class FlockHandle:
             self.h = None
 
     __del__ = close
+
+    def set_params(self, comm_radius, dt, action_scalar, mean_pooling, centralized):
+        """New comm_radius / dt / action_scalar / mean_pooling / centralized for the later
+        launches, the state kept (fe_set_params)."""
+        c = FeConfig(self.cfg.n_agents, self.cfg.n_envs, float(comm_radius), float(dt), float(action_scalar),
+                     int(bool(mean_pooling)), int(bool(centralized)), self.cfg.n_neighbors, self.cfg.device)
+        check(self.lib.fe_set_params(self.h, ctypes.byref(c)))
+        self.cfg = c
 
     # -- variants (include/gymflock.h fe_variant)
     def set_variant(self, n_frozen=0, n_vel_zero=0, u_scale=None, u_clip=0.0, x_scale=1.0,
@@ -454,11 +484,15 @@ class FlockHandle:
         if rc:
             check(rc)
 
-    def step_host_knn(self, u_addr, f64, sv, net, rew, idx, obs):
-        """fe_step_host_knn: step_host plus the new state's k nearest (addresses of host
-        destinations, page-locked ones written in place; any may be None but not both
-        idx and obs)."""
-        rc = self.lib.fe_step_host_knn(self.h, u_addr, sv, net, rew, idx, obs, FE_U_F64 if f64 else 0)
+    def step_host_knn(self, u_addr, f64, sv, net, rew, idx, obs, ctrl=None):
+        """fe_step_host_knn(_ctrl): step_host plus the new state's k nearest (addresses of
+        host destinations, page-locked ones written in place; any may be None but not both
+        idx and obs), and with ctrl the expert action of the new state (fused)."""
+        if ctrl is None:
+            rc = self.lib.fe_step_host_knn(self.h, u_addr, sv, net, rew, idx, obs, FE_U_F64 if f64 else 0)
+        else:
+            rc = self.lib.fe_step_host_knn_ctrl(self.h, u_addr, sv, net, rew, ctrl, idx, obs,
+                                                FE_U_F64 if f64 else 0)
         if rc:
             check(rc)
 
@@ -617,6 +651,11 @@ class FlockHandle:
 
     def comm_destroy(self):
         check(self.lib.fe_comm_destroy(self.h))
+
+    def debug_comm_gate(self, close, max_seconds=30.0):
+        """Tests only: hold (close=True) or release the collectives' side stream with a
+        bounded spin kernel, as a collective stuck on a dead peer would (fe_debug_comm_gate)."""
+        check(self.lib.fe_debug_comm_gate(self.h, int(bool(close)), float(max_seconds)))
 
     def allgather_rewards(self):
         """Enqueue the all-gather of every step's rewards since the previous one."""

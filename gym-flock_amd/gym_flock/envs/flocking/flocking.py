@@ -33,7 +33,11 @@ class FlockingEnv(FlockingRelativeEnv):
         """:12-14. In the default fetch mode ("direct") one library call with one wait
         (fe_step_host_knn): the step with the k-nearest selection fused in, the rim kNN,
         and every output (state_values, network, reward, the neighbour rows and indices)
-        written into one pooled page-locked block."""
+        written into one pooled page-locked block. Once controller() has been asked for,
+        the expert action of the new state (controller() inherited from
+        flocking_relative.py:194-212) is computed in the same launch and lands in the same
+        block (fe_step_host_knn_ctrl), so `u = env.controller(); env.step(u)` stays one
+        call per step."""
         u = np.asarray(u)
         assert u.shape == (self.n_agents, self.nu)
         self.u = u * self.action_scalar
@@ -49,15 +53,17 @@ class FlockingEnv(FlockingRelativeEnv):
         if self._ubuf is None or self._ubuf.a.dtype != dt:
             self._ubuf = nat.PinnedArray((n, 2), dt)  # read by the kernel in place
         self._ubuf.a[...] = u
+        ctrl = self._want_ctrl
         lay = self._klayout
-        if lay is None or lay[0] != (n, k):
+        if lay is None or lay[0] != (n, k, ctrl):
             a64 = lambda b: (b + 63) & ~63  # noqa: E731
             o_ix = a64(4 * n * n)
             o_ob = o_ix + a64(4 * n * k)
-            o_rw = o_ob + a64(16 * n * k)
+            o_ct = o_ob + a64(16 * n * k)
+            o_rw = o_ct + (a64(16 * n) if ctrl else 0)
             o_sv = o_rw + 64
-            lay = self._klayout = ((n, k), o_ix, o_ob, o_rw, o_sv, o_sv + 24 * n)
-        _, o_ix, o_ob, o_rw, o_sv, size = lay
+            lay = self._klayout = ((n, k, ctrl), o_ix, o_ob, o_ct, o_rw, o_sv, o_sv + 24 * n)
+        _, o_ix, o_ob, o_ct, o_rw, o_sv, size = lay
         buf, base = nat.host_pool().block_addr(size)
         if buf is None:  # not page-locked (pool cap): the library copies after the launch
             buf = np.empty(size, np.uint8)
@@ -67,8 +73,11 @@ class FlockingEnv(FlockingRelativeEnv):
         obs = np.ndarray((n, 4 * k), np.float32, buf, o_ob)
         rw = np.ndarray((1,), np.float64, buf, o_rw)
         sv = np.ndarray((n, 6), np.float32, buf, o_sv)
-        h.step_host_knn(self._ubuf.addr, f64, base + o_sv, base, base + o_rw, base + o_ix, base + o_ob)
-        self._ctrl_cache = None
+        ct = np.ndarray((n, 2), np.float64, buf, o_ct) if ctrl else None
+        h.step_host_knn(self._ubuf.addr, f64, base + o_sv, base, base + o_rw, base + o_ix, base + o_ob,
+                        base + o_ct if ctrl else None)
+        self._ctrl_cache = ct
+        self._ctrl_key = self._hkey
         self.state_values, self.state_network = sv, net
         self._reward = float(rw[0])
         self.nearest, self._obs = idx, obs

@@ -68,6 +68,7 @@ class FlockingRelativeEnv(Env):
         # its resulting state in the same launch, and controller() returns it
         self._want_ctrl = False
         self._ctrl_cache = None
+        self._ctrl_key = None  # the handle parameters the cached expert action was computed with
         self._ubuf = None
         self._layout = None  # ((n, ctrl), offsets of the step's page-locked output block)
 
@@ -104,18 +105,33 @@ class FlockingRelativeEnv(Env):
         self.np_random, seed = np_random(seed)
         return [seed]
 
-    def _key(self):
-        return (self.n_agents, self.comm_radius, self.dt, self.action_scalar,
-                bool(self.mean_pooling), bool(self.centralized), self.n_neighbors, self.device)
+    def _key(self, centralized=None):
+        """The device handle's parameters: the first three fix its buffers, the rest are
+        runtime parameters of its launches (fe_set_params)."""
+        c = self.centralized if centralized is None else centralized
+        return (self.n_agents, self.n_neighbors, self.device, float(self.comm_radius), float(self.dt),
+                float(self.action_scalar), bool(self.mean_pooling), bool(c))
 
     def _handle(self):
-        """The device handle for the current parameters (re-created if they changed)."""
+        """The device handle for the current parameters. The reference reads comm_radius,
+        dt, action_scalar, mean_pooling and centralized at call time (e.g. :200-201), so a
+        change of those between calls keeps the state: the handle takes them as runtime
+        parameters. A new n_agents (or device) needs new buffers: the handle is re-created
+        and the state starts unset, as the reference's x no longer fits (reset() next)."""
         key = self._key()
-        if self._h is None or key != self._hkey:
-            if self._h is not None:
+        if self._h is not None and key != self._hkey:
+            if key[:3] == self._hkey[:3]:
+                self._h.set_params(*key[3:])
+                self._hkey = key
+                v = self._variant()
+                if v:
+                    self._h.set_variant(**v)
+            else:
                 self._h.close()
-            self._invalidate()
-            self._ubuf = None
+                self._h = None
+                self._invalidate()
+                self._ubuf = None
+        if self._h is None:
             self._h = nat.FlockHandle(self.n_agents, 1, self.comm_radius, self.dt,
                                       self.action_scalar, self.mean_pooling, self.centralized,
                                       self.n_neighbors, self.device)
@@ -194,6 +210,7 @@ class FlockingRelativeEnv(Env):
         self.state_values, self.state_network = sv, net
         self._reward = float(rw[0])
         self._ctrl_cache = ct
+        self._ctrl_key = self._hkey
 
     def _fetch_obs(self):
         h = self._h
@@ -240,12 +257,15 @@ class FlockingRelativeEnv(Env):
         """:194-212 — Turner-2003 expert action (N,2) float64 for the current state. After
         a step (or reset) the action was computed in that launch already: it is returned
         as is (a fresh array; a second call for the same state gets a copy). Otherwise, or
-        for the other `centralized` setting, one launch."""
+        for other parameters than that launch had (centralized, comm_radius, ...), one
+        launch."""
         if centralized is None:
             centralized = self.centralized
         self._want_ctrl = True
         c = self._ctrl_cache
-        if c is not None and bool(centralized) == bool(self.centralized):
+        # the cached action counts only if it was computed with the parameters asked for
+        # now (centralized, comm_radius, ... as the env holds them at this call, :200-201)
+        if c is not None and self._ctrl_key == self._key(bool(centralized)):
             self._ctrl_cache = c.copy()  # later calls for this state get their own array
             return c
         return self._handle().controller(centralized)[0]

@@ -97,7 +97,9 @@ typedef struct fe_variant {
 } fe_variant;
 
 /* Device pointers owned by the handle (valid until fe_destroy). Ping-pong
- * buffers are reported as their CURRENT slot (the one the next getter reads). */
+ * buffers are reported as their CURRENT slot (the one the next getter reads).
+ * state_values and network are NULL while the last observation went to host arrays
+ * only (fe_step_host / fe_step_host_knn*: the device copies are stale then). */
 typedef struct fe_buffers {
   double* x;             /* (B,N,4) float64 current state                        */
   float* state_values;   /* (B,N,6) float32                                      */
@@ -115,6 +117,11 @@ typedef struct fe_buffers {
 int fe_create(const fe_config* cfg, fe_handle** out);      /* FlockingRelativeEnv.__init__ :20-66 */
 int fe_destroy(fe_handle* h);                               /* close() :303 */
 int fe_get_config(const fe_handle* h, fe_config* out);
+/* Change comm_radius, dt, action_scalar, mean_pooling and centralized for the following
+ * launches, keeping the state (the reference reads these attributes at call time, e.g.
+ * self.centralized in controller() :200-201). n_agents, n_envs, n_neighbors and device
+ * must equal the handle's (GF_EINVAL otherwise). */
+int fe_set_params(fe_handle* h, const fe_config* cfg);
 
 /* State ---------------------------------------------------------------------- */
 int fe_set_state(fe_handle* h, const double* x);            /* env.x = ... (:189) */
@@ -164,6 +171,12 @@ int fe_step_host(fe_handle* h, const void* u, float* state_values, float* networ
  * when they were written straight to the host). */
 int fe_step_host_knn(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
                      int32_t* knn_idx, float* knn_obs, int flags);
+/* Flocking-v0's drop-in expert loop, `u = env.controller(); env.step(u)` (controller()
+ * inherited from flocking_relative.py:194-212 by flocking.py:5, step flocking.py:12-14):
+ * fe_step_host_knn plus controls (B,N,2) f64 = controller() of the resulting state, fused
+ * into the same launch (controls may be NULL: then as fe_step_host_knn). */
+int fe_step_host_knn_ctrl(fe_handle* h, const void* u, float* state_values, float* network, double* rewards,
+                          double* controls, int32_t* knn_idx, float* knn_obs, int flags);
 /* controller(centralized) (:194-212) on the current state; centralized < 0 means the
  * config default. Writes (B,N,2) float64 to u_out (host) if non-NULL. */
 int fe_controller(fe_handle* h, int centralized, double* u_out);
@@ -250,8 +263,20 @@ int fe_gathered_steps(fe_handle* h);
  * rank-major. */
 int fe_allgather_stats(fe_handle* h);
 int fe_get_gathered_stats(fe_handle* h, double* dst);
-/* Destroys the communicator and the metrics path's buffers; fe_comm_init may follow. */
+/* Destroys the communicator and the metrics path's buffers; fe_comm_init may follow. A
+ * side stream that does not drain within the collective timeout is aborted instead. */
 int fe_comm_destroy(fe_handle* h);
+/* Tests only: close = 1 enqueues on the collectives' side stream a one-wave kernel that
+ * spins (s_sleep) until close = 0 is called or max_seconds pass, standing in for a
+ * collective whose peer stopped responding; close = 0 releases it. Needs fe_comm_init. */
+int fe_debug_comm_gate(fe_handle* h, int close, double max_seconds);
+/* The HIP runtime and RCCL this library is bound to in this process (a process that
+ * loaded another copy of either first, e.g. PyTorch's bundled ones, binds that copy):
+ * hipRuntimeGetVersion, hipDriverGetVersion (0 without a driver), ncclGetVersion, and the
+ * paths of the shared objects those entry points resolved to (dladdr). Host-only; any
+ * pointer may be NULL. */
+int fe_runtime_info(int32_t* hip_runtime_version, int32_t* hip_driver_version, int32_t* rccl_version, char* hip_path,
+                    int hip_path_len, char* rccl_path, int rccl_path_len);
 
 /* ============================ Coverage-v0 ==================================== */
 /* gym_flock/envs/spatial/coverage.py. B envs of n_robots robots moving on a per-env

@@ -218,3 +218,26 @@ def test_unpad_gathered_layout():
     np.testing.assert_array_equal(unpad_gathered(np.stack(rblocks), sizes, axis=1), rew)
     np.testing.assert_array_equal(unpad_gathered(np.stack(sblocks), sizes, axis=0), st)
 
+
+
+def test_runtime_info_names_the_bound_libraries():
+    """fe_runtime_info works without a device: the HIP runtime and RCCL versions and the
+    shared objects libgymflock's HIP / RCCL entry points resolved to (this process has
+    not loaded torch, so they are /opt/rocm's)."""
+    from gym_flock import _native as nat
+    info = nat.runtime_info()
+    assert info["hip_runtime"] > 0 and info["rccl"] > 0, info
+    assert "libamdhip64" in info["hip_lib"] and "librccl" in info["rccl_lib"], info
+    assert os.path.exists(info["hip_lib"]) and os.path.exists(info["rccl_lib"]), info
+
+
+def test_u_is_f64_follows_numpy_promotion():
+    """float32 (and float16, computed as float32: its float16 rounding is unpinned) keep
+    the float32 action arithmetic; float64 and integer arrays take float64, as NumPy's
+    u * 10.0 promotes them (flocking_relative.py:95)."""
+    from gym_flock import _native as nat
+    assert not nat.u_is_f64(np.zeros(2, np.float32))
+    assert not nat.u_is_f64(np.zeros(2, np.float16))
+    assert (np.zeros(2, np.float16) * 10.0).dtype == np.float16  # NumPy itself stays in float16
+    assert nat.u_is_f64(np.zeros(2, np.float64))
+    assert nat.u_is_f64(np.zeros(2, np.int64))

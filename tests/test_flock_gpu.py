@@ -446,6 +446,246 @@ def test_flocking_v0_dropin_direct_matches_oracle(n, f64):
         env.close()
 
 
+@pytest.mark.parametrize("n", [10, 100, 300])
+def test_flocking_v0_dropin_expert_loop(n):
+    """Flocking-v0's expert loop through the env API, `u = env.controller(); env.step(u)`
+    for 20 steps (N = 10 and 100: the exact in-step ranking with the actions in the kernel
+    arguments; 300: the fused-key ranking with the controller, actions read from
+    page-locked memory). After the first controller() call every step computes the next
+    expert action in its own launch (fe_step_host_knn_ctrl) and controller() returns it.
+    Against the oracle stepped with the same actions: state bit-exact, kNN indices
+    bit-exact and observations exact, controller rtol 1e-9, network exact."""
+    from gym_flock.envs.flocking.flocking import FlockingEnv
+    from gym_flock.init_states import synthetic_state
+    env = FlockingEnv()
+    env.n_agents = n
+    env._make_spaces()
+    env.x = synthetic_state(n, 31)
+    env.compute_helpers()
+    for t in range(20):
+        x = env.x
+        if t > 0:
+            assert env._ctrl_cache is not None  # computed by the previous step's launch
+        u = env.controller()
+        np.testing.assert_allclose(u, orc.controller(x), rtol=1e-9, atol=1e-12)
+        (obs, net), r, done, _ = env.step(u)
+        ref = orc.step(x, u, with_controller=True)
+        ridx, robs = orc.knn_observation(ref["x"])
+        np.testing.assert_array_equal(env.x, ref["x"])
+        np.testing.assert_array_equal(env.nearest, ridx)
+        np.testing.assert_array_equal(obs, robs.astype(np.float32))
+        np.testing.assert_array_equal(net, ref["network"].astype(np.float32))
+        np.testing.assert_allclose(r, ref["reward"], rtol=1e-12)
+        assert env._ctrl_cache is not None  # fused into the step's launch
+        np.testing.assert_allclose(env._ctrl_cache, ref["ctrl"], rtol=1e-9, atol=1e-12)
+    env.close()
+
+
+@pytest.mark.parametrize("mode", ["direct", "pooled"])
+def test_flocking_v0_episode_fixture(mode):
+    """The reference's recorded N=10 episode (20 expert then 20 float32 random actions)
+    through Flocking-v0's env API: the same states and networks, the 7-nearest rows of
+    each recorded state, and controller() as recorded."""
+    from gym_flock.envs.flocking.flocking import FlockingEnv
+    f = np.load(os.path.join(GOLDEN, "flock_n10_episode.npz"))
+    env = FlockingEnv()
+    env.n_agents = 10
+    env._make_spaces()
+    env.fetch_mode = mode
+    env.x = f["x0"]
+    env.compute_helpers()
+    for t in range(40):
+        if not f["u_is_f32"][t]:
+            np.testing.assert_allclose(env.controller(), f["u"][t], rtol=1e-9, atol=1e-12)
+            u = f["u"][t]
+        else:
+            u = f["u"][t].astype(np.float32)
+        (obs, net), r, _, _ = env.step(u)
+        np.testing.assert_array_equal(env.x, f["x"][t])
+        ridx, robs = orc.knn_observation(f["x"][t])
+        np.testing.assert_array_equal(env.nearest if mode == "direct" else env._handle().knn(0)[0], ridx)
+        np.testing.assert_array_equal(obs, robs.astype(np.float32))
+        np.testing.assert_array_equal(net, f["net"][t].astype(np.float32))
+        np.testing.assert_allclose(r, f["reward"][t], rtol=1e-12)
+        np.testing.assert_allclose(env.controller(), f["ctrl"][t], rtol=1e-9, atol=1e-12)
+    env.close()
+
+
+def _small_knn_cases(n, rs):
+    """The nine kNN shapes of _knn_cases rebuilt at a small N (exact in-step ranking at
+    N <= 128, the fused-key ranking above): sparse, tied lattices, coincident agents,
+    large offsets, dense lattices and swarms, a detached sparse group."""
+    w = int(np.ceil(np.sqrt(n)))
+    g = np.stack(np.meshgrid(np.arange(w), np.arange(w)), -1).reshape(-1, 2)[:n] * 2.0
+    side = np.sqrt(n / 100.0)
+    cases = {}
+    x = np.zeros((n, 4))
+    x[:, :2] = rs.uniform(-12, 12, size=(n, 2)) * side  # dispersed: almost every row below k neighbours
+    cases["dispersed"] = x
+    x = np.zeros((n, 4))
+    x[:, :2] = g[rs.permutation(n)]  # lattice: exact r2 ties everywhere, no neighbours
+    cases["lattice"] = x
+    x = cases["lattice"].copy()
+    x[:, :2] += rs.uniform(-1, 1, size=(n, 2)) * 1e-12
+    cases["lattice_jitter"] = x
+    x = np.zeros((n, 4))
+    x[:, :2] = rs.uniform(-8, 8, size=(n, 2)) * side
+    x[10:20, :2] = x[0, :2]  # coincident agents (r2 = 0 ties)
+    cases["coincident_ragged"] = x
+    x = cases["dispersed"].copy()
+    x[:, :2] += 3.0e6
+    cases["offset"] = x
+    x = np.zeros((n, 4))
+    x[:, :2] = g[rs.permutation(n)] * 0.125  # ~20 neighbours each, exact ties
+    cases["dense_lattice"] = x
+    x = cases["dense_lattice"].copy()
+    x[:, :2] += rs.uniform(-1, 1, size=(n, 2)) * 1e-3
+    x[:, 2:] = rs.uniform(-1, 1, size=(n, 2))
+    cases["dense_jitter"] = x
+    x = np.zeros((n, 4))
+    x[:, :2] = rs.uniform(-1.8, 1.8, size=(n, 2)) * side
+    x[:, 2:] = rs.uniform(-1, 1, size=(n, 2))
+    x[50:54, :2] = x[7, :2]
+    x[60, :2] = x[61, :2] + np.array([3e-9, 0.0])  # closer than one key step
+    cases["dense_random"] = x
+    x = cases["dense_random"].copy()
+    x[:12, :2] += 30.0 + rs.uniform(-5, 5, size=(12, 2))  # a detached, sparse group
+    cases["dense_with_rim"] = x
+    return cases
+
+
+KNN_CASES = ["dispersed", "lattice", "lattice_jitter", "coincident_ragged", "offset", "dense_lattice",
+             "dense_jitter", "dense_random", "dense_with_rim"]
+
+
+@pytest.mark.parametrize("n", [100, 128, 129])
+def test_knn_small_env_cases_vs_oracle(n):
+    """Flocking-v0 at the reference's default size and around the exact-ranking limit
+    (N <= 128: every row ranked exactly in the step from the env's LDS tile; 129: the
+    fused-key ranking with inline scans and the rim kernel): the nine kNN shapes, both
+    agent orders, k = 7, through the batched step (FE_WITH_KNN, zero actions) and through
+    FlockingEnv.step in direct mode (one fe_step_host_knn call). Indices bit-exact,
+    observations exact, against the oracle's stable argsort."""
+    from gym_flock.envs.flocking.flocking import FlockingEnv
+    cases = _small_knn_cases(n, np.random.RandomState(2100 + n))
+    env = FlockingEnv()
+    env.n_agents = n
+    env._make_spaces()
+    for case in KNN_CASES:
+        x0 = cases[case]
+        xb = np.stack([x0, x0[::-1].copy()])
+        h = nat.FlockHandle(n, 2, n_neighbors=7)
+        h.set_state(xb)
+        u0 = np.zeros((2, n, 2), np.float32)
+        h.step(u0, nat.FE_WITH_KNN)
+        for b in range(2):
+            x1 = h.get_state(b)
+            np.testing.assert_array_equal(x1, orc.integrate(xb[b], u0[b]), err_msg=case)
+            idx, obs = h.knn(b)
+            ridx, robs = orc.knn_observation(x1, 7)
+            np.testing.assert_array_equal(idx, ridx, err_msg=case)
+            np.testing.assert_array_equal(obs, robs.astype(np.float32), err_msg=case)
+            # the drop-in step from the same state
+            env.x = xb[b]
+            (eobs, enet), _, _, _ = env.step(np.zeros((n, 2), np.float32))
+            np.testing.assert_array_equal(env.nearest, ridx, err_msg=case + " (env)")
+            np.testing.assert_array_equal(eobs, robs.astype(np.float32), err_msg=case + " (env)")
+        h.close()
+    env.close()
+
+
+@pytest.mark.parametrize("n", [100, 128, 129])
+def test_knn_small_env_continuous(n):
+    """30 continuous Flocking-v0 steps of 4 envs at N around the exact-ranking limit
+    (split steps, resident actions, a spread swarm: most rows below k neighbours), the
+    state chain bit-exact and indices / observations against the oracle every 3rd step."""
+    B = 4
+    x0 = synthetic_batch(B, n, seed0=6100 + n)
+    x0[:, :, :2] *= 2.0
+    u = np.random.RandomState(n).uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+    h = nat.FlockHandle(n, B, n_neighbors=7)
+    h.set_state(x0)
+    h.set_actions(u)
+    x = x0.copy()
+    for t in range(1, 31):
+        h.step(None, nat.FE_U_RESIDENT | nat.FE_WITH_KNN)
+        x = np.stack([orc.integrate(x[b], u[b]) for b in range(B)])
+        if t % 3 == 0:
+            np.testing.assert_array_equal(h.get_state(), x)
+            idx, obs = h.knn()
+            for b in range(B):
+                ridx, robs = orc.knn_observation(x[b])
+                np.testing.assert_array_equal(idx[b], ridx)
+                np.testing.assert_array_equal(obs[b], robs.astype(np.float32))
+    h.close()
+
+
+def test_params_change_mid_episode_keeps_state():
+    """Changing centralized, comm_radius, dt, action_scalar or mean_pooling between steps
+    keeps the episode's state (the reference reads them at call time, :200-201): each
+    step and controller() against the oracle with the parameters of that call, the
+    state chain bit-exact. Flocking-v0 too (its kNN under the new radius)."""
+    from gym_flock.envs.flocking.flocking import FlockingEnv
+    from gym_flock.envs.flocking.flocking_relative import FlockingRelativeEnv
+    from gym_flock.init_states import synthetic_state
+    n = 100
+    rs = np.random.RandomState(77)
+    plan = [dict(), dict(centralized=False), dict(comm_radius=1.2), dict(dt=0.02),
+            dict(mean_pooling=False), dict(action_scalar=5.0), dict(centralized=True, comm_radius=0.9)]
+    for cls in (FlockingRelativeEnv, FlockingEnv):
+        env = cls()
+        env.n_agents = n
+        env._make_spaces()
+        env.x = synthetic_state(n, 5)
+        env.compute_helpers()
+        env.controller()  # the expert action is fused from here on
+        for change in plan:
+            for k, v in change.items():
+                setattr(env, k, v)
+            p = dict(comm_radius=env.comm_radius, dt=env.dt, action_scalar=env.action_scalar,
+                     mean_pooling=env.mean_pooling)
+            x = env.x
+            np.testing.assert_allclose(env.controller(), orc.controller(x, p["comm_radius"], p["action_scalar"],
+                                                                       env.centralized), rtol=1e-9, atol=1e-12)
+            u = rs.uniform(-1, 1, size=(n, 2)).astype(np.float32)
+            (o, net), r, _, _ = env.step(u)
+            ref = orc.step(x, u, with_controller=True, centralized=env.centralized, **p)
+            np.testing.assert_array_equal(env.x, ref["x"])
+            np.testing.assert_array_equal(net, ref["network"].astype(np.float32))
+            np.testing.assert_allclose(r, ref["reward"], rtol=1e-12)
+            np.testing.assert_allclose(env.controller(), ref["ctrl"], rtol=1e-9, atol=1e-12)
+            np.testing.assert_allclose(env.controller(centralized=not env.centralized),
+                                       orc.step(x, u, with_controller=True, centralized=not env.centralized,
+                                                **p)["ctrl"], rtol=1e-9, atol=1e-12)
+            if cls is FlockingEnv:
+                ridx, robs = orc.knn_observation(ref["x"])
+                np.testing.assert_array_equal(env.nearest, ridx)
+                np.testing.assert_array_equal(o, robs.astype(np.float32))
+        env.close()
+
+
+def test_float16_actions_take_float32_arithmetic():
+    """float16 actions are computed as float32 actions of the same values (the kernels have
+    float32 and float64 arithmetic; the reference's float16 rounding is parity unpinned)."""
+    from gym_flock.envs.flocking.flocking_relative import FlockingRelativeEnv
+    from gym_flock.init_states import synthetic_state
+    n = 64
+    x0 = synthetic_state(n, 9)
+    u16 = np.random.RandomState(9).uniform(-1, 1, size=(n, 2)).astype(np.float16)
+    outs = []
+    for u in (u16, u16.astype(np.float32)):
+        env = FlockingRelativeEnv()
+        env.n_agents = n
+        env._make_spaces()
+        env.x = x0
+        (sv, net), r, _, _ = env.step(u)
+        outs.append((env.x, sv.copy(), net.copy(), r))
+        env.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(outs[0][0], orc.step(x0, u16.astype(np.float32))["x"])
+
+
 def test_config5_size_sampled_rows():
     """N=8192 (BASELINE.json configs[4]'s agent count; 16-row blocks, 16 LDS tiles per
     row sweep): the whole state and reward, and 40 sampled rows of the network,
@@ -731,15 +971,17 @@ def test_knn_radius_history_continuous(spread):
     h.close()
 
 
-@pytest.mark.parametrize("per_wave", [1, 2, 3, 8])
-def test_knn_unranked_rows_inline_and_rim(per_wave):
+@pytest.mark.parametrize("n,per_wave", [(256, 1), (256, 2), (256, 3), (256, 8), (128, 3), (128, 8), (129, 3),
+                                        (129, 8)])
+def test_knn_unranked_rows_inline_and_rim(n, per_wave):
     """Rows the fused step cannot rank (here: outliers 3 comm radii from everyone, with
     no radius history yet) go to the wave's own exact scan when a wave (8 rows at N=256)
     holds at most two of them, and to the rim kNN kernel otherwise. per_wave outliers in
     every 8-row group: 1 and 2 take the inline scan, 3 and 8 the rim kernel (env 1 mixes
-    the two: outliers only in its even groups). Indices bit-exact and observations exact
+    the two: outliers only in its even groups). N=128: the exact in-step ranking takes
+    every row; 129: the first size past it. Indices bit-exact and observations exact
     against the oracle for 4 continuous steps (the history then ranks them in the step)."""
-    n, B = 256, 3
+    B = 3
     x0 = synthetic_batch(B, n, seed0=91)
     for b in range(B):
         for g in range(n // 8):

@@ -146,8 +146,12 @@ def test_rendezvous_drops_stray_peers_and_goes_on():
     assert not err and out, err
     g0 = out[0]
     assert len(g0.refused) == 2
-    threading.Thread(target=lambda: g1.barrier()).start()
+    done1 = []
+    t1 = threading.Thread(target=lambda: done1.append(g1.barrier() is None))
+    t1.start()
     g0.barrier()
+    t1.join(timeout=30)   # rank 1's barrier returned before either side closes
+    assert not t1.is_alive() and done1 == [True], done1
     g0.close()
     g1.close()
 

@@ -141,3 +141,42 @@ def test_comm_init_peer_never_joins():
     assert "timed out" in fields["MSG"], out
     assert fields["STEP_OK"] == "True", out
     print("lone-rank init failed after %s s (child wall %.1f s): %s" % (secs, wall, fields["MSG"]))
+
+
+def test_steps_never_wait_behind_a_stuck_collective():
+    """A collective that never completes (a gate kernel holds the side stream, as a peer
+    that stopped responding would) must not hold the step streams: the ring slots a step
+    overwrites are released by the staging copies, which wait only for the steps. 86
+    steps (past the 64-slot ring) and their reward reads finish while the gate is shut;
+    the gather queued behind it then delivers its steps once the gate opens, and the
+    stats gather the same."""
+    B, N = 3, 32
+    v = VecFlockingRelative(B, N)
+    v.reset(seed=5)
+    g = RcclRewardGather(v.h, 1, 0, v.h.comm_unique_id(), timeout=60.0)
+    u = np.random.RandomState(5).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+    for _ in range(8):
+        v.step(u)
+    g.issue()
+    g.result()
+    v.h.debug_comm_gate(True, max_seconds=40.0)
+    try:
+        t0 = time.monotonic()
+        hist = []
+        for _ in range(8):
+            v.step(u)
+            hist.append(v.rewards())
+        g.issue()  # queued behind the gate
+        for _ in range(8):
+            v.step(u)
+            hist.append(v.rewards())
+        g.issue()  # its send block's previous collective (before the gate) is complete
+        for _ in range(70):  # past the ring: each slot's staging copy has run
+            v.step(u)
+            v.rewards()
+        held = time.monotonic() - t0
+    finally:
+        v.h.debug_comm_gate(False)
+    assert held < 20.0, "steps waited %.1f s behind the gated collective" % held
+    np.testing.assert_array_equal(g.result(), np.array(hist[8:16]))
+    v.close()

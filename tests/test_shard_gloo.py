@@ -4,14 +4,18 @@ with the oracle, since there is no GPU) and all-gathers them, twice: with
 GlooRewardGather, and in the RCCL path's padded block layout (shard.pad_block on every
 rank, one fixed-size all-gather, shard.unpad_gathered: the code RcclRewardGather.result
 runs). 5 envs over 2 ranks are uneven shards (3 + 2). Both gathered vectors must equal
-the single-process batch in global env order."""
+the single-process batch in global env order.
+
+torch is imported only inside the spawned workers: collecting this module (which a
+`-m gpu` run does too) must not load torch's bundled HIP runtime into the test process,
+where libgymflock would then bind it instead of the ROCm runtime it was built against."""
+import multiprocessing as mp
 import os
 import socket
 import sys
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 from conftest import ROOT
 
