@@ -454,6 +454,85 @@ def bench_dropin(args):
     return out
 
 
+def bench_dropin_coverage(args):
+    """The reference driver's loop (test.py:43-74) on one Coverage-v0 env through the
+    drop-in API: `env.step(env.controller(random=True))` and `env.step(env.controller(
+    greedy=True))`, whole episodes (reset every EPISODE_LENGTH steps or at done; resets
+    untimed), per call, at R=6 (the module defaults: 500 padded nodes, nearby starts) and
+    R=200 (max_nodes 1000, starts anywhere, as config 4). "direct" (the env default) is one
+    cov_step_host call per step (the greedy actions of the next state fused into it);
+    "getters" is cov_step then the observation and reward getters. The CPU side: the
+    reference's own step op sequence (oracle/cpu_ref_coverage.py) with np.random choices,
+    and with the greedy expert of oracle/coverage.py (a vectorised port, faster than the
+    reference's controller) plus its time matrix per map."""
+    from gym_flock.envs.spatial import CoverageEnv
+    out = {}
+    for R, M, nearby, episodes in ((6, 500, True, 6), (200, 1000, False, 3)):
+        row = {}
+        for mode in ("getters", "direct"):
+            for pol in ("random", "greedy"):
+                np.random.seed(8)
+                env = CoverageEnv(n_robots=R, nearby_starts=nearby, max_nodes=M)
+                env.fetch_mode = mode
+                env.seed(3)
+                steps, el, first, el_first = 0, 0.0, 0, 0.0
+                for ep in range(episodes + 1):  # the first episode warms up (not counted)
+                    env.reset()
+                    done, k = False, 0
+                    while not done:
+                        t0 = time.perf_counter()
+                        a = env.controller(random=True) if pol == "random" else env.controller(greedy=True)
+                        _, _, done, _ = env.step(a)
+                        dt = time.perf_counter() - t0
+                        if ep > 0:
+                            steps += 1
+                            el += dt
+                            if k == 0:
+                                first += 1
+                                el_first += dt
+                        k += 1
+                env.close()
+                r = {"step_ms": 1e3 * el / steps, "steps": steps}
+                if pol == "greedy":  # the first step of an episode builds the new map's time matrix
+                    r["step_ms_after_first"] = 1e3 * (el - el_first) / max(1, steps - first)
+                    r["first_step_ms"] = 1e3 * el_first / max(1, first)
+                row["%s_%s" % (mode, pol)] = r
+        if not args.no_cpu_baseline:
+            from oracle import coverage as oc
+            from oracle.cpu_ref_coverage import CpuCoverage
+            from gym_flock.envs.spatial.maps import generate_targets
+            np.random.seed(8)
+            targets = generate_targets()
+            T = len(targets)
+            rs = np.random.RandomState(0)
+            cpu = CpuCoverage(targets, R, M)
+            cpu.reset(rs.choice(T, R, replace=False), rs.choice(T, T // 2, replace=False) + R)
+            k = 40 if R <= 6 else 5
+            t0 = time.perf_counter()
+            for _ in range(k):
+                cpu.step(rs.choice(4, size=(R, 1)))
+            row["cpu_ref_1core_random"] = {"step_ms": 1e3 * (time.perf_counter() - t0) / k,
+                                           "kind": "reference op sequence (oracle/cpu_ref_coverage.py)"}
+            o = oc.CoverageOracle(targets, R, M)
+            t0 = time.perf_counter()
+            cost, prev = oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R)
+            tm = time.perf_counter() - t0
+            o.reset(rs.choice(T, R, replace=False), rs.choice(T, T // 2, replace=False) + R)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                cur = o.closest()
+                a, _ = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+                o.step(a)
+            row["cpu_port_1core_greedy"] = {"step_ms": 1e3 * (time.perf_counter() - t0) / k,
+                                            "time_matrix_ms_per_map": 1e3 * tm,
+                                            "kind": "port (oracle/coverage.py, NumPy, 1 thread)"}
+        out["r%d" % R] = row
+    out["note"] = ("per call of env.step(env.controller(...)) on one CoverageEnv, whole episodes after one warm-up "
+                   "episode, resets untimed; the map is regenerated at every reset as in the reference, so a greedy "
+                   "episode's first step builds its time matrix (first_step_ms)")
+    return out
+
+
 def bench_greedy(v, targets, R, M, B, K, args):
     """§8f: the greedy expert (controller(greedy=True)) on the same batch: the per-graph
     time-matrix build for all B envs, then K expert steps (device controller + step,
@@ -930,6 +1009,8 @@ def main():
             line["n8192_config5"] = bench_config5(args)
             log("drop-in single-env path (N=100, 1024)...")
             line["dropin"] = bench_dropin(args)
+            log("drop-in Coverage env (R=6, 200)...")
+            line["dropin_coverage"] = bench_dropin_coverage(args)
         if not args.no_cpu_baseline:
             # rank 0 after the timed region (the other ranks are done stepping): the same
             # host-core baseline beside every world size's line

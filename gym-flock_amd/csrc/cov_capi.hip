@@ -92,6 +92,7 @@ struct cov_handle {
   int64_t timing_count = 0;
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
+  int32_t* herr = nullptr;  // cov_step_host: page-locked per-env copies of the error word
 };
 
 namespace {
@@ -129,6 +130,7 @@ void cov_release(cov_handle* h) {
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
+  if (h->herr) hipHostFree(h->herr);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1]})
     if (e) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -497,6 +499,107 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
   }
   if (!(flags & (COV_ACTIONS_DEVICE | COV_ACTIONS_RESIDENT | COV_ACTIONS_GREEDY)))
     CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// The device address of page-locked host memory, or nullptr (pageable; its failed
+// lookup's error is cleared so later launch checks do not see it).
+template <class T>
+T* cov_mapped(T* p) {
+  if (!p) return nullptr;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return static_cast<T*>(d);
+}
+}  // namespace
+
+extern "C" {
+
+int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* edges, int32_t* senders,
+                  int32_t* receivers, int64_t* step, double* reward, uint8_t* done, int32_t* closest,
+                  int32_t* next_actions, uint8_t* needs_random, int flags) {
+  if (!h || !actions) return cfail(GF_EINVAL, "null argument");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (flags & ~COV_NEXT_GREEDY) return cfail(GF_EINVAL, "flags: 0 or COV_NEXT_GREEDY");
+  const bool ng = flags & COV_NEXT_GREEDY;
+  if (!ng && (next_actions || needs_random)) return cfail(GF_EINVAL, "next_actions / needs_random need COV_NEXT_GREEDY");
+  const size_t B = h->cfg.n_envs, R = h->cfg.n_robots, M = h->cfg.max_nodes, E = 4 * M, n = B * R;
+  for (size_t k = 0; k < n; ++k)
+    if (actions[k] < 0 || actions[k] >= 4) return cfail(GF_EINVAL, "action outside [0, 4) (coverage.py:189 index)");
+  // one launch on the handle's stream after everything outstanding on both streams
+  if (int rc = use(h)) return rc;
+  gf::CovArgs a = h->a;
+  if (ng) {
+    if (!h->tm_ready || !h->tm_glist)
+      if (int rc = ensure_time_matrix(h)) return rc;
+    if (!h->tm_glist)
+      return cfail(GF_EINVAL, "COV_NEXT_GREEDY needs max_nodes - n_robots <= 1024 (the per-node greedy lists)");
+    a.next_greedy = 1;
+    a.glist = h->tm_glist;
+    a.glen = h->tm_glen;
+    a.gstride = h->gstride;
+    a.gactions = h->actions;  // the next expert actions stay resident as well
+    a.needs_random = h->needs_random;
+  }
+  // page-locked destinations are written by the step's own workgroups through their
+  // mapped addresses; any other one gets a copy after the launch
+  a.h_nodes = cov_mapped(nodes);
+  a.h_edges = cov_mapped(edges);
+  a.h_senders = cov_mapped(senders);
+  a.h_receivers = cov_mapped(receivers);
+  a.h_step = cov_mapped(step);
+  a.h_reward = cov_mapped(reward);
+  a.h_done = cov_mapped(done);
+  a.h_closest = cov_mapped(closest);
+  a.h_next = cov_mapped(next_actions);
+  a.h_nrand = cov_mapped(needs_random);
+  // the device error word of each env as its workgroup ends, in page-locked scratch
+  if (!h->herr) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(B, 16) * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
+      return cfail(GF_ENOMEM, "hipHostMalloc (error words)");
+    h->herr = static_cast<int32_t*>(p);
+  }
+  std::memset(h->herr, 0, B * sizeof(int32_t));
+  a.h_err = cov_mapped(h->herr);
+  hipError_t e;
+  if (n * 4 <= (size_t)gf::kCovUInlineBytes) {
+    e = gf::launch_cov_step_uin(a, actions, h->stream);  // actions in the kernel arguments
+  } else {
+    CV_HIP(hipMemcpyAsync(h->actions, actions, n * 4, hipMemcpyHostToDevice, h->stream));
+    a.actions = h->actions;
+    e = gf::launch_cov_step(a, h->stream);
+  }
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
+  const gf::CovArgs& d = h->a;
+  if (nodes && !a.h_nodes) CV_HIP(hipMemcpyAsync(nodes, d.nodes, B * M * 3 * 4, hipMemcpyDeviceToHost, h->stream));
+  if (edges && !a.h_edges) CV_HIP(hipMemcpyAsync(edges, d.edges, B * E * 4, hipMemcpyDeviceToHost, h->stream));
+  if (senders && !a.h_senders) CV_HIP(hipMemcpyAsync(senders, d.senders, B * E * 4, hipMemcpyDeviceToHost, h->stream));
+  if (receivers && !a.h_receivers)
+    CV_HIP(hipMemcpyAsync(receivers, d.receivers, B * E * 4, hipMemcpyDeviceToHost, h->stream));
+  if (step && !a.h_step) CV_HIP(hipMemcpyAsync(step, d.obs_step, B * 8, hipMemcpyDeviceToHost, h->stream));
+  if (reward && !a.h_reward) CV_HIP(hipMemcpyAsync(reward, d.reward, B * 8, hipMemcpyDeviceToHost, h->stream));
+  if (done && !a.h_done) CV_HIP(hipMemcpyAsync(done, d.done, B, hipMemcpyDeviceToHost, h->stream));
+  if (closest && !a.h_closest) CV_HIP(hipMemcpyAsync(closest, d.cur, n * 4, hipMemcpyDeviceToHost, h->stream));
+  if (next_actions && !a.h_next) CV_HIP(hipMemcpyAsync(next_actions, h->actions, n * 4, hipMemcpyDeviceToHost, h->stream));
+  if (needs_random && !a.h_nrand)
+    CV_HIP(hipMemcpyAsync(needs_random, h->needs_random, n, hipMemcpyDeviceToHost, h->stream));
+  // spin on the stream: a drop-in step is latency-bound (a blocking wait's wake-up costs
+  // a sizeable part of it)
+  for (;;) {
+    const hipError_t q = hipStreamQuery(h->stream);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return cfail(GF_EHIP, std::string("cov_step_host: ") + hipGetErrorString(q));
+  }
+  int err = 0;
+  for (size_t b = 0; b < B; ++b) err |= h->herr[b];
+  if (err) return check_err(h);  // reads, clears and reports the device error word
   return GF_OK;
 }
 

@@ -42,6 +42,30 @@ struct CovArgs {
   int gstride;
   int32_t* gactions;      // (B,R) the greedy actions taken (written)
   uint8_t* needs_random;  // (B,R) robots the reference hands to np_random.choice (action 0 here)
+  // cov_step_host: after the step, controller(greedy=True)'s actions of the RESULTING state
+  // from the greedy lists (glist / glen / gstride) into gactions / needs_random (and the
+  // host copies below), for the next step of an expert loop
+  int next_greedy;
+  // cov_step_host: every output of the env written by the step's own workgroup to page-
+  // locked host memory (mapped device addresses) at its end; any may be nullptr
+  float* h_nodes;         // (B,M,3)
+  float* h_edges;         // (B,4M)
+  int32_t* h_senders;     // (B,4M)
+  int32_t* h_receivers;   // (B,4M)
+  int64_t* h_step;        // (B)
+  double* h_reward;       // (B)
+  uint8_t* h_done;        // (B)
+  int32_t* h_closest;     // (B,R) each robot's node after the step (closest_targets, global)
+  int32_t* h_next;        // (B,R) next_greedy actions
+  uint8_t* h_nrand;       // (B,R) next_greedy needs_random flags
+  int32_t* h_err;         // (B) the device error word as this env's workgroup ends
+};
+
+// cov_step_host: one env's actions travel in the kernel arguments up to this many bytes
+constexpr int kCovUInlineBytes = 2048;
+struct CovArgsU {
+  CovArgs a;
+  alignas(16) int32_t u[kCovUInlineBytes / 4];
 };
 
 // Greedy lists (built with the time matrix, cov_greedy_list_kernel): for every source
@@ -164,5 +188,8 @@ hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s);
 hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_t* visited0, hipStream_t s);
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s);
+// the step with a.actions read from `u` (host memory, copied into the kernel arguments;
+// B * R * 4 <= kCovUInlineBytes)
+hipError_t launch_cov_step_uin(const CovArgs& a, const int32_t* u, hipStream_t s);
 
 }  // namespace gf

@@ -12,6 +12,9 @@
 // leaves the arrays equal to what the reference rebuilds every step.
 #include <limits.h>
 
+#include <cstring>
+#include <type_traits>
+
 #include "coverage_internal.h"
 
 namespace gf {
@@ -163,8 +166,19 @@ __device__ __forceinline__ int action_node(const int32_t* nbr, const int32_t* cn
 // node's position, visited flag, neighbours and their coordinates (cov_graph_kernel's
 // table) together, and rewrites its 8 tail edges; a robot that stayed keeps its edges.
 // After an external placement, a new graph or a reset, everything is recomputed.
-template <int NT>
-__global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
+// UIN (cov_step_host): the env batch's actions arrive in the kernel arguments (CovArgsU)
+// instead of being read from memory, one dependent round trip fewer.
+template <int NT, bool UIN = false>
+__global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<UIN, CovArgsU, CovArgs>::type p) {
+  [[maybe_unused]] CovArgs uargs;
+  if constexpr (UIN) {
+    uargs = p.a;
+    uargs.actions = p.u;
+  }
+  const CovArgs& a = *[&]() -> const CovArgs* {
+    if constexpr (UIN) return &uargs;
+    else return &p;
+  }();
   constexpr int RPT = kCovThreads / NT;  // robots per thread when R <= kCovThreads
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = a.env0 + blockIdx.x;
@@ -202,7 +216,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
   GF_COV_STAMP(0);
   const int32_t* act = a.actions ? a.actions + (size_t)b * R : nullptr;
   // COV_ACTIONS_GREEDY: controller(greedy=True) picks each robot's action in this launch
-  const bool greedy = a.glist != nullptr;
+  const bool greedy = a.glist != nullptr && !a.next_greedy;
   const bool has_act = act || greedy;
   // One robot per thread (R <= NT): the data of the node a robot will end on
   // (if it moves: the chosen node; in a full pass: its node) is loaded right after the
@@ -253,7 +267,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
   const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
   const bool full = dirty || !has_act;  // recompute every robot's action edges
   const bool any_vis = nv0 > 0;
-  if (greedy) {
+  if (greedy || a.next_greedy) {
     // the env's visited flags as bits, before this step marks any (ballots, no atomics),
     // read after the robots' loads are in flight
     const int lane = tid & 63, wv = tid >> 6;
@@ -505,15 +519,68 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(CovArgs a) {
   }
   GF_COV_STAMP(3);
   __syncthreads();
+  const int newly = *counter;
+  const int nv = nv0 + newly;
   if (tid == 0) {
-    const int newly = *counter;
-    const int nv = nv0 + newly;
     a.nvisited[b] = nv;
     a.obs_step[b] = sc0;
     a.step_counter[b] = sc0 + 1;
     a.reward[b] = static_cast<double>(newly);
     a.done[b] = (sc0 + 1 == a.episode_length || nv == T) ? 1 : 0;
     a.dirty[b] = 0;
+  }
+  if (a.next_greedy) {
+    // controller(greedy=True) (:800-872) on the resulting state, for the next step of an
+    // expert loop: this step's visits (the `seen` node bits) joined to the visited bits,
+    // then each robot's first unmasked entry of its new node's greedy list
+    for (int t = tid; t < T; t += NT) {
+      const int n = t + R;
+      if ((seen[n >> 5] >> (n & 31)) & 1u) atomicOr(&gvis[t >> 5], 1u << (t & 31));
+    }
+    __syncthreads();
+    for (int i = tid; i < R; i += NT) {
+      const int c = new_s[i];
+      const size_t row = (size_t)b * Tm + (c - R);
+      const int g = greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, nv > 0, nv >= T);
+      const uint32_t flag = static_cast<uint32_t>(g) >> 2;
+      if (flag & kGreedyErr) atomicOr(a.err, 8);
+      const int ai = (flag & kGreedyRnd) ? 0 : (g & 3);
+      const uint8_t nr = (flag & kGreedyRnd) ? 1 : 0;
+      a.gactions[(size_t)b * R + i] = ai;
+      a.needs_random[(size_t)b * R + i] = nr;
+      if (a.h_next) a.h_next[(size_t)b * R + i] = ai;
+      if (a.h_nrand) a.h_nrand[(size_t)b * R + i] = nr;
+    }
+  }
+  if (a.h_nodes || a.h_edges || a.h_senders || a.h_receivers || a.h_closest || a.h_step || a.h_err) {
+    // cov_step_host: the env's whole observation and step outputs to page-locked host
+    // memory, 16-byte stores where both sides are aligned. The workgroup reads back what
+    // its own waves wrote above: after the barrier those stores are visible to it.
+    __syncthreads();
+    auto put = [&](auto* dst, const auto* src, size_t n) {
+      using T1 = typename std::remove_const<typename std::remove_pointer<decltype(src)>::type>::type;
+      static_assert(sizeof(T1) == 4, "4-byte elements");
+      if (!dst) return;
+      if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        const size_t n4 = n >> 2;
+        for (size_t k = tid; k < n4; k += NT) reinterpret_cast<int4*>(dst)[k] = reinterpret_cast<const int4*>(src)[k];
+        for (size_t k = (n4 << 2) + tid; k < n; k += NT) dst[k] = src[k];
+      } else {
+        for (size_t k = tid; k < n; k += NT) dst[k] = src[k];
+      }
+    };
+    put(a.h_nodes ? a.h_nodes + (size_t)b * M * 3 : nullptr, nodes, (size_t)M * 3);
+    put(a.h_edges ? a.h_edges + (size_t)b * E : nullptr, edg, (size_t)E);
+    put(a.h_senders ? a.h_senders + (size_t)b * E : nullptr, snd, (size_t)E);
+    put(a.h_receivers ? a.h_receivers + (size_t)b * E : nullptr, rcv, (size_t)E);
+    if (a.h_closest)
+      for (int i = tid; i < R; i += NT) a.h_closest[(size_t)b * R + i] = new_s[i];
+    if (tid == 0) {
+      if (a.h_step) a.h_step[b] = sc0;
+      if (a.h_reward) a.h_reward[b] = static_cast<double>(newly);
+      if (a.h_done) a.h_done[b] = (sc0 + 1 == a.episode_length || nv == T) ? 1 : 0;
+      if (a.h_err) a.h_err[b] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 #ifdef GF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -648,6 +715,18 @@ hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStr
 hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_t* visited0, hipStream_t s) {
   hipLaunchKernelGGL(cov_reset_kernel, dim3(a.B), dim3(kCovThreads), 0, s, a, start, visited0);
   return hipGetLastError();
+}
+
+hipError_t launch_cov_step_uin(const CovArgs& a, const int32_t* u, hipStream_t s) {
+  const size_t bytes = (size_t)a.B * a.R * 4;
+  if (bytes > (size_t)kCovUInlineBytes || !u) return hipErrorInvalidValue;
+  CovArgsU p;
+  p.a = a;
+  p.a.actions = nullptr;
+  std::memcpy(p.u, u, bytes);
+  void* args[] = {&p};
+  return hipLaunchKernel(reinterpret_cast<const void*>(&cov_step_kernel<kCovThreads, true>), dim3(a.B),
+                         dim3(kCovThreads), args, cov_step_lds_bytes(a.R, a.M), s);
 }
 
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {

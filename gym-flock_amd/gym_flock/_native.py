@@ -65,6 +65,7 @@ COV_ACTIONS_GREEDY = 0x20
 COV_OUT_DEVICE = 0x4
 COV_FLAT_F32 = 0x8
 COV_MASK_ALL = 0x10
+COV_NEXT_GREEDY = 0x40
 
 
 class GymFlockError(RuntimeError):
@@ -133,6 +134,7 @@ SIGNATURES = {
     "cov_reset": [_P, _P, _P],
     "cov_step": [_P, _P, _I],
     "cov_set_actions": [_P, _P],
+    "cov_step_host": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I],
     "cov_set_robot_positions": [_P, _I, _P],
     "cov_get_obs": [_P, _I, _P, _P, _P, _P, _P],
     "cov_get_rewards": [_P, _P, _P],
@@ -748,6 +750,18 @@ class CoverageHandle:
     def set_actions(self, actions):
         a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
         check(self.lib.cov_set_actions(self.h, ptr(a)))
+
+    def step_host(self, actions, nodes, edges, senders, receivers, step, reward, done, closest,
+                  next_actions=None, needs_random=None):
+        """cov_step_host: one launch and one wait; the arguments after `actions` (B,R) int32
+        are addresses (ints) of host destinations or None, page-locked ones written by the
+        kernel in place. With next_actions / needs_random, controller(greedy=True)'s actions
+        of the resulting state come back too (COV_NEXT_GREEDY)."""
+        flags = COV_NEXT_GREEDY if (next_actions is not None or needs_random is not None) else 0
+        rc = self.lib.cov_step_host(self.h, actions.ctypes.data, nodes, edges, senders, receivers, step, reward,
+                                    done, closest, next_actions, needs_random, flags)
+        if rc:
+            check(rc)
 
     def actions(self):
         """(resident actions (B,R) int32, needs_random (B,R) bool) of the last greedy call or

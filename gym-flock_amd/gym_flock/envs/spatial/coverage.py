@@ -85,6 +85,16 @@ class CoverageEnv(Env):
         self.step_counter = 0
         self.last_loc = None
         self.fig = None
+        # how step() runs: "direct" = one cov_step_host call (actions in the kernel
+        # arguments, observation / reward / done / each robot's new node written by the
+        # step into one pooled page-locked block, one wait); "getters" = cov_step, then
+        # the observation and reward getters (a host round trip each)
+        self.fetch_mode = "direct"
+        self._closest = None       # robots' nodes after the last step (the next last_loc)
+        self._want_greedy = False  # controller(greedy=True) in use: steps fuse the next one
+        self._greedy_cache = None  # (actions, needs_random) of the current state, device-made
+        self._abuf = None
+        self._layout = None
 
     def seed(self, seed=None):
         self.np_random, seed = np_random(seed)
@@ -102,6 +112,7 @@ class CoverageEnv(Env):
         self.n_agents = self.n_targets + self.n_robots
         self.max_edges = self.max_nodes * MAX_EDGES
         self._h.set_targets(self.targets, env=0)
+        self._closest = self._greedy_cache = None
         self.n_motion_edges = int(self._h.n_motion()[0])
         if self.nearby_starts:
             n_nearest = self.get_n_nearest(self.np_random.choice(self.n_targets), self.n_robots * NEARBY_DENSITY)
@@ -151,18 +162,65 @@ class CoverageEnv(Env):
         visited[0, drop - self.n_robots] = 0
         self._h.reset(starts[None], visited)
         self.step_counter = 1
+        self._closest = starts.astype(np.int64) + self.n_robots  # robots sit on their start targets
+        self._greedy_cache = None
         return self._h.obs(0)
 
     def step(self, action):
-        """coverage.py:174-204."""
-        if action is not None:
-            a = np.asarray(action).reshape(-1)
-            if a.shape[0] != self.n_robots or np.any((a < 0) | (a >= self.n_actions)):
-                raise IndexError("each robot's action must be in [0, %d)" % self.n_actions)
-            self.last_loc = self.closest_targets
+        """coverage.py:174-204 (with _get_obs_reward :234-364). In the default fetch mode
+        ("direct") one library call with one wait (cov_step_host): the actions travel in
+        the kernel arguments and the step writes the whole observation, reward, done flag
+        and each robot's new node (the next step's last_loc) into one pooled page-locked
+        block; once controller(greedy=True) is in use, the expert's actions for the
+        resulting state are computed in the same launch."""
+        if action is None:  # pragma: no cover (the reference skips the move)
+            self._h.step(np.zeros((1, self.n_robots)))
+            return self._obs_reward()
+        a = np.asarray(action).reshape(-1)
+        if a.shape[0] != self.n_robots or np.any((a < 0) | (a >= self.n_actions)):
+            raise IndexError("each robot's action must be in [0, %d)" % self.n_actions)
+        self.last_loc = self._closest if self._closest is not None else self.closest_targets
+        if self.fetch_mode != "direct":
             self._h.step(a[None])
-        else:
-            self._h.step(np.zeros((1, self.n_robots)))  # pragma: no cover
+            self._closest = self._greedy_cache = None
+            return self._obs_reward()
+        R, M = self.n_robots, self.max_nodes
+        if self._abuf is None:
+            self._abuf = np.empty((1, R), np.int32)
+        self._abuf[0] = a
+        ng = self._want_greedy
+        lay = self._layout
+        if lay is None or lay[0] != ng:
+            a64 = lambda b: (b + 63) & ~63  # noqa: E731
+            o = [0]
+            for nbytes in (12 * M, 16 * M, 16 * M, 16 * M, 8, 8, 1, 4 * R, 4 * R if ng else 0, R if ng else 0):
+                o.append(o[-1] + a64(nbytes))
+            lay = self._layout = (ng, o)
+        o = lay[1]
+        buf, base = nat.host_pool().block_addr(o[-1])
+        if buf is None:  # not page-locked (pool cap): the library copies after the launch
+            buf = np.empty(o[-1], np.uint8)
+            base = buf.ctypes.data
+        nodes = np.ndarray((M, 3), np.float32, buf, o[0])
+        edges = np.ndarray((4 * M, 1), np.float32, buf, o[1])
+        snd = np.ndarray((4 * M,), np.int32, buf, o[2])
+        rcv = np.ndarray((4 * M,), np.int32, buf, o[3])
+        stp = np.ndarray((1, 1), np.int64, buf, o[4])
+        rw = np.ndarray((1,), np.float64, buf, o[5])
+        dn = np.ndarray((1,), np.uint8, buf, o[6])
+        cl = np.ndarray((R,), np.int32, buf, o[7])
+        nxt = np.ndarray((R,), np.int32, buf, o[8]) if ng else None
+        nrd = np.ndarray((R,), np.uint8, buf, o[9]) if ng else None
+        self._h.step_host(self._abuf, base + o[0], base + o[1], base + o[2], base + o[3], base + o[4], base + o[5],
+                          base + o[6], base + o[7], base + o[8] if ng else None, base + o[9] if ng else None)
+        self._closest = cl.astype(np.int64)
+        self._greedy_cache = (nxt.copy(), nrd.astype(bool)) if ng else None
+        reward, done = float(rw[0]), bool(dn[0])
+        self.step_counter += 1
+        self.episode_reward += reward
+        return {"nodes": nodes, "edges": edges, "senders": snd, "receivers": rcv, "step": stp}, reward, done, {}
+
+    def _obs_reward(self):
         obs = self._h.obs(0)
         r, d = self._h.rewards()
         reward, done = float(r[0]), bool(d[0])
@@ -208,9 +266,14 @@ class CoverageEnv(Env):
             return self.np_random.choice(self.n_actions, size=(self.n_robots, 1))
         if not greedy:
             raise AssertionError("Vehicle routing controller is not available if OR-Tools is not imported.")
-        a, rnd = self._h.controller_greedy()
-        a = a[0].copy()
-        for i in np.nonzero(rnd[0])[0]:
+        self._want_greedy = True
+        if self._greedy_cache is not None:  # computed by the step that made this state
+            a, rnd = self._greedy_cache
+            a = a.copy()
+        else:
+            a, rnd = self._h.controller_greedy()
+            a, rnd = a[0].copy(), rnd[0]
+        for i in np.nonzero(rnd)[0]:
             a[i] = self.np_random.choice(self.n_actions)
         return a.reshape(self.n_robots, 1).astype(np.int32)
 

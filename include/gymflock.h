@@ -316,6 +316,23 @@ int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited);
 /* step(action) (:174-204, :234-364): actions[B][R] in [0,4). */
 int cov_step(cov_handle* h, const int32_t* actions, int flags);
 int cov_set_actions(cov_handle* h, const int32_t* actions);
+/* The drop-in env's step(action) (coverage.py:174-204 with _get_obs_reward :234-364) as
+ * one launch and one wait, the reference driver's loop (test.py:43-74): actions[B][R] in
+ * [0,4) (B*R <= 512: passed in the kernel arguments), then the whole observation of every
+ * env, step counter, reward, done flag and each robot's node after the step (the next
+ * step's last_loc, closest_targets :427-432) written to the given host arrays: nodes
+ * (B,M,3) f32, edges (B,4M) f32, senders / receivers (B,4M) i32, step (B) i64, reward (B)
+ * f64, done (B) u8, closest (B,R) i32. Page-locked destinations (fe_host_alloc) are
+ * written by the step's own workgroups through their mapped addresses, others by copies
+ * after it; any pointer may be NULL. flags: COV_NEXT_GREEDY also computes, in the same
+ * launch, controller(greedy=True)'s actions of the resulting state (:800-872) into
+ * next_actions (B,R) i32 and needs_random (B,R) u8 (robots the reference hands to
+ * np_random.choice(4), action 0 here), which also stay resident (COV_ACTIONS_RESIDENT);
+ * it builds the time matrices first if the graph changed. */
+#define COV_NEXT_GREEDY 0x40
+int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* edges, int32_t* senders,
+                  int32_t* receivers, int64_t* step, double* reward, uint8_t* done, int32_t* closest,
+                  int32_t* next_actions, uint8_t* needs_random, int flags);
 /* Place one env's robots anywhere (x[:R] = ...); closest targets are recomputed. */
 int cov_set_robot_positions(cov_handle* h, int env, const double* xr);
 /* Observation of one env (:353): nodes (M,3) f32, edges (4M) f32, senders/receivers

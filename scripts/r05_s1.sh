@@ -16,5 +16,7 @@ print("plain", d["ms_per_step"], d["roofline"]["frac"], "knn", d["flocking_v0_kn
 for n in ("n100", "n1024"):
     print(n, {k: {kk: round(vv * 1e3, 1) for kk, vv in v.items()} for k, v in d["dropin"][n].items()})
 print(d.get("runtime"))
+for r in ("r6", "r200"):
+    print(r, {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()} for k, v in d["dropin_coverage"][r].items()})
 PY
 exit $rc

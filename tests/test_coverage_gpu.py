@@ -146,21 +146,34 @@ def test_external_robot_positions_recompute_closest():
     h.close()
 
 
-def test_env_api_reproduces_reference_reset_and_episode():
+@pytest.mark.parametrize("mode", ["direct", "getters"])
+def test_env_api_reproduces_reference_reset_and_episode(mode):
     """CoverageEnv with the fixture's seeds regenerates the reference's map, starts and
-    unvisited set (global and env RNGs in the reference's call order)."""
+    unvisited set (global and env RNGs in the reference's call order), then replays the
+    recorded random episode. "direct" (the default) is one cov_step_host call per step:
+    every observation, reward and done flag as recorded, last_loc the robots' nodes
+    before the move (:183), and the arrays a step returned stay as they were after
+    later steps (fresh arrays per call)."""
     from gym_flock.envs.spatial import CoverageEnv
     f = np.load(os.path.join(GOLDEN, "coverage_r6_random.npz"))
     np.random.seed(3)
     env = CoverageEnv(n_robots=6, nearby_starts=False, max_nodes=500)
+    env.fetch_mode = mode
     env.seed(4)
     np.random.seed(3)
     obs = env.reset()
     assert_obs(obs, f)
+    kept = []
+    prev = env.closest_targets
     for t in range(len(f["actions"])):
         obs, r, d, _ = env.step(f["actions"][t].reshape(-1, 1))
+        np.testing.assert_array_equal(env.last_loc, prev)
+        prev = f["closest"][t]
         assert_obs(obs, f, t)
         assert r == f["reward"][t] and d == f["done"][t]
+        kept.append((t, obs))
+    for t, o in kept[::7]:
+        assert_obs(o, f, t)
     with pytest.raises(IndexError):
         env.step(np.full((6, 1), 4))
     env.close()

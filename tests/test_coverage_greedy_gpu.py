@@ -62,24 +62,35 @@ def test_greedy_episode_matches_reference(path):
     h.close()
 
 
+@pytest.mark.parametrize("mode", ["direct", "getters"])
 @pytest.mark.parametrize("path", GREEDY, ids=os.path.basename)
-def test_env_api_greedy_controller(path):
+def test_env_api_greedy_controller(path, mode):
     """CoverageEnv.controller(greedy=True) with the fixture's seeds reproduces the
-    reference's expert episode, including its np_random fallback draws."""
+    reference's expert episode, including its np_random fallback draws. "direct" (the
+    default): after the first controller() call every step is one cov_step_host launch
+    that also computes the expert's actions for the resulting state, which the next
+    controller() call takes (the fallback draws on the host, in robot order) without a
+    device call. Observations, rewards, done flags and the robots' nodes as recorded."""
     from gym_flock.envs.spatial import CoverageEnv
     f = np.load(path)
     name = os.path.basename(path)
     np.random.seed(MAP_SEED[name])
     env = CoverageEnv(n_robots=int(f["n_robots"]), nearby_starts=False, max_nodes=int(f["max_nodes"]))
+    env.fetch_mode = mode
     env.seed(ENV_SEED[name])
     np.random.seed(MAP_SEED[name])
     env.reset()
     for t in range(len(f["actions"])):
+        if mode == "direct" and t > 0:
+            assert env._greedy_cache is not None  # made by the previous step's launch
         a = env.controller(random=False, greedy=True)
         assert a.shape == (int(f["n_robots"]), 1) and a.dtype == np.int32
         np.testing.assert_array_equal(a[:, 0], f["actions"][t])
-        _, r, d, _ = env.step(a)
+        obs, r, d, _ = env.step(a)
         assert r == f["reward"][t] and d == f["done"][t]
+        for k in ("nodes", "edges", "senders", "receivers", "step"):
+            np.testing.assert_array_equal(obs[k].reshape(f[k][t].shape), f[k][t], err_msg=k)
+        np.testing.assert_array_equal(env.closest_targets, f["closest"][t])
     np.testing.assert_array_equal(env.graph_cost, f["graph_cost"])
     np.testing.assert_array_equal(env.graph_previous, f["graph_previous"])
     with pytest.raises(AssertionError):
@@ -326,3 +337,54 @@ def test_fused_greedy_deep_list_scans_vs_oracle():
         np.testing.assert_array_equal(h.robots(0)[1], o.closest())
     assert max(depths) > 64, depths  # scans past two round trips of the loader
     h.close()
+
+
+def test_cov_step_host_batched_matches_step_and_getters():
+    """cov_step_host on a batch of 3 envs with distinct maps, page-locked destinations
+    (written by the step's own workgroups) on even steps and pageable numpy arrays (copies
+    after the launch) on odd steps, with COV_NEXT_GREEDY: every env's observation, step,
+    reward, done, robot nodes and next greedy actions equal those of cov_step + the
+    getters + cov_controller_greedy on a second handle stepped with the same actions."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, R, M = 3, 10, 700
+    maps = []
+    for b in range(B):
+        np.random.seed(300 + b)
+        maps.append(generate_targets())
+    hs = [nat.CoverageHandle(R, B, M) for _ in range(2)]
+    rs = np.random.RandomState(31)
+    start = np.stack([rs.choice(len(maps[b]), R, replace=False) for b in range(B)]).astype(np.int32)
+    visited = np.ones((B, M - R), np.uint8)
+    for b in range(B):
+        visited[b, :len(maps[b])] = rs.randint(0, 2, len(maps[b]))
+    for h in hs:
+        for b in range(B):
+            h.set_targets(maps[b], env=b)
+        h.reset(start, visited)
+    pool = nat.host_pool()
+    for t in range(12):
+        a = rs.randint(0, 4, size=(B, R)).astype(np.int32)
+        new = pool.array if t % 2 == 0 else (lambda shape, dt: np.empty(shape, dt))
+        o = dict(nodes=new((B, M, 3), np.float32), edges=new((B, 4 * M), np.float32),
+                 senders=new((B, 4 * M), np.int32), receivers=new((B, 4 * M), np.int32),
+                 step=new((B,), np.int64), reward=new((B,), np.float64), done=new((B,), np.uint8),
+                 closest=new((B, R), np.int32), nxt=new((B, R), np.int32), nrd=new((B, R), np.uint8))
+        hs[0].step_host(a, *(o[k].ctypes.data for k in ("nodes", "edges", "senders", "receivers", "step", "reward",
+                                                         "done", "closest", "nxt", "nrd")))
+        hs[1].step(a)
+        r1, d1 = hs[1].rewards()
+        np.testing.assert_array_equal(o["reward"], r1)
+        np.testing.assert_array_equal(o["done"].astype(bool), d1)
+        ga, gr = hs[1].controller_greedy()
+        np.testing.assert_array_equal(o["nxt"], ga)
+        np.testing.assert_array_equal(o["nrd"].astype(bool), gr)
+        for b in range(B):
+            ob = hs[1].obs(b)
+            np.testing.assert_array_equal(o["nodes"][b], ob["nodes"])
+            np.testing.assert_array_equal(o["edges"][b], ob["edges"][:, 0])
+            np.testing.assert_array_equal(o["senders"][b], ob["senders"])
+            np.testing.assert_array_equal(o["receivers"][b], ob["receivers"])
+            assert o["step"][b] == ob["step"][0, 0]
+            np.testing.assert_array_equal(o["closest"][b], hs[1].robots(b)[1])
+    for h in hs:
+        h.close()
