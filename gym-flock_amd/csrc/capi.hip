@@ -123,26 +123,20 @@ struct fe_handle {
   int max_envs = 0;
   std::vector<int32_t> shard_sizes;     // every rank's n_envs (fe_comm_init's exchange)
   double comm_timeout = kCommInitTimeoutS;  // bound on every wait for a collective
-  // The staging copies into the send blocks run on stage_stream, which waits only for the
-  // step streams, never for a collective: the ring slots a step overwrites are therefore
-  // released by the steps' own progress, and a collective stuck on a dead peer cannot
-  // hold the step streams (they wait only on staging events). A send block is reused
-  // only after the host has seen (bounded, comm_event_wait) the collective that read it
-  // complete; the reward send block is double-buffered so that this is the collective
-  // two gathers back.
-  hipStream_t stage_stream = nullptr;
-  double* gsend[2] = {nullptr, nullptr};  // kRewardSlots x max_envs each: the gathered steps, padded
-  hipEvent_t ag_done[2] = {nullptr, nullptr};  // the reward collective that read gsend[k]
-  bool ag_live[2] = {false, false};
-  int64_t n_gathers = 0;                // reward gathers issued (send block = count % 2)
-  hipEvent_t stage_ev = nullptr;        // the latest staging copy (the collective waits for it)
+  // The step streams never wait on the side stream on the device: a collective stuck on
+  // a dead peer (and, through it, everything queued behind it) must not stall the steps.
+  // A step about to overwrite a ring slot that a gather's staging copy has not read yet
+  // waits for that copy on the host, bounded by comm_timeout (next_reward_slot); normally
+  // the copy finished long before (the slot was written kRewardSlots steps ago).
+  double* gsend = nullptr;              // kRewardSlots x max_envs: the gathered steps, padded
+  std::string comm_lost;                // why a step call tore the metrics path down
   double* gather = nullptr;             // nranks x kRewardSlots x max_envs
   hipEvent_t step_ev = nullptr;
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
   hipEvent_t ag_ev = nullptr;           // completion of the latest reward all-gather
   // ring slots a reward gather's staging copy still reads: steps [first, ...) until ev
-  // (an event on stage_stream)
+  // (an event on the side stream)
   struct RingRead {
     int64_t first;
     hipEvent_t ev;
@@ -157,8 +151,6 @@ struct fe_handle {
   double* stats_gather = nullptr;       // nranks x max_envs x 2 (fe_allgather_stats)
   hipEvent_t sg_ev = nullptr;           // completion of the latest stats all-gather
   bool sg_pending = false;
-  hipEvent_t ss_copy_ev = nullptr;      // stats_sum -> ssend staging copy (stage_stream)
-  bool ss_copy_pending = false;
   // fe_debug_comm_gate: a bounded spin kernel on comm_stream, released by this page-locked
   // flag, stands in for a collective whose peer stopped responding (tests only)
   unsigned* gate_flag = nullptr;
@@ -386,20 +378,21 @@ bool comm_stream_drained(fe_handle* h) {
 //
 // abort: a collective (or the initialisation) may never finish because a peer is gone.
 // The communicator is then aborted on the process's communicator worker, and the side
-// stream, the events it waits on and the buffers its collectives use are abandoned
-// rather than synchronised or freed (a kernel of the aborted collective may still touch
-// them), so that this call cannot hang. The staging stream is drained and released: it
-// waits only for the step streams, never for a collective. A non-abort release whose
-// side stream does not drain within the collective timeout becomes an abort.
+// stream, its events and the buffers its collectives use are abandoned rather than
+// synchronised or freed (a kernel of the aborted collective may still touch them), so
+// that this call cannot hang; the step streams never wait on the side stream. A
+// non-abort release whose side stream does not drain within the collective timeout
+// becomes an abort.
 void comm_release(fe_handle* h, bool abort) {
   if (!abort && h->comm && !comm_stream_drained(h)) abort = true;
   if (abort) {
     if (h->comm) abort_comm_later(h->comm, h->cfg.device);
     h->comm = nullptr;
     h->comm_stream = nullptr;
-    h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = h->stage_ev = nullptr;
-    h->ag_done[0] = h->ag_done[1] = nullptr;
-    h->gsend[0] = h->gsend[1] = h->gather = h->ssend = h->stats_gather = nullptr;
+    h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = nullptr;
+    h->ring_reads.clear();  // events the side stream may still record: abandoned
+    h->ev_free.clear();
+    h->gsend = h->gather = h->ssend = h->stats_gather = nullptr;
   }
   if (h->comm) {
     ncclCommDestroy(h->comm);
@@ -410,13 +403,7 @@ void comm_release(fe_handle* h, bool abort) {
     hipStreamDestroy(h->comm_stream);
     h->comm_stream = nullptr;
   }
-  if (h->stage_stream) {
-    hipStreamSynchronize(h->stage_stream);  // behind the step streams only
-    hipStreamDestroy(h->stage_stream);
-    h->stage_stream = nullptr;
-  }
-  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev, &h->stage_ev, &h->ss_copy_ev,
-                        &h->ag_done[0], &h->ag_done[1]})
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev})
     if (*e) {
       hipEventDestroy(*e);
       *e = nullptr;
@@ -425,14 +412,12 @@ void comm_release(fe_handle* h, bool abort) {
   h->ring_reads.clear();
   for (hipEvent_t e : h->ev_free) hipEventDestroy(e);
   h->ev_free.clear();
-  for (double** p : {&h->gsend[0], &h->gsend[1], &h->gather, &h->ssend, &h->stats_gather})
+  for (double** p : {&h->gsend, &h->gather, &h->ssend, &h->stats_gather})
     if (*p) {
       hipFree(*p);
       *p = nullptr;
     }
-  h->ag_issued = h->sg_pending = h->ss_copy_pending = false;
-  h->ag_live[0] = h->ag_live[1] = false;
-  h->n_gathers = 0;
+  h->ag_issued = h->sg_pending = false;
   h->last_count = 0;
   h->nranks = 1;
   h->rank = 0;
@@ -470,18 +455,34 @@ int check_env(const fe_handle* h, int env) {
 
 double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h->cfg.n_envs; }
 
+int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what);
+
+int no_comm(const fe_handle* h) {
+  return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down" +
+                             (h->comm_lost.empty() ? std::string(")") : ": " + h->comm_lost + ")"));
+}
+
 // Advance the reward ring before a launch that writes rewards. The slot last held the
-// step kRewardSlots launches back; if a reward gather's staging copy may still read it,
-// both step streams wait for that copy first (a device-side wait, no host sync). The copy
-// runs on the staging stream behind the steps it reads and nothing else, so this wait
-// can never be held by a collective.
+// step kRewardSlots launches back. A reward gather's staging copy (on the side stream,
+// behind the previous collectives) that may still read it has normally finished long
+// ago: its event is queried on the host. If not, the host waits for it, bounded by the
+// collective timeout; on expiry (a collective stuck on a peer that stopped responding)
+// the metrics path is torn down (the communicator aborted, the reason kept for the next
+// metrics call) and the step goes on. The step streams never wait on the side stream on
+// the device, so nothing queued behind a stuck collective can stall them.
 int next_reward_slot(fe_handle* h) {
   const int64_t s = h->steps_written;
   h->rslot = static_cast<int>(s % kRewardSlots);
   while (!h->ring_reads.empty() && h->ring_reads.front().first <= s - kRewardSlots) {
     const hipEvent_t e = h->ring_reads.front().ev;
-    GF_HIP(hipStreamWaitEvent(h->stream, e, 0));
-    if (h->stream2) GF_HIP(hipStreamWaitEvent(h->stream2, e, 0));
+    const hipError_t q = hipEventQuery(e);
+    if (q != hipSuccess) {
+      if (q != hipErrorNotReady) return fail_hip("reward gather staging copy", q);
+      if (comm_event_wait(h, e, "reward all-gather staging copy (ring slot reuse)") != GF_OK) {
+        h->comm_lost = g_err;  // comm_release emptied ring_reads: the step goes on
+        break;
+      }
+    }
     h->ring_reads.pop_front();
     h->ev_free.push_back(e);
   }
@@ -1264,8 +1265,8 @@ int fe_get_stats_ex(fe_handle* h, int env, double* vel_diffs, double* min_dists,
 namespace {
 // get_stats (:136-143) on every env of the current state, then each env's means of the
 // two arrays into stats_sum (B,2), on the handle's stream. A pending stats gather's
-// staging copy still reads stats_sum: the stream waits for that copy first (on the
-// staging stream, behind the step streams only: never behind a collective).
+// staging copy may still read stats_sum: the host waits for that gather (bounded, as
+// next_reward_slot; on expiry the metrics path is torn down and the summary goes on).
 int stats_summary_dev(fe_handle* h) {
   if (!h->vel_diffs) {
     if (int rc = dalloc(&h->vel_diffs, h->BN)) return rc;
@@ -1274,9 +1275,11 @@ int stats_summary_dev(fe_handle* h) {
   }
   if (!h->stats_sum)
     if (int rc = dalloc(&h->stats_sum, (size_t)h->cfg.n_envs * 2)) return rc;
-  if (h->ss_copy_pending) {
-    GF_HIP(hipStreamWaitEvent(h->stream, h->ss_copy_ev, 0));
-    h->ss_copy_pending = false;
+  if (h->sg_pending && h->comm) {
+    const hipError_t q = hipEventQuery(h->sg_ev);
+    if (q != hipSuccess && q != hipErrorNotReady) return fail_hip("stats all-gather", q);
+    if (q == hipErrorNotReady && comm_event_wait(h, h->sg_ev, "stats all-gather (send block reuse)") != GF_OK)
+      h->comm_lost = g_err;
   }
   gf::StatsArgs s{h->x[h->cur], h->vel_diffs, h->min_dists, h->degree,
                   h->cfg.comm_radius * h->cfg.comm_radius, h->cfg.n_agents, h->cfg.n_envs};
@@ -1461,7 +1464,6 @@ int fe_sync(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (int rc = use_dev(h)) return rc;
   GF_HIP(hipStreamSynchronize(h->stream));
-  if (h->stage_stream) GF_HIP(hipStreamSynchronize(h->stage_stream));  // behind the steps only
   if (h->comm && !comm_stream_drained(h)) {
     comm_release(h, true);
     return fail(GF_ECOMM, "fe_sync: a collective did not complete within the timeout (a rank stopped "
@@ -1674,7 +1676,9 @@ int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
       rc = fail(GF_ECOMM, "shard-size all-gather: timed out (a rank stopped responding)");
     } else if (q != hipSuccess) {
       rc = fail(GF_EHIP, std::string("shard-size all-gather: ") + hipGetErrorString(q));
-    } else if (hipMemcpy(sizes.data(), dsz, 4 * (size_t)nranks, hipMemcpyDeviceToHost) != hipSuccess) {
+    } else if (hipMemcpyAsync(sizes.data(), dsz, 4 * (size_t)nranks, hipMemcpyDeviceToHost, h->comm_stream) !=
+                   hipSuccess ||
+               hipStreamSynchronize(h->comm_stream) != hipSuccess) {
       rc = fail(GF_EHIP, "shard-size copy");
     } else {
       rc = fe_check_shard_sizes(nranks, sizes.data());
@@ -1685,12 +1689,9 @@ int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
   h->shard_sizes = sizes;
   h->max_envs = *std::max_element(sizes.begin(), sizes.end());
   const size_t W = h->max_envs;
-  GF_HIP(hipStreamCreateWithFlags(&h->stage_stream, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev, &h->stage_ev, &h->ss_copy_ev, &h->ag_done[0],
-                        &h->ag_done[1]})
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev})
     GF_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  if ((rc = comm_alloc(h, &h->gsend[0], (size_t)kRewardSlots * W)) ||
-      (rc = comm_alloc(h, &h->gsend[1], (size_t)kRewardSlots * W)) ||
+  if ((rc = comm_alloc(h, &h->gsend, (size_t)kRewardSlots * W)) ||
       (rc = comm_alloc(h, &h->gather, (size_t)nranks * kRewardSlots * W)) || (rc = comm_alloc(h, &h->ssend, W * 2)) ||
       (rc = comm_alloc(h, &h->stats_gather, (size_t)nranks * W * 2)))
     return rc;
@@ -1761,6 +1762,7 @@ int fe_comm_init_timeout(fe_handle* h, int nranks, int rank, const uint8_t id[12
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
   h->comm = job->comm;
+  h->comm_lost.clear();
   const ncclResult_t r = job->r;
   if (r != ncclSuccess && r != ncclInProgress) {
     comm_release(h, true);
@@ -1781,7 +1783,7 @@ int fe_comm_init(fe_handle* h, int nranks, int rank, const uint8_t id[128]) {
 
 int fe_comm_info(fe_handle* h, int32_t* count, int32_t* user_rank, int32_t* device, char* bus_id, int bus_id_len) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->comm) return no_comm(h);
   int c = 0, ur = 0, d = 0;
   ncclResult_t r = ncclCommCount(h->comm, &c);
   if (r == ncclSuccess) r = ncclCommUserRank(h->comm, &ur);
@@ -1796,7 +1798,7 @@ int fe_comm_info(fe_handle* h, int32_t* count, int32_t* user_rank, int32_t* devi
 
 int fe_comm_shard_sizes(fe_handle* h, int32_t* sizes, int32_t* max_envs) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->comm) return no_comm(h);
   if (sizes) std::copy(h->shard_sizes.begin(), h->shard_sizes.end(), sizes);
   if (max_envs) *max_envs = h->max_envs;
   return GF_OK;
@@ -1804,7 +1806,7 @@ int fe_comm_shard_sizes(fe_handle* h, int32_t* sizes, int32_t* max_envs) {
 
 int fe_allgather_rewards(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->comm) return no_comm(h);
   // a step-path call: the gather's stream waits for both step streams' latest work
   // (events only), so back-to-back split steps around it stay split and out of phase
   // (use_dev's join would make the next step a single launch)
@@ -1820,30 +1822,24 @@ int fe_allgather_rewards(fe_handle* h) {
                                std::to_string(kRewardSlots) + " steps)");
   }
   const size_t B = h->cfg.n_envs, W = h->max_envs;
-  // the send block this gather stages into was read by the collective two gathers back:
-  // the host confirms it complete (bounded; normally long done) before overwriting it
-  const int k = static_cast<int>(h->n_gathers & 1);
-  if (h->ag_live[k]) {
-    if (int rc = comm_event_wait(h, h->ag_done[k], "reward all-gather (send block reuse)")) return rc;
-    h->ag_live[k] = false;
-  }
-  // the staging copy waits for both step streams' latest work (events only), on the
-  // staging stream: behind the steps it reads, never behind a collective
+  // the side stream waits for both step streams' latest work (events only; the step
+  // streams never wait for the side stream)
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
-  GF_HIP(hipStreamWaitEvent(h->stage_stream, h->step_ev, 0));
+  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
   if (h->stream2) {
     GF_HIP(hipEventRecord(h->step_ev2, h->stream2));
-    GF_HIP(hipStreamWaitEvent(h->stage_stream, h->step_ev2, 0));
+    GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev2, 0));
   }
-  // the steps' ring slots (two runs when they wrap) into the padded send block
-  double* gs = h->gsend[k];
+  // the steps' ring slots (two runs when they wrap) into the padded send block, behind
+  // the previous collective (which read it) on the same stream
+  double* gs = h->gsend;
   const int s0 = static_cast<int>(first % kRewardSlots);
   const int n1 = static_cast<int>(std::min<int64_t>(count, kRewardSlots - s0));
   GF_HIP(hipMemcpy2DAsync(gs, W * 8, h->reward_ring + (size_t)s0 * B, B * 8, B * 8, n1, hipMemcpyDeviceToDevice,
-                          h->stage_stream));
+                          h->comm_stream));
   if (n1 < count)
     GF_HIP(hipMemcpy2DAsync(gs + (size_t)n1 * W, W * 8, h->reward_ring, B * 8, B * 8, count - n1,
-                            hipMemcpyDeviceToDevice, h->stage_stream));
+                            hipMemcpyDeviceToDevice, h->comm_stream));
   hipEvent_t rd = nullptr;  // the copy's completion: the slots are free again
   if (!h->ev_free.empty()) {
     rd = h->ev_free.back();
@@ -1852,16 +1848,11 @@ int fe_allgather_rewards(fe_handle* h) {
     GF_HIP(hipEventCreateWithFlags(&rd, hipEventDisableTiming));
   }
   h->ring_reads.push_back({first, rd});
-  GF_HIP(hipEventRecord(rd, h->stage_stream));
-  GF_HIP(hipEventRecord(h->stage_ev, h->stage_stream));
-  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->stage_ev, 0));
+  GF_HIP(hipEventRecord(rd, h->comm_stream));
   if (int rc = comm_enqueued(h, ncclAllGather(gs, h->gather, (size_t)count * W, ncclFloat64, h->comm, h->comm_stream),
                              "ncclAllGather (rewards)"))
     return rc;
   GF_HIP(hipEventRecord(h->ag_ev, h->comm_stream));
-  GF_HIP(hipEventRecord(h->ag_done[k], h->comm_stream));
-  h->ag_live[k] = true;
-  h->n_gathers++;
   h->ag_issued = true;
   h->last_count = static_cast<int>(count);
   h->gathered_upto = h->steps_written;
@@ -1870,37 +1861,30 @@ int fe_allgather_rewards(fe_handle* h) {
 
 int fe_get_gathered_rewards(fe_handle* h, double* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
-  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->comm) return no_comm(h);
   if (!h->ag_issued) return fail(GF_ESTATE, "no all-gather issued");
   if (int rc = use_dev(h)) return rc;
   if (int rc = comm_event_wait(h, h->ag_ev, "reward all-gather")) return rc;
   const size_t n = (size_t)h->nranks * h->last_count * h->max_envs;
-  GF_HIP(hipMemcpy(dst, h->gather, n * 8, hipMemcpyDeviceToHost));
-  return GF_OK;
+  return d2h(h, dst, h->gather, n * 8);  // (on the handle's stream: no use of the null stream)
 }
 
 int fe_gathered_steps(fe_handle* h) { return h ? h->last_count : 0; }
 
 int fe_allgather_stats(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->comm) return no_comm(h);
   if (!h->has_state) return fail(GF_ESTATE, "state not set");
   // the summaries are taken on the whole current state (both step halves joined); the
   // collective then runs on the side stream, like the reward all-gather
   if (int rc = use_dev(h)) return rc;
-  // the send block is still read by the previous stats collective: the host confirms it
-  // complete (bounded) before the staging copy overwrites it
-  if (h->sg_pending)
-    if (int rc = comm_event_wait(h, h->sg_ev, "stats all-gather (send block reuse)")) return rc;
-  if (int rc = stats_summary_dev(h)) return rc;
+  if (int rc = stats_summary_dev(h)) return rc;  // (after the previous stats gather, bounded)
+  if (!h->comm) return fail(GF_ECOMM, "metrics path torn down: " + h->comm_lost);
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
-  GF_HIP(hipStreamWaitEvent(h->stage_stream, h->step_ev, 0));
-  // into the padded send block on the staging stream (behind the summary, no collective)
+  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
+  // into the padded send block, on the side stream (after the previous stats gather)
   GF_HIP(hipMemcpyAsync(h->ssend, h->stats_sum, (size_t)h->cfg.n_envs * 2 * sizeof(double), hipMemcpyDeviceToDevice,
-                        h->stage_stream));
-  GF_HIP(hipEventRecord(h->ss_copy_ev, h->stage_stream));
-  h->ss_copy_pending = true;
-  GF_HIP(hipStreamWaitEvent(h->comm_stream, h->ss_copy_ev, 0));
+                        h->comm_stream));
   if (int rc = comm_enqueued(h, ncclAllGather(h->ssend, h->stats_gather, (size_t)h->max_envs * 2, ncclFloat64,
                                               h->comm, h->comm_stream),
                              "ncclAllGather (stats)"))
@@ -1912,12 +1896,11 @@ int fe_allgather_stats(fe_handle* h) {
 
 int fe_get_gathered_stats(fe_handle* h, double* dst) {
   if (!h || !dst) return fail(GF_EINVAL, "null argument");
-  if (!h->comm) return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down)");
+  if (!h->comm) return no_comm(h);
   if (!h->sg_pending) return fail(GF_ESTATE, "no stats all-gather issued");
   if (int rc = use_dev(h)) return rc;
   if (int rc = comm_event_wait(h, h->sg_ev, "stats all-gather")) return rc;
-  GF_HIP(hipMemcpy(dst, h->stats_gather, (size_t)h->nranks * h->max_envs * 2 * sizeof(double), hipMemcpyDeviceToHost));
-  return GF_OK;
+  return d2h(h, dst, h->stats_gather, (size_t)h->nranks * h->max_envs * 2 * sizeof(double));
 }
 
 int fe_comm_destroy(fe_handle* h) {

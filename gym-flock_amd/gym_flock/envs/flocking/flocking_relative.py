@@ -107,10 +107,17 @@ class FlockingRelativeEnv(Env):
 
     def _key(self, centralized=None):
         """The device handle's parameters: the first three fix its buffers, the rest are
-        runtime parameters of its launches (fe_set_params)."""
+        runtime parameters of its launches (fe_set_params); the variant's fields (last)
+        are runtime parameters too (fe_set_variant)."""
         c = self.centralized if centralized is None else centralized
-        return (self.n_agents, self.n_neighbors, self.device, float(self.comm_radius), float(self.dt),
-                float(self.action_scalar), bool(self.mean_pooling), bool(c))
+        v = self._variant()
+        return (self.n_agents, self.n_neighbors, self.device, float(self.comm_radius), float(self._key_dt()),
+                float(self.action_scalar), bool(self.mean_pooling), bool(c),
+                None if not v else tuple(sorted(v.items())))
+
+    def _key_dt(self):
+        """The dt of the handle's launches (a variant that sets dt per step overrides it)."""
+        return self.dt
 
     def _handle(self):
         """The device handle for the current parameters. The reference reads comm_radius,
@@ -121,24 +128,26 @@ class FlockingRelativeEnv(Env):
         key = self._key()
         if self._h is not None and key != self._hkey:
             if key[:3] == self._hkey[:3]:
-                self._h.set_params(*key[3:])
+                if key[3:8] != self._hkey[3:8]:
+                    self._h.set_params(*key[3:8])
+                if key[8] != self._hkey[8]:
+                    if key[8]:
+                        self._h.set_variant(**dict(key[8]))
+                    else:
+                        self._h.clear_variant()
                 self._hkey = key
-                v = self._variant()
-                if v:
-                    self._h.set_variant(**v)
             else:
                 self._h.close()
                 self._h = None
                 self._invalidate()
                 self._ubuf = None
         if self._h is None:
-            self._h = nat.FlockHandle(self.n_agents, 1, self.comm_radius, self.dt,
+            self._h = nat.FlockHandle(self.n_agents, 1, self.comm_radius, self._key_dt(),
                                       self.action_scalar, self.mean_pooling, self.centralized,
                                       self.n_neighbors, self.device)
             self._hkey = key
-            v = self._variant()
-            if v:
-                self._h.set_variant(**v)
+            if key[8]:
+                self._h.set_variant(**dict(key[8]))
         return self._h
 
     def _variant(self):

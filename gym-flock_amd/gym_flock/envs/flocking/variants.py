@@ -63,9 +63,6 @@ class FlockingLeaderEnv(FlockingRelativeEnv):
         self.mask = np.ones((self.n_agents,))
         self.mask[0:self.n_leaders] = 0
 
-    def _key(self):
-        return super(FlockingLeaderEnv, self)._key() + (_frozen_prefix(self.mask, self.n_agents),)
-
     def _variant(self):
         return dict(u_scale=1.0, n_frozen=_frozen_prefix(self.mask, self.n_agents))
 
@@ -125,10 +122,6 @@ class FlockingObstacleEnv(FlockingRelativeEnv):
         super(FlockingObstacleEnv, self).params_from_cfg(args)
         self.mask[0:self.n_obstacles] = 0
 
-    def _key(self):
-        return super(FlockingObstacleEnv, self)._key() + (_frozen_prefix(self.mask, self.n_agents),
-                                                          self.n_obstacles)
-
     def _variant(self):
         return dict(u_scale=1.0, n_frozen=_frozen_prefix(self.mask, self.n_agents),
                     n_vel_zero=self.n_obstacles)
@@ -177,10 +170,8 @@ class FlockingStochasticEnv(FlockingRelativeEnv):
         self.max_accel = 0.5
         self.scale = 6.0
 
-    def _key(self):
-        k = list(super(FlockingStochasticEnv, self)._key())
-        k[2] = None  # dt changes every step; it goes to the device per step (fe_set_dt)
-        return tuple(k) + (self.max_accel, self.scale)
+    def _key_dt(self):
+        return self.dt_mean  # dt changes every step; it goes to the device per step (fe_set_dt)
 
     def _variant(self):
         return dict(u_scale=self.scale, u_clip=self.max_accel, x_scale=self.scale,

@@ -144,39 +144,47 @@ def test_comm_init_peer_never_joins():
 
 
 def test_steps_never_wait_behind_a_stuck_collective():
-    """A collective that never completes (a gate kernel holds the side stream, as a peer
-    that stopped responding would) must not hold the step streams: the ring slots a step
-    overwrites are released by the staging copies, which wait only for the steps. 86
-    steps (past the 64-slot ring) and their reward reads finish while the gate is shut;
-    the gather queued behind it then delivers its steps once the gate opens, and the
-    stats gather the same."""
+    """A collective that does not complete (a gate kernel holds the collectives' side
+    stream, as a peer that stopped responding would) does not hold the step streams: they
+    never wait on the side stream on the device. 56 steps (and their reward reads) after
+    a gather queued behind the gate finish while it is shut. The step that reuses that
+    gather's first ring slot (64 steps on) waits for its staging copy on the host, bounded
+    by the collective timeout, and goes on as soon as the gate opens (2 s later here); the
+    gather then delivers exactly its steps."""
+    import threading
     B, N = 3, 32
     v = VecFlockingRelative(B, N)
     v.reset(seed=5)
     g = RcclRewardGather(v.h, 1, 0, v.h.comm_unique_id(), timeout=60.0)
     u = np.random.RandomState(5).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
-    for _ in range(8):
+    for _ in range(8):  # steps 0-7
         v.step(u)
     g.issue()
     g.result()
-    v.h.debug_comm_gate(True, max_seconds=40.0)
+    v.h.debug_comm_gate(True, max_seconds=30.0)
+    opener = None
     try:
-        t0 = time.monotonic()
         hist = []
-        for _ in range(8):
+        for _ in range(8):  # steps 8-15
             v.step(u)
             hist.append(v.rewards())
-        g.issue()  # queued behind the gate
-        for _ in range(8):
-            v.step(u)
-            hist.append(v.rewards())
-        g.issue()  # its send block's previous collective (before the gate) is complete
-        for _ in range(70):  # past the ring: each slot's staging copy has run
+        g.issue()  # its staging copy and collective queue behind the gate
+        t0 = time.monotonic()
+        for _ in range(56):  # steps 16-71: no ring slot of the pending gather is reused
             v.step(u)
             v.rewards()
-        held = time.monotonic() - t0
+        free_run = time.monotonic() - t0
+        opener = threading.Timer(2.0, lambda: v.h.debug_comm_gate(False))
+        opener.start()
+        t1 = time.monotonic()
+        v.step(u)  # step 72 reuses step 8's slot: waits (host, bounded) for the staging copy
+        v.rewards()
+        waited = time.monotonic() - t1
     finally:
+        if opener is not None:
+            opener.join()
         v.h.debug_comm_gate(False)
-    assert held < 20.0, "steps waited %.1f s behind the gated collective" % held
-    np.testing.assert_array_equal(g.result(), np.array(hist[8:16]))
+    assert free_run < 5.0, "steps waited %.1f s behind the gated collective" % free_run
+    assert 1.0 < waited < 15.0, waited
+    np.testing.assert_array_equal(g.result(), np.array(hist))
     v.close()
