@@ -467,7 +467,9 @@ def bench_dropin_coverage(args):
     reference's controller) plus its time matrix per map."""
     from gym_flock.envs.spatial import CoverageEnv
     out = {}
-    for R, M, nearby, episodes in ((6, 500, True, 6), (200, 1000, False, 3)):
+    # max_nodes 1000 for both: the map generator's target count varies from reset to reset
+    # (~390-560 here), and the module default of 500 padded nodes rejects the larger maps
+    for R, M, nearby, episodes in ((6, 1000, True, 6), (200, 1000, False, 3)):
         row = {}
         for mode in ("getters", "direct"):
             for pol in ("random", "greedy"):
@@ -529,7 +531,8 @@ def bench_dropin_coverage(args):
         out["r%d" % R] = row
     out["note"] = ("per call of env.step(env.controller(...)) on one CoverageEnv, whole episodes after one warm-up "
                    "episode, resets untimed; the map is regenerated at every reset as in the reference, so a greedy "
-                   "episode's first step builds its time matrix (first_step_ms)")
+                   "episode's first step builds its time matrix (first_step_ms); max_nodes 1000 (the generated maps "
+                   "hold up to ~560 targets)")
     return out
 
 

@@ -20,17 +20,7 @@ constexpr int kTileDefault = 512;   // default tile (measured best, see step_til
 constexpr size_t kStepLdsPlainFloor = 24 * 1024;  // plain step: 6 workgroups per CU, not 7
 constexpr int kKnnLdsMax = 4096;    // kNN stages the env's positions in LDS up to this N
 constexpr int kKnnGridCells = 2048; // kNN: cells of the per-env uniform grid (at most)
-#ifndef GF_KNN_RIM_U
-#define GF_KNN_RIM_U 4
-#endif
-constexpr int kInlineRimU = GF_KNN_RIM_U;  // fused kNN inline rim scan: columns in flight per lane
-// Flocking-v0 step register demand (A/B switch): 1 = the velocity sums of the env kept per
-// wave in LDS (not per thread through every pass), the neighbour velocity sums taken as
-// sum_j v_j (the row's deg * v_i subtracted at the end) and the row's state read from LDS
-// per pair, so that fewer values stay live through the feature pass
-#ifndef GF_KNN_LEAN
-#define GF_KNN_LEAN 0
-#endif
+constexpr int kInlineRimU = 4;      // fused kNN inline rim scan: columns in flight per lane
 constexpr int kStoreTab = 16;      // network rows: float4 table entries per wave (one per nibble)
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
 constexpr int kStepExactKnnMax = 128;  // fused kNN: envs up to this size are ranked exactly in

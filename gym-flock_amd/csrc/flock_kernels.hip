@@ -684,13 +684,11 @@ __device__ __forceinline__ void store_network_rows(const StepArgs& a, const uint
 // row combined, state_values (:124-129), the updated state, the controller (:194-226)
 // and, by the env's first block, the reward (instant_cost :145-147). `writer` = the
 // thread holding slice 0 of a valid row.
-// LEANV (the lean Flocking-v0 step, GF_KNN_LEAN): svx / svy arrive as the env's whole sums
-// and f0 / f3 as the row's sums of its neighbours' velocities; deg_row is its degree.
-template <bool DYN, bool UF64, bool CTRL, bool VAR, bool LEANV = false>
+template <bool DYN, bool UF64, bool CTRL, bool VAR>
 __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile, double* red, const St& me,
                                               double f0, double f1, double f2, double f3, double f4,
                                               double f5, double gx, double gy, double svx, double svy, int b,
-                                              int i0, int i_row, bool writer, int S, int tid, int deg_row = 0) {
+                                              int i0, int i_row, bool writer, int S, int tid) {
   const int N = a.N, T = a.T;
   const size_t env0 = (size_t)b * N;
   // combine the S slices of each row (butterfly: identical bits in every lane)
@@ -709,15 +707,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
   });
 
   // every thread summed its share of the env's velocities while staging the tiles
-  double Svx = svx, Svy = svy;
-  if constexpr (!LEANV) {
-    Svx = block_sum(svx, red);
-    Svy = block_sum(svy, red);
-  } else {
-    // sum_j (v_i - v_j) over the row's neighbours = deg v_i - sum_j v_j
-    f0 = static_cast<double>(deg_row) * me.vx - f0;
-    f3 = static_cast<double>(deg_row) * me.vy - f3;
-  }
+  const double Svx = block_sum(svx, red), Svy = block_sum(svy, red);
 
   if (writer && !GF_ABLATE(a, 256)) {  // diag 256: skip the per-row outputs (timing only)
     const size_t g = env0 + i_row;
@@ -799,10 +789,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 // no spills; its LDS is floored to hold it at 6 workgroups per CU, see
 // kStepLdsPlainFloor), 6 with the controller (79 VGPRs, 23.2 KiB of LDS: 6 per CU);
 // variants are not capped (their extra state would spill).
-#ifndef GF_KNN_WAVES
-#define GF_KNN_WAVES 5
-#endif
-constexpr int kWavesPlain = 6, kWavesPf = 4, kWavesCtrl = 6, kWavesKnn = GF_KNN_WAVES, kWavesKnnCtrl = 4;
+constexpr int kWavesPlain = 6, kWavesPf = 4, kWavesCtrl = 6, kWavesKnn = 5, kWavesKnnCtrl = 4;
 // Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
 // wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
 // its HW_ID / XCC_ID, for scripts/phase_timeline.py. Product builds compile it out.
@@ -881,11 +868,6 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   // and the block's predicted rows in order (prow[p]: the p-th predicted row)
   [[maybe_unused]] float* ptc = rthr + R + wid_of(threadIdx.x) * R;
   [[maybe_unused]] int* prow = reinterpret_cast<int*>(rthr + 5 * R);
-  // the lean Flocking-v0 step (GF_KNN_LEAN): the env's velocity sums per wave (x, y of
-  // wave w at 2w, 2w + 1) and every row's degree
-  constexpr bool kLean = GF_KNN_LEAN && kSupK;
-  [[maybe_unused]] double* wsv = reinterpret_cast<double*>(prow + R);
-  [[maybe_unused]] int* rdeg = reinterpret_cast<int*>(wsv + 8);
 
   const int nrows = min(R, N - i0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -935,9 +917,6 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   const bool frow = fr < nrows;
   double f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, gx = 0, gy = 0;
   double svx = 0, svy = 0;  // partial sums of the env's velocities (controller, reward)
-  if constexpr (kLean) {
-    if (tid < 8) wsv[tid] = 0.0;  // published by the first tile's barriers
-  }
   float rx32 = 0.f, ry32 = 0.f, Pr = 0.f;  // lane r: row r's float32 position; rows' max |coord|
   // kNN rows predicted to lack k neighbours (their k-th nearest two states back was
   // at >= 0.8 comm_radius): predm (wave-uniform) marks them, rthr[r] holds row r's
@@ -968,20 +947,9 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   // one neighbour pair (row fr = me, tile column c): features and controller gradient.
   // The row's state is read from LDS per feature pass, so it holds no registers
   // through pass 1.
-  auto pair_terms = [&](const auto& me, int j0, int c, bool isadj, bool isnear, double ksc) {
-    // (kLean: the neighbour's velocity is read only for an adjacent pair, below)
-    [[maybe_unused]] St o;
-    double opx, opy;
-    if constexpr (kLean) {
-      const double2 op = *reinterpret_cast<const double2*>(&tile[c]);
-      opx = op.x;
-      opy = op.y;
-    } else {
-      o = tile[c];
-      opx = o.px;
-      opy = o.py;
-    }
-    const double dx = me.px - opx, dy = me.py - opy;
+  auto pair_terms = [&](const St& me, int j0, int c, bool isadj, bool isnear, double ksc) {
+    const St o = tile[c];
+    const double dx = me.px - o.px, dy = me.py - o.py;
     const double r2 = dx * dx + dy * dy;
     if constexpr (kOuter) {  // a pass-1 candidate: both decisions exactly (:117, :225)
       isadj = r2 < a.cr2;
@@ -1011,16 +979,10 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
     if (isadj) {
       // obstacle variant: no velocity difference for pairs touching agents < nvz
       const bool vz = VAR && (i_row < a.n_vel_zero || j0 + c < a.n_vel_zero);
-      if constexpr (kLean) {  // sum_j v_j (the epilogue takes deg v_i - it)
-        const volatile St* ov = &tile[c];
-        f0 += ov->vx;
-        f3 += ov->vy;
-      } else {
-        f0 += vz ? 0.0 : me.vx - o.vx;
-        f3 += vz ? 0.0 : me.vy - o.vy;
-      }
+      f0 += vz ? 0.0 : me.vx - o.vx;
       f1 += q1x;
       f2 += q2x;
+      f3 += vz ? 0.0 : me.vy - o.vy;
       f4 += q1y;
       f5 += q2y;
     }
@@ -1038,13 +1000,7 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   // cursor bookkeeping cost more than it saved: 266 vs 215 us, DESIGN.md.)
   auto feature_pass = [&](int j0, int nch) {
     if (!frow || GF_ABLATE(a, 2)) return;
-    // kLean: the row's position re-read from LDS per pair (no registers held for it)
-    const St me_r = rows[fr];
-    const volatile St& me_v = rows[fr];
-    const auto& me = [&]() -> const auto& {
-      if constexpr (kLean) return me_v;
-      else return me_r;
-    }();
+    const St me = rows[fr];
     // kNN: this row's candidate words (predicted rows) and key scale 2^qbits / Tr
     [[maybe_unused]] const uint64_t* crow = nullptr;
     [[maybe_unused]] double ksc = 0.0;
@@ -1100,19 +1056,13 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
     [[maybe_unused]] const int ti = j0 / T;
     if (ti == 0) GF_STAMP(1);
     float pt = 0.f;
-    [[maybe_unused]] double tsx = 0, tsy = 0;  // kLean: this tile's share of the velocity sums
     auto stage = [&](int t, const St& s) {
       tile[t] = s;
       if (one_tile && static_cast<unsigned>(t - i0) < static_cast<unsigned>(nrows)) rows[t - i0] = s;
       const float fx = static_cast<float>(s.px), fy = static_cast<float>(s.py);
       pt = fmaxf(pt, fmaxf(fabsf(fx), fabsf(fy)));
-      if constexpr (kLean) {
-        tsx += s.vx;
-        tsy += s.vy;
-      } else {
-        svx += s.vx;
-        svy += s.vy;
-      }
+      svx += s.vx;
+      svy += s.vy;
     };
     if constexpr (PF >= 1) {
 #pragma unroll
@@ -1146,14 +1096,6 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
             if (lane == p) rp = __builtin_ctzll(pm);
           if (lane < nrows) prow[lane] = rp;
         }
-      }
-    }
-    if constexpr (kLean) {  // the wave's share into its LDS slots (in tile order: fixed bits)
-      tsx = wave_sum(tsx);
-      tsy = wave_sum(tsy);
-      if (lane == 0) {
-        wsv[2 * wid] += tsx;
-        wsv[2 * wid + 1] += tsy;
       }
     }
     const float Pt = block_max(pt, redf);  // also the barrier that publishes the tile
@@ -1431,7 +1373,6 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
     with_slices(S, [&](auto Sc) { deg = group_sum_c<decltype(Sc)::value>(deg); });
     if (frow && fs == 0) {
       inv[fr] = a.mean_pooling ? static_cast<float>(1.0 / static_cast<double>(deg == 0 ? 1 : deg)) : 1.0f;
-      if constexpr (kLean) rdeg[fr] = deg;
       if (a.degree_out) a.degree_out[env0 + i0 + fr] = deg;
     }
   }
@@ -1519,12 +1460,8 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   }
 
   const St me = frow ? rows[fr] : St{0, 0, 0, 0};
-  if constexpr (kLean) {  // the env's velocity sums from the waves' slots, a fixed tree
-    svx = (wsv[0] + wsv[2]) + (wsv[4] + wsv[6]);
-    svy = (wsv[1] + wsv[3]) + (wsv[5] + wsv[7]);
-  }
-  step_epilogue<DYN, UF64, CTRL, VAR, kLean>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0,
-                                             i_row, frow && fs == 0, S, tid, (kLean && frow) ? rdeg[fr] : 0);
+  step_epilogue<DYN, UF64, CTRL, VAR>(a, tile, red, me, f0, f1, f2, f3, f4, f5, gx, gy, svx, svy, b, i0, i_row,
+                                      frow && fs == 0, S, tid);
   if constexpr (KN > 0) {
     // Flocking-v0 observation x_i - x_j of this lane's neighbour(s) (flocking.py:24)
     auto knn_out = [&](const St& o, int m) {
@@ -1999,7 +1936,6 @@ size_t step_lds_bytes(int N, int R, int T, bool ctrl, bool knn) {
   s += (size_t)R * Wn * 8 + ((ctrl && knn) ? (size_t)R * Wt * 8 : 0) + (knn ? (size_t)R * Wt * 8 : 0);
   // inv (R floats); kNN: rthr (R), the waves' candidate-bound tables (4R), prow (R ints)
   s += 8 * sizeof(double) + (((size_t)R * 4 * (knn ? 7 : 1) + 15) / 16) * 16;
-  if (knn) s += 8 * sizeof(double) + (size_t)R * 4;  // the lean kNN step's velocity sums, degrees
   s += 4 * kStoreTab * 16 + (((size_t)R * 8 + 31) & ~size_t(31));  // row table, rows' float32 positions
   return s;
 }
