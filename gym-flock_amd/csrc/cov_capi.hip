@@ -659,7 +659,9 @@ int cov_set_robot_positions(cov_handle* h, int env, const double* xr) {
 int cov_get_obs(cov_handle* h, int env, float* nodes, float* edges, int32_t* senders, int32_t* receivers,
                 int64_t* step) {
   if (!h || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
-  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  // before the first reset the arrays hold the graph's static part (the motion edges the
+  // env's nearby-starts draw walks, coverage.py:655-673); the robots' part follows reset
+  if (!h->has_state && !h->has_graph) return cfail(GF_ESTATE, "set the targets (cov_set_targets) or reset first");
   if (int rc = use(h)) return rc;
   const size_t M = h->cfg.max_nodes, E = 4 * M;
   const gf::CovArgs& a = h->a;

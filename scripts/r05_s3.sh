@@ -3,6 +3,8 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/r05_s3; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_coverage_gpu.py tests/test_coverage_greedy_gpu.py -m gpu -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_cov.log 2>&1; r0=$?; echo "coverage tests rc=$r0"; tail -3 $O/pytest_cov.log
+[ $r0 -gt 1 ] && exit $r0
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 --cpu-seconds 6 > $O/bench20.json 2> $O/bench20.err; rc=$?; echo "bench rc=$rc"; tail -3 $O/bench20.err
 python - $O/bench20.json <<'PY'
 import json, sys

@@ -313,3 +313,48 @@ def test_full_config4_batch_properties_and_sampled_parity():
         live = s >= 0
         assert (s[live] < R + T).all() and (rcv[live] < R + T).all()
     v.close()
+
+
+def test_default_env_nearby_starts():
+    """CoverageEnv() with the module defaults (NEARBY_STARTS, 500 padded nodes) builds its
+    start region from the motion graph before any reset (get_n_nearest, coverage.py:655-673,
+    reading the graph's static observation) and resets inside it: the region equals the
+    oracle's breadth-first growth from the drawn node over the reference's motion edges
+    (utils.py:8-24), and the robots start on distinct targets of it. One direct step and
+    its observation against the CPU reference op sequence."""
+    from gym_flock.envs.spatial import CoverageEnv
+    from oracle.cpu_ref_coverage import CpuCoverage
+    seen = []
+    orig = CoverageEnv.get_n_nearest
+
+    def spy(self, i, n):
+        seen.append(int(i))
+        return orig(self, i, n)
+
+    CoverageEnv.get_n_nearest = spy
+    try:
+        np.random.seed(3)  # a map of 431 targets (coverage_r6_random's)
+        env = CoverageEnv()
+        env.seed(11)
+        np.random.seed(3)
+        obs = env.reset()
+    finally:
+        CoverageEnv.get_n_nearest = orig
+    R, T = env.n_robots, env.n_targets
+    cpu = CpuCoverage(env.targets, R, env.max_nodes)
+    s, q = cpu.motion_edges[0] - R, cpu.motion_edges[1] - R
+    want = {seen[-1]}
+    while len(want) < 5 * R:
+        want |= set(q[np.isin(s, list(want))].tolist())
+    np.testing.assert_array_equal(np.nonzero(env.start_region)[0], sorted(want))
+    starts = env.closest_targets - R
+    assert len(set(starts.tolist())) == R and all(env.start_region[t] for t in starts)
+    vis = env.visited[R:, 0]
+    cpu.reset(starts, np.nonzero(vis[:T] == 0)[0] + R)
+    a = np.random.RandomState(2).randint(0, 4, size=(R, 1))
+    obs, r, d, _ = env.step(a)
+    ref, rr, dd, _ = cpu.step(a)
+    for k in ("nodes", "edges", "senders", "receivers"):
+        np.testing.assert_array_equal(obs[k].reshape(ref[k].shape), ref[k], err_msg=k)
+    assert r == rr and d == dd
+    env.close()
