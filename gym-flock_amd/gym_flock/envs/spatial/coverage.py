@@ -273,8 +273,9 @@ class CoverageEnv(Env):
         else:
             a, rnd = self._h.controller_greedy()
             a, rnd = a[0].copy(), rnd[0]
-        for i in np.nonzero(rnd)[0]:
-            a[i] = self.np_random.choice(self.n_actions)
+        k = np.nonzero(rnd)[0]
+        if len(k):  # one draw per robot in robot order: a batched draw is the same stream
+            a[k] = self.np_random.choice(self.n_actions, size=len(k))
         return a.reshape(self.n_robots, 1).astype(np.int32)
 
     def construct_time_matrix(self, edge_time=1.0):
