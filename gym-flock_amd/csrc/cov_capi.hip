@@ -439,6 +439,8 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     a.glist = h->tm_glist;
     a.glen = h->tm_glen;
     a.gstride = h->gstride;
+    a.gcost = h->tm_cost;
+    a.gprev = h->tm_prevT;
     a.gactions = h->actions;
     a.needs_random = h->needs_random;
   } else if (flags & COV_ACTIONS_DEVICE) {
@@ -544,6 +546,8 @@ int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* ed
     a.glist = h->tm_glist;
     a.glen = h->tm_glen;
     a.gstride = h->gstride;
+    a.gcost = h->tm_cost;
+    a.gprev = h->tm_prevT;
     a.gactions = h->actions;  // the next expert actions stay resident as well
     a.needs_random = h->needs_random;
   }

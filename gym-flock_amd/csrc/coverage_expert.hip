@@ -548,6 +548,14 @@ __global__ __launch_bounds__(256) void cov_greedy_list_step_kernel(CovGreedyArgs
     if (vis[t]) atomicOr(&vbits[t >> 5], 1u << (t & 31));
   __syncthreads();
   const bool any_vis = a.nvisited[b] > 0;
+  // few targets left unvisited: the short candidate list instead of deep list scans
+  int* ulist = reinterpret_cast<int*>(vbits + (Tm + 31) / 32);
+  int* ucount = ulist + kGreedyDirectMax;
+  const bool gdirect = T - a.nvisited[b] <= kGreedyDirectMax;
+  if (gdirect) {
+    greedy_direct_list(vbits, T, any_vis, ulist, ucount);
+    __syncthreads();
+  }
   const bool dirty = a.dirty[b] != 0;
   for (int i = threadIdx.x; i < R; i += 256) {
     int c;
@@ -568,7 +576,9 @@ __global__ __launch_bounds__(256) void cov_greedy_list_step_kernel(CovGreedyArgs
       c = a.cur[(size_t)b * R + i] - R;
     }
     const size_t row = (size_t)b * Tm + c;
-    const int g = greedy_from_list(a.glist + row * a.gstride, a.glen + row, vbits, any_vis, a.nvisited[b] >= T);
+    const int g = gdirect ? greedy_direct(a.cost + row * Tm, a.prevT + row * Tm, a.nbr + row * 4, a.cnt[row], ulist,
+                                          *ucount)
+                          : greedy_from_list(a.glist + row * a.gstride, a.glen + row, vbits, any_vis, a.nvisited[b] >= T);
     const uint32_t flag = (uint32_t)g >> 2;
     if (flag & kGreedyErr) atomicOr(a.err, 8);
     a.actions[(size_t)b * R + i] = (flag & kGreedyRnd) ? 0 : (g & 3);
@@ -585,7 +595,8 @@ hipError_t launch_cov_greedy_lists(const CovTmArgs& a, int n_envs_sel, hipStream
 
 hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s) {
   if (a.glist) {
-    hipLaunchKernelGGL(cov_greedy_list_step_kernel, dim3(a.B), dim3(256), ((a.Tmax + 31) / 32) * 4, s, a);
+    hipLaunchKernelGGL(cov_greedy_list_step_kernel, dim3(a.B), dim3(256),
+                       ((a.Tmax + 31) / 32) * 4 + (kGreedyDirectMax + 1) * 4, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(cov_greedy_kernel, dim3(a.B, (a.R + kGreedyRobotsPerBlock - 1) / kGreedyRobotsPerBlock),

@@ -40,6 +40,8 @@ struct CovArgs {
   const uint16_t* glist;  // (B,Tmax,gstride) or nullptr: actions come from `actions`
   const uint16_t* glen;   // (B,Tmax)
   int gstride;
+  const uint16_t* gcost;  // (B,Tmax,Tmax) hop counts [source][target] (greedy_direct)
+  const int16_t* gprev;   // (B,Tmax,Tmax) graph_previous[t, c] at [c][t] (greedy_direct)
   int32_t* gactions;      // (B,R) the greedy actions taken (written)
   uint8_t* needs_random;  // (B,R) robots the reference hands to np_random.choice (action 0 here)
   // cov_step_host: after the step, controller(greedy=True)'s actions of the RESULTING state
@@ -114,6 +116,58 @@ __device__ __forceinline__ int greedy_from_list(const uint16_t* row, const uint1
     }
   }
   return static_cast<int>(kGreedyRnd << 2);
+}
+
+// When few targets are left unvisited the list scan runs deep: late in an episode every
+// target near a robot is visited and its list's first unvisited entry lies hundreds of
+// entries in (a dependent load per 32 entries; 50-80 us steps at config 4). With at most
+// kGreedyDirectMax unvisited targets (excluding target 0 once anything is visited, the
+// reference's mask) the kernels take the minimum (hop count, target) over that short list
+// directly from the robot's cost row instead: the same target, as the list is in that
+// order. ulist: the env's unvisited candidates in ascending target order (LDS).
+constexpr int kGreedyDirectMax = 32;
+constexpr uint32_t kCostInf = 0xFFFF;   // uint16 cost matrix: unreachable
+constexpr uint32_t kCostMax = 1000;     // MAX_COST (coverage.py:68)
+__device__ __forceinline__ int greedy_direct(const uint16_t* crow, const int16_t* prow, const int32_t* nbr4,
+                                             int n, const int* ulist, int U) {
+  uint32_t key = 0xFFFFFFFFu;
+  for (int k0 = 0; k0 < U; k0 += 8) {  // eight loads of the row in flight
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = k0 + k < U ? crow[ulist[k0 + k]] : kCostInf;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (v[k] != kCostInf && v[k] < kCostMax) key = min(key, v[k] << 10 | static_cast<uint32_t>(ulist[k0 + k]));
+  }
+  if (key == 0xFFFFFFFFu) return static_cast<int>(kGreedyRnd << 2);  // every candidate out of reach
+  const int t = static_cast<int>(key & 1023u);
+  const int p = prow[t];
+  if (p < 0) return static_cast<int>(kGreedyRnd << 2);  // :863
+  const int4 nb = *reinterpret_cast<const int4*>(nbr4);
+  int act = (n > 3 && nb.w == p) ? 3 : 4;  // the first of the node's action targets equal to the next hop
+  act = (n > 2 && nb.z == p) ? 2 : act;
+  act = (n > 1 && nb.y == p) ? 1 : act;
+  act = (n > 0 && nb.x == p) ? 0 : act;
+  if (act == 4) return static_cast<int>(kGreedyErr << 2);
+  return act;
+}
+// The candidates of greedy_direct from the visited bits (one wave: lane-ordered ballots
+// keep ascending target order); returns their count (<= kGreedyDirectMax is the caller's
+// condition: T - visited <= kGreedyDirectMax). Every wave calls it; wave 0 writes.
+__device__ __forceinline__ void greedy_direct_list(const uint32_t* vbits, int T, bool any_vis, int* ulist, int* ucount) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  int cnt = 0;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    const bool cand = t < T && !((vbits[t >> 5] >> (t & 31)) & 1u) && !(t == 0 && any_vis);
+    const uint64_t m = __ballot(cand);
+    const int pos = cnt + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0));
+    if (cand && pos < kGreedyDirectMax) ulist[pos] = t;
+    cnt += __popcll(m);
+  }
+  if (lane == 0) *ucount = cnt;
 }
 
 // Greedy expert (coverage_expert.hip).

@@ -192,6 +192,8 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
   int* counter = reinterpret_cast<int*>(seen + (M + 31) / 32);
   int* first = counter + 4;                                    // M: first claimer of each node
   uint32_t* gvis = reinterpret_cast<uint32_t*>(first + M);     // greedy: visited bits, 64 per 2 words
+  int* ulist = reinterpret_cast<int*>(gvis + ((a.Tmax + 63) / 64) * 2);  // greedy_direct candidates
+  int* ucount = ulist + kGreedyDirectMax;
   const int W = (M + 31) / 32;
   const int tid = threadIdx.x;
   const double* tg = a.tgt + (size_t)b * Tm * 2;
@@ -281,6 +283,12 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     }
     __syncthreads();
   }
+  // few targets left unvisited: the greedy actions from the short candidate list
+  const bool gdirect = greedy && T - nv0 <= kGreedyDirectMax;
+  if (gdirect) {
+    greedy_direct_list(gvis, T, any_vis, ulist, ucount);
+    __syncthreads();
+  }
   // robot i: its node c and the node n its action points at (claiming c if n == c)
   auto pick = [&](int i, const Ld& l, int& c) {
     c = l.c;
@@ -304,7 +312,9 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     int n = c;
     if (greedy) {  // :814-869 from the node's greedy list; fallbacks take action 0 here
       const size_t row = (size_t)b * Tm + (c - R);
-      const int g = greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, any_vis, nv0 >= T);
+      const int g = gdirect ? greedy_direct(a.gcost + row * Tm, a.gprev + row * Tm, nbr + 4 * (c - R), cnt[c - R],
+                                            ulist, *ucount)
+                            : greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, any_vis, nv0 >= T);
       const uint32_t flag = static_cast<uint32_t>(g) >> 2;
       if (flag & kGreedyErr) atomicOr(a.err, 8);
       ai = (flag & kGreedyRnd) ? 0 : (g & 3);
@@ -538,10 +548,17 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
       if ((seen[n >> 5] >> (n & 31)) & 1u) atomicOr(&gvis[t >> 5], 1u << (t & 31));
     }
     __syncthreads();
+    const bool ndirect = T - nv <= kGreedyDirectMax;
+    if (ndirect) {
+      greedy_direct_list(gvis, T, nv > 0, ulist, ucount);
+      __syncthreads();
+    }
     for (int i = tid; i < R; i += NT) {
       const int c = new_s[i];
       const size_t row = (size_t)b * Tm + (c - R);
-      const int g = greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, nv > 0, nv >= T);
+      const int g = ndirect ? greedy_direct(a.gcost + row * Tm, a.gprev + row * Tm, nbr + 4 * (c - R), cnt[c - R],
+                                            ulist, *ucount)
+                            : greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, nv > 0, nv >= T);
       const uint32_t flag = static_cast<uint32_t>(g) >> 2;
       if (flag & kGreedyErr) atomicOr(a.err, 8);
       const int ai = (flag & kGreedyRnd) ? 0 : (g & 3);
@@ -704,7 +721,8 @@ hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all
 }
 
 size_t cov_step_lds_bytes(int R, int M) {
-  return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16 + (size_t)M * 4 + (size_t)((M - R + 63) / 64) * 8;
+  return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16 + (size_t)M * 4 + (size_t)((M - R + 63) / 64) * 8 +
+         (size_t)(kGreedyDirectMax + 1) * 4;
 }
 
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {

@@ -388,3 +388,51 @@ def test_cov_step_host_batched_matches_step_and_getters():
             np.testing.assert_array_equal(o["closest"][b], hs[1].robots(b)[1])
     for h in hs:
         h.close()
+
+
+def test_greedy_list_and_direct_paths_vs_oracle():
+    """60 unvisited targets on the r20 map, 40 greedy steps: the greedy actions come from
+    the list scan while more than 32 targets are unvisited and from the direct minimum over
+    the short candidate list after that (until none is left). Through the three device
+    forms at once: the fused greedy step (COV_ACTIONS_GREEDY), cov_step_host's next-state
+    actions (COV_NEXT_GREEDY) and the standalone controller (cov_controller_greedy), each
+    against the oracle's greedy expert, robots' nodes checked every step."""
+    f = np.load(GREEDY[-1])
+    hs = [_handle_for(f)[0] for _ in range(2)]
+    R, T, M = int(f["n_robots"]), int(f["n_targets"]), int(f["max_nodes"])
+    o = oc.CoverageOracle(f["targets"], R, M)
+    cost, prev = oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R)
+    rs = np.random.RandomState(8)
+    start = rs.choice(T, R, replace=False)
+    left = rs.choice(np.setdiff1d(np.arange(T), start), size=60, replace=False)
+    vis = np.ones((1, M - R), np.uint8)
+    vis[0, left] = 0
+    for h in hs:
+        h.reset(start[None], vis)
+    o.reset(start, left + R)
+    pool = nat.host_pool()
+    outs = {k: pool.array(shape, dt) for k, shape, dt in (("nxt", (1, R), np.int32), ("nrd", (1, R), np.uint8))}
+    n_left = []
+    for t in range(40):
+        cur = o.closest()
+        ea, er = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+        ea[er] = 0
+        n_left.append(int((o.visited[R:] == 0).sum()))
+        ga, gr = hs[1].controller_greedy()  # standalone kernel on the second handle's state
+        np.testing.assert_array_equal(ga[0], ea)
+        np.testing.assert_array_equal(gr[0], er)
+        if t > 0:  # the previous cov_step_host computed this state's actions already
+            np.testing.assert_array_equal(outs["nxt"][0], ea)
+            np.testing.assert_array_equal(outs["nrd"][0].astype(bool), er)
+        hs[0].step(greedy=True)
+        a0, r0 = hs[0].actions()
+        np.testing.assert_array_equal(a0[0], ea)
+        np.testing.assert_array_equal(r0[0], er)
+        hs[1].step_host(ea[None].astype(np.int32), None, None, None, None, None, None, None, None,
+                        outs["nxt"].ctypes.data, outs["nrd"].ctypes.data)
+        o.step(ea)
+        for h in hs:
+            np.testing.assert_array_equal(h.robots(0)[1], o.closest())
+    assert max(n_left) > 32 and min(n_left) <= 32, n_left  # both paths taken
+    for h in hs:
+        h.close()
