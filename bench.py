@@ -572,15 +572,40 @@ def bench_greedy(v, targets, R, M, B, K, args):
         v.sync()
         ep_t += loop(lambda: v.step(greedy=True), 75)
         ep_k += 75
+    # the reference's own semantics in episodes: the fallback robots' actions drawn on the
+    # host (np_random.choice(4) per robot in robot order, coverage.py:863-864), so every
+    # step is the greedy kernel, a device-to-host copy of the actions and flags, the draws,
+    # the upload and the step
+    rng = np.random.RandomState(17)
+    fa_t, fa_k = 0.0, 0
+    for e in range(4):
+        v.reset(seed=100 + e)
+        v.sync()
+        t0 = time.perf_counter()
+        for _ in range(75):
+            a, rnd = v.h.controller_greedy()
+            k = np.nonzero(rnd.ravel())[0]
+            if len(k):
+                a.ravel()[k] = rng.choice(4, size=len(k))
+            v.step(a)
+        v.sync()
+        fa_t += time.perf_counter() - t0
+        fa_k += 75
     del state
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
-           "expert_step_ms": 1e3 * el / K, "expert_robot_steps_per_s": R * B * K / el,
-           "expert_step_ms_two_launches": 1e3 * el_sep / K,
            "expert_step_ms_in_episodes": 1e3 * ep_t / ep_k,
-           "note": "expert step = controller(greedy=True) + step for every env; fused: the greedy actions "
-                   "come from per-node greedy lists inside the step's own launch (COV_ACTIONS_GREEDY); "
-                   "two_launches: cov_greedy kernel then the resident step; fallback robots take action 0 "
-                   "(no host round trip)"}
+           "expert_robot_steps_per_s_in_episodes": R * B * ep_k / ep_t,
+           "expert_step_ms_in_episodes_host_fallback_draws": 1e3 * fa_t / fa_k,
+           "expert_step_ms_steady_all_visited": 1e3 * el / K,
+           "expert_step_ms_two_launches_steady": 1e3 * el_sep / K,
+           "note": "expert step = controller(greedy=True) + step for every env. in_episodes (the headline): reset "
+                   "every 75 steps (EPISODE_LENGTH), resets untimed; fused: the greedy actions come from per-node "
+                   "greedy lists (or, with at most 32 targets unvisited, the direct minimum over them) inside the "
+                   "step's own launch (COV_ACTIONS_GREEDY), fallback robots take action 0 (no host round trip); "
+                   "host_fallback_draws: the reference's semantics, the greedy kernel, the actions and flags to "
+                   "the host, np_random draws for the fallback robots, the upload and the step; "
+                   "steady_all_visited: thousands of steps from one reset, every target visited (every robot "
+                   "on its fallback)"}
     if not args.no_cpu_baseline:
         from oracle import coverage as oc
         o = oc.CoverageOracle(targets, R, M)
