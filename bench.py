@@ -538,8 +538,9 @@ def bench_dropin_coverage(args):
 
 def bench_greedy(v, targets, R, M, B, K, args):
     """§8f: the greedy expert (controller(greedy=True)) on the same batch: the per-graph
-    time-matrix build for all B envs, then K expert steps (device controller + step,
-    actions resident; fallback robots keep action 0, no host round trip)."""
+    time-matrix build for all B envs, then expert steps (greedy actions and the step in one
+    launch per half batch; fallback robots draw np_random.choice(4) from their env's stream
+    on the device, as the reference does, or take action 0 in the "fallback_action0" form)."""
     v.set_targets(targets)  # invalidates every env's time matrix
     v.sync()
     t0 = time.perf_counter()
@@ -563,15 +564,21 @@ def bench_greedy(v, targets, R, M, B, K, args):
     loop(lambda: v.step(greedy=True), 20)
     el = loop(lambda: v.step(greedy=True), K)
     el_sep = loop(separate, K)
+    el0 = loop(lambda: v.step(greedy=True, fallback="zero"), K)
     # in episodes: reset every 75 steps (the reference's EPISODE_LENGTH), resets untimed,
     # so most steps see unvisited targets nearby (the long run above is mostly the
-    # all-visited tail, where every robot falls back)
-    ep_t, ep_k = 0.0, 0
+    # all-visited tail, where every robot falls back); each reset seeds every env's
+    # np_random (seed + b, after reset's draws) and the fallback draws continue it
+    ep_t, ep_k, z_t = 0.0, 0, 0.0
     for e in range(4):
         v.reset(seed=100 + e)
         v.sync()
         ep_t += loop(lambda: v.step(greedy=True), 75)
         ep_k += 75
+    for e in range(4):
+        v.reset(seed=100 + e)
+        v.sync()
+        z_t += loop(lambda: v.step(greedy=True, fallback="zero"), 75)
     # the reference's own semantics in episodes: the fallback robots' actions drawn on the
     # host (np_random.choice(4) per robot in robot order, coverage.py:863-864), so every
     # step is the greedy kernel, a device-to-host copy of the actions and flags, the draws,
@@ -595,17 +602,20 @@ def bench_greedy(v, targets, R, M, B, K, args):
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
            "expert_step_ms_in_episodes": 1e3 * ep_t / ep_k,
            "expert_robot_steps_per_s_in_episodes": R * B * ep_k / ep_t,
+           "expert_step_ms_in_episodes_fallback_action0": 1e3 * z_t / ep_k,
            "expert_step_ms_in_episodes_host_fallback_draws": 1e3 * fa_t / fa_k,
            "expert_step_ms_steady_all_visited": 1e3 * el / K,
-           "expert_step_ms_two_launches_steady": 1e3 * el_sep / K,
-           "note": "expert step = controller(greedy=True) + step for every env. in_episodes (the headline): reset "
-                   "every 75 steps (EPISODE_LENGTH), resets untimed; fused: the greedy actions come from per-node "
-                   "greedy lists (or, with at most 32 targets unvisited, the direct minimum over them) inside the "
-                   "step's own launch (COV_ACTIONS_GREEDY), fallback robots take action 0 (no host round trip); "
-                   "host_fallback_draws: the reference's semantics, the greedy kernel, the actions and flags to "
-                   "the host, np_random draws for the fallback robots, the upload and the step; "
-                   "steady_all_visited: thousands of steps from one reset, every target visited (every robot "
-                   "on its fallback)"}
+           "expert_step_ms_steady_all_visited_fallback_action0": 1e3 * el0 / K,
+           "expert_step_ms_two_launches_steady_fallback_action0": 1e3 * el_sep / K,
+           "note": "expert step = controller(greedy=True) + step for every env, the reference's semantics. "
+                   "in_episodes (the headline): reset every 75 steps (EPISODE_LENGTH), resets untimed; the greedy "
+                   "actions come from per-node greedy lists (or, with at most 32 targets unvisited, the direct "
+                   "minimum over them) inside the step's own launch (COV_ACTIONS_GREEDY), and the fallback robots "
+                   "draw np_random.choice(4) from their env's MT19937 stream on the device in robot order "
+                   "(COV_GREEDY_RNG, bit-exact with the host RandomState); fallback_action0: the same with "
+                   "action 0 for the fallback robots; host_fallback_draws: the greedy kernel, the actions and "
+                   "flags to the host, np_random draws there, the upload and the step; steady_all_visited: "
+                   "thousands of steps from one reset, every target visited (every robot draws)"}
     if not args.no_cpu_baseline:
         from oracle import coverage as oc
         o = oc.CoverageOracle(targets, R, M)

@@ -93,6 +93,9 @@ struct cov_handle {
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
   int32_t* herr = nullptr;  // cov_step_host: page-locked per-env copies of the error word
+  // COV_GREEDY_RNG: every env's np_random stream (cov_set_rng; allocated on first use)
+  uint32_t* mt_key = nullptr;  // (B,624)
+  int32_t* mt_pos = nullptr;   // (B)
 };
 
 namespace {
@@ -126,7 +129,7 @@ void cov_release(cov_handle* h) {
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
                   a.receivers, a.obs_step, a.axy, a.nrec, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT, h->tm_glist, h->tm_glen,
                   h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
-                  h->goff};
+                  h->goff, h->mt_key, h->mt_pos};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -420,11 +423,44 @@ int cov_set_actions(cov_handle* h, const int32_t* actions) {
   return GF_OK;
 }
 
+int cov_set_rng(cov_handle* h, const uint32_t* keys, const int32_t* pos) {
+  if (!h || !keys || !pos) return cfail(GF_EINVAL, "null argument");
+  const size_t B = h->cfg.n_envs;
+  if (h->cfg.n_robots > gf::kMtN)
+    return cfail(GF_EINVAL, "device np_random draws need n_robots <= 624 (one key regeneration per step)");
+  for (size_t b = 0; b < B; ++b)
+    if (pos[b] < 0 || pos[b] > gf::kMtN) return cfail(GF_EINVAL, "stream position outside [0, 624]");
+  if (int rc = use(h)) return rc;
+  if (!h->mt_key) {
+    int rc;
+    if ((rc = calloc_dev(&h->mt_key, B * gf::kMtN)) || (rc = calloc_dev(&h->mt_pos, B))) return rc;
+  }
+  CV_HIP(hipMemcpyAsync(h->mt_key, keys, B * gf::kMtN * 4, hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipMemcpyAsync(h->mt_pos, pos, B * 4, hipMemcpyHostToDevice, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
+int cov_get_rng(cov_handle* h, uint32_t* keys, int32_t* pos) {
+  if (!h || !keys || !pos) return cfail(GF_EINVAL, "null argument");
+  if (!h->mt_key) return cfail(GF_ESTATE, "no np_random streams on the device (cov_set_rng)");
+  if (int rc = use(h)) return rc;
+  const size_t B = h->cfg.n_envs;
+  CV_HIP(hipMemcpyAsync(keys, h->mt_key, B * gf::kMtN * 4, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipMemcpyAsync(pos, h->mt_pos, B * 4, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return GF_OK;
+}
+
 int cov_step(cov_handle* h, const int32_t* actions, int flags) {
   if (!h) return cfail(GF_EINVAL, "null handle");
   if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
   CV_HIP(hipSetDevice(h->cfg.device));
   gf::CovArgs a = h->a;
+  if ((flags & COV_GREEDY_RNG) && !(flags & COV_ACTIONS_GREEDY))
+    return cfail(GF_EINVAL, "COV_GREEDY_RNG needs COV_ACTIONS_GREEDY");
+  if ((flags & COV_GREEDY_RNG) && !h->mt_key)
+    return cfail(GF_ESTATE, "COV_GREEDY_RNG: set the envs' np_random streams first (cov_set_rng)");
   if (flags & COV_ACTIONS_GREEDY) {
     // controller(greedy=True) in the step's own launch, from the greedy lists
     if (!h->tm_ready || !h->tm_glist) {
@@ -432,6 +468,8 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
       if (int rc = ensure_time_matrix(h)) return rc;
     }
     if (!h->tm_glist) {  // Tmax > kGreedyListMaxT: the row-scan greedy kernel, then the step
+      if (flags & COV_GREEDY_RNG)
+        return cfail(GF_EINVAL, "COV_GREEDY_RNG needs max_nodes - n_robots <= 1024 (the greedy lists)");
       if (int rc = cov_controller_greedy(h, nullptr, nullptr, nullptr)) return rc;
       return cov_step(h, nullptr, COV_ACTIONS_RESIDENT);
     }
@@ -443,6 +481,10 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     a.gprev = h->tm_prevT;
     a.gactions = h->actions;
     a.needs_random = h->needs_random;
+    if (flags & COV_GREEDY_RNG) {
+      a.mt_key = h->mt_key;
+      a.mt_pos = h->mt_pos;
+    }
   } else if (flags & COV_ACTIONS_DEVICE) {
     if (!actions) return cfail(GF_EINVAL, "null action pointer");
     a.actions = actions;

@@ -44,6 +44,11 @@ struct CovArgs {
   const int16_t* gprev;   // (B,Tmax,Tmax) graph_previous[t, c] at [c][t] (greedy_direct)
   int32_t* gactions;      // (B,R) the greedy actions taken (written)
   uint8_t* needs_random;  // (B,R) robots the reference hands to np_random.choice (action 0 here)
+  // COV_GREEDY_RNG: those robots draw np_random.choice(4) (:863-864) from their env's
+  // MT19937 stream instead, in robot order, as numpy's legacy RandomState does (nullptr:
+  // action 0). The stream is RandomState.get_state()'s key words and position.
+  uint32_t* mt_key;       // (B,624)
+  int32_t* mt_pos;        // (B) in [0, 624]
   // cov_step_host: after the step, controller(greedy=True)'s actions of the RESULTING state
   // from the greedy lists (glist / glen / gstride) into gactions / needs_random (and the
   // host copies below), for the next step of an expert loop
@@ -168,6 +173,51 @@ __device__ __forceinline__ void greedy_direct_list(const uint32_t* vbits, int T,
     cnt += __popcll(m);
   }
   if (lane == 0) *ucount = cnt;
+}
+
+// np_random's generator (numpy's legacy RandomState: MT19937, the published algorithm of
+// Matsumoto & Nishimura). choice(4) with uniform p is randint(0, 4): one 32-bit output,
+// masked to 2 bits (the mask equals the range, so no draw is ever rejected).
+constexpr int kMtN = 624, kMtM = 397;
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  return y ^ (y >> 18);
+}
+__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t next, uint32_t far) {
+  const uint32_t y = (cur & 0x80000000u) | (next & 0x7fffffffu);
+  return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+// The key's regeneration (after 624 outputs) by the whole workgroup on a key in LDS. Word i
+// mixes words i, i+1 and i+397 (mod 624, the wrapped ones already regenerated), so three
+// passes of at most 227 independent words each, then word 623: [0,227) reads only old
+// words, [227,454) reads the first pass's results, [454,623) the second's. Ends with a
+// barrier. Every thread of the workgroup calls it.
+template <int NT>
+__device__ __forceinline__ void mt_regen(uint32_t* k) {
+  constexpr int P = kMtN - kMtM;  // 227
+  constexpr int S = (P + NT - 1) / NT;
+  auto pass = [&](int lo, int hi) {
+    uint32_t v[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int i = lo + static_cast<int>(threadIdx.x) + s * NT;
+      if (i < hi) v[s] = mt_mix(k[i], k[i + 1], k[i < P ? i + kMtM : i - P]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int i = lo + static_cast<int>(threadIdx.x) + s * NT;
+      if (i < hi) k[i] = v[s];
+    }
+    __syncthreads();
+  };
+  pass(0, P);
+  pass(P, 2 * P);
+  pass(2 * P, kMtN - 1);
+  if (threadIdx.x == 0) k[kMtN - 1] = mt_mix(k[kMtN - 1], k[0], k[kMtM - 1]);
+  __syncthreads();
 }
 
 // Greedy expert (coverage_expert.hip).

@@ -214,7 +214,10 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
   }
   if (a.actions || a.glist)
     for (int k = tid; k < M; k += NT) first[k] = INT_MAX;
-  if (tid == 0) *counter = 0;
+  if (tid == 0) {
+    counter[0] = 0;  // targets newly visited
+    counter[1] = 0;  // COV_GREEDY_RNG: fallback robots
+  }
   GF_COV_STAMP(0);
   const int32_t* act = a.actions ? a.actions + (size_t)b * R : nullptr;
   // COV_ACTIONS_GREEDY: controller(greedy=True) picks each robot's action in this launch
@@ -289,6 +292,19 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     greedy_direct_list(gvis, T, any_vis, ulist, ucount);
     __syncthreads();
   }
+  // the node action ai of a robot on c points at (:184-200)
+  auto aim = [&](int c, int ai, const int4& offer) {
+    return dirty ? action_node(nbr, cnt, c, ai, R)
+                 : (ai == 0 ? offer.x : ai == 1 ? offer.y : ai == 2 ? offer.z : offer.w);
+  };
+  auto prefetch = [&](Pf& p, int n) {
+    const int t = n - R;
+    p.n = n;
+    p.r0 = rec[4 * t];
+    p.r1 = rec[4 * t + 1];
+    p.r2 = rec[4 * t + 2];
+    p.was = vis[t];
+  };
   // robot i: its node c and the node n its action points at (claiming c if n == c)
   auto pick = [&](int i, const Ld& l, int& c) {
     c = l.c;
@@ -310,16 +326,22 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     }
     cur_s[i] = c;
     int n = c;
-    if (greedy) {  // :814-869 from the node's greedy list; fallbacks take action 0 here
+    if (greedy) {  // :814-869 from the node's greedy list; fallbacks: action 0 or drawn below
       const size_t row = (size_t)b * Tm + (c - R);
       const int g = gdirect ? greedy_direct(a.gcost + row * Tm, a.gprev + row * Tm, nbr + 4 * (c - R), cnt[c - R],
                                             ulist, *ucount)
                             : greedy_from_list(a.glist + row * a.gstride, a.glen + row, gvis, any_vis, nv0 >= T);
       const uint32_t flag = static_cast<uint32_t>(g) >> 2;
       if (flag & kGreedyErr) atomicOr(a.err, 8);
-      ai = (flag & kGreedyRnd) ? 0 : (g & 3);
+      const bool rnd = flag & kGreedyRnd;
+      ai = rnd ? 0 : (g & 3);
+      a.needs_random[(size_t)b * R + i] = rnd ? 1 : 0;
+      if (rnd && a.mt_key) {  // COV_GREEDY_RNG: drawn in robot order after every pick
+        chosen[i] = -1;
+        atomicAdd(counter + 1, 1);
+        return c;
+      }
       a.gactions[(size_t)b * R + i] = ai;
-      a.needs_random[(size_t)b * R + i] = (flag & kGreedyRnd) ? 1 : 0;
     }
     if (has_act) {
       // step (:184-200): the node the action points at; robots that stay claim first
@@ -327,8 +349,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
         atomicOr(a.err, 4);
         ai = 0;
       }
-      n = dirty ? action_node(nbr, cnt, c, ai, R)
-                : (ai == 0 ? offer.x : ai == 1 ? offer.y : ai == 2 ? offer.z : offer.w);
+      n = aim(c, ai, offer);
       chosen[i] = n;
       if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
     }
@@ -347,15 +368,8 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     }
     // then every slot's record: no wait for one slot's record before the next slot
 #pragma unroll
-    for (int j = 0; j < RPT; ++j) {
-      const int t = pf[j].n - R;
-      if (t >= 0) {
-        pf[j].r0 = rec[4 * t];
-        pf[j].r1 = rec[4 * t + 1];
-        pf[j].r2 = rec[4 * t + 2];
-        pf[j].was = vis[t];
-      }
-    }
+    for (int j = 0; j < RPT; ++j)
+      if (pf[j].n >= 0) prefetch(pf[j], pf[j].n);
   } else {
     for (int i = tid; i < R; i += NT) {
       int c;
@@ -364,6 +378,66 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
   }
   __syncthreads();
   GF_COV_STAMP(1);
+
+  if (greedy && a.mt_key && counter[1] > 0) {
+    // COV_GREEDY_RNG: u_ind[i] = np_random.choice(4) for each fallback robot in robot
+    // order (:861-864): the k-th fallback robot takes output pos + k of its env's stream.
+    // The key goes through LDS; when pos + k passes 624 the key is regenerated in LDS
+    // (the earlier words read first) and written back. R <= 624 (checked by the host):
+    // at most one regeneration per step.
+    uint32_t* kb = reinterpret_cast<uint32_t*>(ucount + 1);
+    uint32_t* pm = kb + kMtN;  // fallback robots as bits, 32 per word
+    uint32_t* key = a.mt_key + (size_t)b * kMtN;
+    const int nfall = counter[1];
+    const int pos = a.mt_pos[b];
+    for (int k = tid; k < kMtN; k += NT) kb[k] = key[k];
+    {
+      const int lane = tid & 63, wv = tid >> 6;
+      for (int k0 = wv * 64; k0 < R; k0 += NT) {
+        const uint64_t m = __ballot(k0 + lane < R && chosen[k0 + lane] < 0);
+        if (lane == 0) {
+          pm[k0 >> 5] = static_cast<uint32_t>(m);
+          pm[(k0 >> 5) + 1] = static_cast<uint32_t>(m >> 32);
+        }
+      }
+    }
+    __syncthreads();
+    auto word = [&](int i) {  // the stream index of robot i's draw
+      int r = __popc(pm[i >> 5] & ((1u << (i & 31)) - 1u));
+      for (int w = 0; w < (i >> 5); ++w) r += __popc(pm[w]);
+      return pos + r;
+    };
+    // the raw words parked in new_s, which the claim resolution below writes first
+    for (int i = tid; i < R; i += NT)
+      if (chosen[i] < 0 && word(i) < kMtN) new_s[i] = static_cast<int>(kb[word(i)]);
+    if (pos + nfall > kMtN) {
+      mt_regen<NT>(kb);  // its first barrier orders the reads above before its writes
+      for (int i = tid; i < R; i += NT)
+        if (chosen[i] < 0 && word(i) >= kMtN) new_s[i] = static_cast<int>(kb[word(i) - kMtN]);
+      for (int k = tid; k < kMtN; k += NT) key[k] = kb[k];
+    }
+    if (tid == 0) a.mt_pos[b] = pos + nfall > kMtN ? pos + nfall - kMtN : pos + nfall;
+    auto draw = [&](int i, const int4& offer, Pf* p) {
+      const int c = cur_s[i];
+      const int ai = static_cast<int>(mt_temper(static_cast<uint32_t>(new_s[i])) & 3u);
+      a.gactions[(size_t)b * R + i] = ai;
+      const int n = aim(c, ai, offer);
+      chosen[i] = n;
+      if (n == c) atomicOr(&claim[n >> 5], 1u << (n & 31));
+      else if (p) prefetch(*p, n);
+    };
+    if (one) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int i = tid + j * NT;
+        if (i < R && chosen[i] < 0) draw(i, ld[j].offer, &pf[j]);
+      }
+    } else {
+      for (int i = tid; i < R; i += NT)
+        if (chosen[i] < 0) draw(i, load(i).offer, nullptr);
+    }
+    __syncthreads();
+  }
 
   if (has_act) {
     // then, in robot order, a move succeeds unless its node is already claimed; a
@@ -722,7 +796,7 @@ hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all
 
 size_t cov_step_lds_bytes(int R, int M) {
   return (size_t)3 * R * 4 + (size_t)2 * ((M + 31) / 32) * 4 + 16 + (size_t)M * 4 + (size_t)((M - R + 63) / 64) * 8 +
-         (size_t)(kGreedyDirectMax + 1) * 4;
+         (size_t)(kGreedyDirectMax + 1) * 4 + (size_t)kMtN * 4 + (size_t)((R + 63) / 64) * 8;
 }
 
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {

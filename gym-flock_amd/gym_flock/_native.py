@@ -66,6 +66,7 @@ COV_OUT_DEVICE = 0x4
 COV_FLAT_F32 = 0x8
 COV_MASK_ALL = 0x10
 COV_NEXT_GREEDY = 0x40
+COV_GREEDY_RNG = 0x80
 
 
 class GymFlockError(RuntimeError):
@@ -134,6 +135,8 @@ SIGNATURES = {
     "cov_reset": [_P, _P, _P],
     "cov_step": [_P, _P, _I],
     "cov_set_actions": [_P, _P],
+    "cov_set_rng": [_P, _P, _P],
+    "cov_get_rng": [_P, _P, _P],
     "cov_step_host": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I],
     "cov_set_robot_positions": [_P, _I, _P],
     "cov_get_obs": [_P, _I, _P, _P, _P, _P, _P],
@@ -701,6 +704,7 @@ class CoverageHandle:
         # ~7 us, host-bound
         self._step_resident = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_RESIDENT)
         self._step_greedy = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_GREEDY)
+        self._step_greedy_rng = functools.partial(self.lib.cov_step, h, None, COV_ACTIONS_GREEDY | COV_GREEDY_RNG)
 
     def close(self):
         h = getattr(self, "h", None)
@@ -735,12 +739,13 @@ class CoverageHandle:
         assert vi.shape == (self.n_envs, self.t_max), vi.shape
         check(self.lib.cov_reset(self.h, ptr(st), ptr(vi)))
 
-    def step(self, actions=None, resident=False, greedy=False):
+    def step(self, actions=None, resident=False, greedy=False, rng=False):
         """actions (B,R) host ints; or resident=True (the last set/greedy actions); or
         greedy=True: controller(greedy=True)'s actions computed inside the step's launch
-        (fallback robots take action 0, needs_random flags them)."""
+        (fallback robots take action 0, needs_random flags them; with rng=True they draw
+        np_random.choice(4) from the envs' device streams, set_rng)."""
         if resident or greedy:
-            rc = self._step_greedy() if greedy else self._step_resident()
+            rc = (self._step_greedy_rng() if rng else self._step_greedy()) if greedy else self._step_resident()
             if rc:
                 check(rc)
             return
@@ -750,6 +755,26 @@ class CoverageHandle:
     def set_actions(self, actions):
         a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
         check(self.lib.cov_set_actions(self.h, ptr(a)))
+
+    def set_rng(self, states):
+        """Every env's np_random stream for step(greedy=True, rng=True): a list of B
+        RandomState objects (or get_state() tuples), copied to the device (cov_set_rng)."""
+        keys = np.empty((self.n_envs, 624), np.uint32)
+        pos = np.empty(self.n_envs, np.int32)
+        assert len(states) == self.n_envs
+        for b, st in enumerate(states):
+            st = st.get_state() if hasattr(st, "get_state") else st
+            assert st[0] == "MT19937" and len(st[1]) == 624, "a legacy RandomState (MT19937) state"
+            keys[b], pos[b] = st[1], st[2]
+        check(self.lib.cov_set_rng(self.h, ptr(keys), ptr(pos)))
+
+    def get_rng(self):
+        """(keys (B,624) uint32, pos (B) int32): the device streams after the steps that drew
+        from them; RandomState.set_state(("MT19937", keys[b], pos[b])) continues env b's."""
+        keys = np.empty((self.n_envs, 624), np.uint32)
+        pos = np.empty(self.n_envs, np.int32)
+        check(self.lib.cov_get_rng(self.h, ptr(keys), ptr(pos)))
+        return keys, pos
 
     def step_host(self, actions, nodes, edges, senders, receivers, step, reward, done, closest,
                   next_actions=None, needs_random=None):

@@ -157,24 +157,45 @@ class VecCoverage:
             self.n_targets[env] = len(targets)
 
     def reset(self, seed=0):
+        """Env b is a reference env whose np_random was seeded seed + env_offset + b: its
+        reset draws here, and its stream then continues on the device for the greedy
+        expert's fallback draws (step(greedy=True)); np_random(b) reads it back."""
         R, tmax = self.n_robots, self.h.t_max
         start = np.empty((self.n_envs, R), np.int32)
         visited = np.ones((self.n_envs, tmax), np.uint8)
+        rngs = []
         for b in range(self.n_envs):
             rs = np.random.RandomState(seed + self.env_offset + b)
             T = int(self.n_targets[b])
             start[b] = rs.choice(np.arange(T), size=(R,), replace=False)
             drop = rs.choice(np.arange(T) + R, size=(int(T * self.frac),), replace=False)
             visited[b, drop - R] = 0
+            rngs.append(rs)
         self.h.reset(start, visited)
+        if R <= 624:  # cov_set_rng: one key regeneration per step at most
+            self.h.set_rng(rngs)
+            self._rng = True
         return start, visited
 
-    def step(self, actions=None, resident=False, greedy=False):
+    def np_random(self, env):
+        """Env `env`'s np_random after the fallback draws of the steps so far (a RandomState
+        continuing the device stream)."""
+        keys, pos = self.h.get_rng()
+        rs = np.random.RandomState()
+        rs.set_state(("MT19937", keys[env], int(pos[env])))
+        return rs
+
+    def step(self, actions=None, resident=False, greedy=False, fallback="draw"):
         """actions (B,R); or resident=True (the last set/greedy actions); or greedy=True
-        (the greedy expert's actions computed in the step's own launch; fallback robots
-        take action 0, see include/gymflock.h COV_ACTIONS_GREEDY)."""
+        (controller(greedy=True), coverage.py:800-872, computed in the step's own launch).
+        fallback: robots the reference hands to np_random.choice(4) (:861-864) draw it from
+        their env's stream on the device ("draw", the reference's semantics) or take
+        action 0 ("zero"); include/gymflock.h COV_ACTIONS_GREEDY, COV_GREEDY_RNG."""
         if resident or greedy:
-            rc = self.h._step_greedy() if greedy else self.h._step_resident()
+            if greedy:
+                rc = self.h._step_greedy_rng() if fallback == "draw" else self.h._step_greedy()
+            else:
+                rc = self.h._step_resident()
             if rc:
                 nat.check(rc)
             return

@@ -301,9 +301,13 @@ typedef struct cov_handle cov_handle;
 #define COV_ACTIONS_GREEDY   0x20 /* the step's actions are controller(greedy=True)'s (:800-872),
                                     computed in the same launch from per-node greedy lists
                                     built with the time matrix; robots the reference hands to
-                                    np_random.choice(4) take action 0 (needs_random flags them:
-                                    for the reference's draws use cov_controller_greedy). The
-                                    actions taken stay resident (COV_ACTIONS_RESIDENT). */
+                                    np_random.choice(4) take action 0 (needs_random flags them),
+                                    or with COV_GREEDY_RNG draw it on the device. The actions
+                                    taken stay resident (COV_ACTIONS_RESIDENT). */
+#define COV_GREEDY_RNG       0x80 /* with COV_ACTIONS_GREEDY: each fallback robot takes
+                                    np_random.choice(4) (:861-864) from its env's stream (set
+                                    by cov_set_rng), in robot order, bit-exact with numpy's
+                                    legacy RandomState; the stream advances on the device */
 
 int cov_create(const cov_config* cfg, cov_handle** out);        /* CoverageEnv.__init__ :83 */
 int cov_destroy(cov_handle* h);
@@ -316,6 +320,12 @@ int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited);
 /* step(action) (:174-204, :234-364): actions[B][R] in [0,4). */
 int cov_step(cov_handle* h, const int32_t* actions, int flags);
 int cov_set_actions(cov_handle* h, const int32_t* actions);
+/* Every env's np_random stream for COV_GREEDY_RNG steps, in the layout of numpy's
+ * RandomState.get_state() (MT19937): keys[B][624] the key words, pos[B] in [0, 624] the
+ * position. Needs n_robots <= 624. cov_get_rng reads them back (after the steps that
+ * drew from them), to continue the stream on the host with RandomState.set_state. */
+int cov_set_rng(cov_handle* h, const uint32_t* keys, const int32_t* pos);
+int cov_get_rng(cov_handle* h, uint32_t* keys, int32_t* pos);
 /* The drop-in env's step(action) (coverage.py:174-204 with _get_obs_reward :234-364) as
  * one launch and one wait, the reference driver's loop (test.py:43-74): actions[B][R] in
  * [0,4) (B*R <= 512: passed in the kernel arguments), then the whole observation of every

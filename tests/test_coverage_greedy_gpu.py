@@ -262,7 +262,7 @@ def test_fused_greedy_step_equals_separate():
             vb.h.set_robot_positions(1, xr)
         ea, er = va.h.controller_greedy()
         va.step(resident=True)
-        vb.step(greedy=True)
+        vb.step(greedy=True, fallback="zero")
         ga, gr = vb.h.actions()
         np.testing.assert_array_equal(ga, ea)
         np.testing.assert_array_equal(gr, er)
@@ -436,3 +436,117 @@ def test_greedy_list_and_direct_paths_vs_oracle():
     assert max(n_left) > 32 and min(n_left) <= 32, n_left  # both paths taken
     for h in hs:
         h.close()
+
+
+def _reset_stream(seed, T, R):
+    """A reference env's np_random after reset's two draws (coverage.py:405-424)."""
+    rs = np.random.RandomState(seed)
+    rs.choice(np.arange(T), size=(R,), replace=False)
+    rs.choice(np.arange(T) + R, size=(int(T * 0.5),), replace=False)
+    return rs
+
+
+@pytest.mark.parametrize("path", GREEDY, ids=os.path.basename)
+def test_device_rng_greedy_episode_matches_reference(path):
+    """COV_GREEDY_RNG: the recorded greedy episode as fused greedy steps, the fallback
+    robots' np_random.choice(4) (coverage.py:861-864) drawn on the device from the env's
+    stream (the fixture's seed after reset's draws): actions, rewards and robots' nodes
+    bit-exact at every step, and the device stream afterwards equals the host RandomState
+    after as many draws."""
+    f = np.load(path)
+    h, R, T, M = _handle_for(f)
+    start = oc.closest_targets(f["x0"][:R], f["targets"], R) - R
+    visited = np.ones((1, M - R), np.uint8)
+    visited[0, :T] = f["visited0"][R:].astype(np.uint8)
+    h.reset(start[None], visited)
+    rs = _reset_stream(ENV_SEED[os.path.basename(path)], T, R)
+    h.set_rng([rs])
+    n_draws = 0
+    for t in range(len(f["actions"])):
+        h.step(greedy=True, rng=True)
+        a, rnd = h.actions()
+        np.testing.assert_array_equal(a[0], f["actions"][t])
+        n_draws += int(rnd.sum())
+        r, d = h.rewards()
+        assert r[0] == f["reward"][t] and d[0] == f["done"][t]
+        np.testing.assert_array_equal(h.robots(0)[1], f["closest"][t])
+    assert n_draws > 0
+    rs.randint(0, 4, size=n_draws)
+    keys, pos = h.get_rng()
+    st = rs.get_state()
+    assert pos[0] == st[2]
+    np.testing.assert_array_equal(keys[0], st[1])
+    h.close()
+
+
+@pytest.mark.parametrize("R", [16, 200])
+def test_device_rng_batched_vs_oracle(R):
+    """VecCoverage.step(greedy=True) with the reference's fallback draws (the default):
+    4 envs with their own maps and streams (seed + b after reset's draws), two half-batch
+    launches per step, against the oracle's greedy expert with per-env RandomStates drawing
+    in robot order. At R=200 most robots fall back once the targets near them are visited,
+    so each stream passes several key regenerations. Actions, fallback flags, rewards and
+    nodes bit-exact every step; the device streams equal the host's at the end."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, M, steps = 4, 1000, 40
+    maps = []
+    for b in range(B):
+        np.random.seed(500 + b)
+        maps.append(generate_targets())
+    v = VecCoverage(B, R, max_nodes=M)
+    for b in range(B):
+        v.set_targets(maps[b], env=b)
+    start, visited = v.reset(seed=40)
+    orcs, mats, rngs = [], [], []
+    for b in range(B):
+        T = len(maps[b])
+        o = oc.CoverageOracle(maps[b], R, M)
+        o.reset(start[b], np.nonzero(visited[b, :T] == 0)[0] + R)
+        orcs.append(o)
+        mats.append(oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R))
+        rngs.append(_reset_stream(40 + b, T, R))
+    n_draws = 0
+    for t in range(steps):
+        v.step(greedy=True)
+        ga, gr = v.h.actions()
+        r, d = v.rewards()
+        for b in range(B):
+            o = orcs[b]
+            cur = o.closest()
+            ea, er = oc.greedy_actions(mats[b][0], mats[b][1], cur, o.visited[R:],
+                                       oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+            k = np.nonzero(er)[0]
+            ea[k] = rngs[b].choice(4, size=len(k))
+            n_draws += len(k)
+            np.testing.assert_array_equal(gr[b], er)
+            np.testing.assert_array_equal(ga[b], ea)
+            _, rr, dd = o.step(ea)
+            assert r[b] == rr and d[b] == dd
+            np.testing.assert_array_equal(v.h.robots(b)[1], o.closest())
+    if R == 200:
+        assert n_draws > 4 * 2 * 624, n_draws  # regenerations in every stream
+    for b in range(B):
+        st, want = v.np_random(b).get_state(), rngs[b].get_state()
+        assert st[2] == want[2]
+        np.testing.assert_array_equal(st[1], want[1])
+    v.close()
+
+
+def test_device_rng_argument_checks():
+    """COV_GREEDY_RNG before cov_set_rng is GF_ESTATE; positions outside [0, 624] and more
+    than 624 robots are refused."""
+    f = np.load(GREEDY[0])
+    h, R, T, M = _handle_for(f)
+    start = np.arange(R, dtype=np.int32)[None]
+    h.reset(start, np.zeros((1, M - R), np.uint8))
+    with pytest.raises(nat.GymFlockError, match="cov_set_rng"):
+        h.step(greedy=True, rng=True)
+    st = list(np.random.RandomState(1).get_state())
+    st[2] = 625
+    with pytest.raises(nat.GymFlockError, match="position"):
+        h.set_rng([tuple(st)])
+    h.close()
+    h = nat.CoverageHandle(700, 1, 1500)
+    with pytest.raises(nat.GymFlockError, match="624"):
+        h.set_rng([np.random.RandomState(1)])
+    h.close()
