@@ -93,6 +93,12 @@ struct cov_handle {
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
   int32_t* herr = nullptr;  // cov_step_host: page-locked per-env copies of the error word
+  // cov_step_host: the launch's completion flag (done_flag.h): device counter, page-locked
+  // word, its mapped address
+  int32_t* fin_cnt = nullptr;
+  int32_t* fin_host = nullptr;
+  int32_t* fin_dev = nullptr;
+  int32_t fin_seq = 0;
   // COV_GREEDY_RNG: every env's np_random stream (cov_set_rng; allocated on first use)
   uint32_t* mt_key = nullptr;  // (B,624)
   int32_t* mt_pos = nullptr;   // (B)
@@ -134,6 +140,8 @@ void cov_release(cov_handle* h) {
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
   if (h->herr) hipHostFree(h->herr);
+  if (h->fin_cnt) hipFree(h->fin_cnt);
+  if (h->fin_host) hipHostFree(h->fin_host);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1]})
     if (e) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -614,6 +622,27 @@ int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* ed
   }
   std::memset(h->herr, 0, B * sizeof(int32_t));
   a.h_err = cov_mapped(h->herr);
+  // every destination page-locked and the actions inline: the launch is the call's only
+  // device work, and the host waits for the kernel's own completion flag (done_flag.h)
+  const bool fin = n * 4 <= (size_t)gf::kCovUInlineBytes && (!nodes || a.h_nodes) && (!edges || a.h_edges) &&
+                   (!senders || a.h_senders) && (!receivers || a.h_receivers) && (!step || a.h_step) &&
+                   (!reward || a.h_reward) && (!done || a.h_done) && (!closest || a.h_closest) &&
+                   (!next_actions || a.h_next) && (!needs_random || a.h_nrand);
+  if (fin) {
+    if (!h->fin_cnt) {
+      if (int rc = calloc_dev(&h->fin_cnt, 1)) return rc;
+      void* p = nullptr;
+      if (hipHostMalloc(&p, 64, hipHostMallocMapped) != hipSuccess)
+        return cfail(GF_ENOMEM, "hipHostMalloc (completion flag)");
+      h->fin_host = static_cast<int32_t*>(p);
+      *h->fin_host = 0;
+      h->fin_dev = cov_mapped(h->fin_host);
+      if (!h->fin_dev) return cfail(GF_EHIP, "completion flag: no mapped address");
+    }
+    a.fin.cnt = h->fin_cnt;
+    a.fin.host = h->fin_dev;
+    a.fin.seq = ++h->fin_seq;
+  }
   hipError_t e;
   if (n * 4 <= (size_t)gf::kCovUInlineBytes) {
     e = gf::launch_cov_step_uin(a, actions, h->stream);  // actions in the kernel arguments
@@ -636,12 +665,18 @@ int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* ed
   if (next_actions && !a.h_next) CV_HIP(hipMemcpyAsync(next_actions, h->actions, n * 4, hipMemcpyDeviceToHost, h->stream));
   if (needs_random && !a.h_nrand)
     CV_HIP(hipMemcpyAsync(needs_random, h->needs_random, n, hipMemcpyDeviceToHost, h->stream));
-  // spin on the stream: a drop-in step is latency-bound (a blocking wait's wake-up costs
-  // a sizeable part of it)
-  for (;;) {
-    const hipError_t q = hipStreamQuery(h->stream);
-    if (q == hipSuccess) break;
-    if (q != hipErrorNotReady) return cfail(GF_EHIP, std::string("cov_step_host: ") + hipGetErrorString(q));
+  if (fin) {
+    const hipError_t q = gf::wait_done(h->fin_host, h->fin_seq, h->stream);
+    if (q == hipErrorUnknown) return cfail(GF_EHIP, "cov_step_host: the step finished without its completion flag");
+    if (q != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_host: ") + hipGetErrorString(q));
+  } else {
+    // spin on the stream: a drop-in step is latency-bound (a blocking wait's wake-up
+    // costs a sizeable part of it)
+    for (;;) {
+      const hipError_t q = hipStreamQuery(h->stream);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return cfail(GF_EHIP, std::string("cov_step_host: ") + hipGetErrorString(q));
+    }
   }
   int err = 0;
   for (size_t b = 0; b < B; ++b) err |= h->herr[b];

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "done_flag.h"
+
 namespace gf {
 
 // Device buffers of a batch of B Coverage envs with R robots and room for M nodes
@@ -66,6 +68,7 @@ struct CovArgs {
   int32_t* h_next;        // (B,R) next_greedy actions
   uint8_t* h_nrand;       // (B,R) next_greedy needs_random flags
   int32_t* h_err;         // (B) the device error word as this env's workgroup ends
+  DoneFlag fin;           // cov_step_host: the grid's completion flag (done_flag.h)
 };
 
 // cov_step_host: one env's actions travel in the kernel arguments up to this many bytes

@@ -677,6 +677,7 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   GF_COV_STAMP(4);
 #endif
+  signal_done(a.fin);  // cov_step_host: the host waits for this, not the stream
 }
 
 // reset (:405-424 after the random draws): robots onto their start targets, the

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "done_flag.h"
+
 namespace gf {
 
 // Ablation switches (StepArgs / KnnArgs .diag, timing experiments that give wrong
@@ -90,6 +92,7 @@ struct StepArgs {
   unsigned knn_qmax;      // 2^qbits - 2
   double knn_qmaxd;       // the same as a double (compared with r2 * scale)
   int knn_jbits;          // bits of the agent index (qbits = 32 - jbits)
+  DoneFlag fin;           // drop-in launch: the grid's completion flag (done_flag.h)
 };
 
 // The drop-in step's actions passed in the kernel arguments (fe_step_host, one env of up

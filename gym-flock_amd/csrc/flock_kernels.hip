@@ -1547,6 +1547,7 @@ void flock_step_kernel(typename std::conditional<UIN, StepArgsU, StepArgs>::type
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   GF_STAMP(11);
 #endif
+  signal_done(a.fin);  // drop-in launches: the host waits for this, not the stream
 }
 
 // ---------------------------------------------------------------------------------

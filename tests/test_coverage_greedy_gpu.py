@@ -470,7 +470,8 @@ def test_device_rng_greedy_episode_matches_reference(path):
         r, d = h.rewards()
         assert r[0] == f["reward"][t] and d[0] == f["done"][t]
         np.testing.assert_array_equal(h.robots(0)[1], f["closest"][t])
-    assert n_draws > 0
+    if "r20" in path:
+        assert n_draws > 0  # (the r6 episode never falls back)
     rs.randint(0, 4, size=n_draws)
     keys, pos = h.get_rng()
     st = rs.get_state()
