@@ -1135,7 +1135,8 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
     }
     a.fin.cnt = h->fin_cnt;
     a.fin.host = h->fin_dev;
-    a.fin.seq = ++h->fin_seq;
+    h->fin_seq = (h->fin_seq & 0x3fffffff) + 1;  // never 0 (the word's initial value), no overflow
+    a.fin.seq = h->fin_seq;
   }
   if (int rc = timed_launch(h, a, dyn, uf64, ctrl)) return rc;
   if (dyn) h->cur ^= 1;

@@ -641,7 +641,8 @@ int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* ed
     }
     a.fin.cnt = h->fin_cnt;
     a.fin.host = h->fin_dev;
-    a.fin.seq = ++h->fin_seq;
+    h->fin_seq = (h->fin_seq & 0x3fffffff) + 1;  // never 0 (the word's initial value), no overflow
+    a.fin.seq = h->fin_seq;
   }
   hipError_t e;
   if (n * 4 <= (size_t)gf::kCovUInlineBytes) {
