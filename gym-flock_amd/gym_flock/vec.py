@@ -174,7 +174,6 @@ class VecCoverage:
         self.h.reset(start, visited)
         if R <= 624:  # cov_set_rng: one key regeneration per step at most
             self.h.set_rng(rngs)
-            self._rng = True
         return start, visited
 
     def np_random(self, env):
