@@ -685,7 +685,9 @@ int timed_launch(fe_handle* h, const gf::StepArgs& a_in, bool dyn, bool uf64, bo
 // kNN of the current state (mode: knn_mode; 0 = a full kNN with no step behind it):
 // 1: the last launch wrote this state's adjacency (packed outputs), which lets agents
 // with >= k neighbours rank only those; 2: the last launch ranked the rows it could.
-int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs_to = nullptr) {
+// fin: the drop-in step's completion flag, carried by the (single, unsplit) rim launch
+int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs_to = nullptr,
+                   const gf::DoneFlag* fin = nullptr) {
 #ifdef GF_DIAG
   if (mode == 2 && (h->diag & 0x80000)) {  // ablation: no rim kNN launch (timing only)
     h->has_knn = true;
@@ -718,7 +720,7 @@ int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs
     // the rim kNN of a fused step goes on the step's own streams, right behind the half
     // that produced its rows: a kNN handle then runs two hardware queues, like a plain
     // one, and the next step's half orders after its rim by stream order (no events)
-    if (h->last_b0 > 0 && h->s2_pending) {
+    if (h->last_b0 > 0 && h->s2_pending && !fin) {
       const int B0 = h->last_b0, N = k.N, K = k.K;
       const size_t e0 = (size_t)B0 * N;
       gf::KnnArgs k1 = k;
@@ -735,6 +737,7 @@ int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs
       if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
     } else {
       if (int rc = join_s2(h)) return rc;
+      if (fin) k.fin = *fin;
       hipError_t e = gf::launch_knn(k, h->stream);
       if (e != hipSuccess) return fail_hip("flock_knn_kernel launch", e);
     }
@@ -1117,11 +1120,14 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
     a.knn_idx = idx_m;
     a.knn_obs = obs_m;
   }
-  // When this launch is the call's only device work (every output page-locked, no rim
-  // kernel, no copy after it), the host waits for the kernel's own completion flag, not
-  // for the stream (done_flag.h: ~8 us sooner)
+  // When the call's device work ends with one launch that writes the last outputs to
+  // page-locked memory (every output page-locked, no copy after it: the step, or the rim
+  // kNN behind it), the host waits for that kernel's own completion flag, not for the
+  // stream (done_flag.h: ~8 us sooner)
   const bool fin = (!state_values || sv_m) && (!network || net_m) && (!rewards || rw_m) && (!ctrl || ct_m) &&
-                   (!knn || (kdirect && gf::step_knn_exact(h->cfg.n_agents, h->T)));
+                   (!knn || kdirect);
+  const bool rim_last = knn && !gf::step_knn_exact(h->cfg.n_agents, h->T);
+  gf::DoneFlag fd{};
   if (fin) {
     if (!h->fin_cnt) {
       if (int rc = dalloc(&h->fin_cnt, 1)) return rc;
@@ -1133,10 +1139,11 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
       h->fin_dev = static_cast<int32_t*>(mapped_ptr(p));
       if (!h->fin_dev) return fail(GF_EHIP, "completion flag: no mapped address");
     }
-    a.fin.cnt = h->fin_cnt;
-    a.fin.host = h->fin_dev;
+    fd.cnt = h->fin_cnt;
+    fd.host = h->fin_dev;
     h->fin_seq = (h->fin_seq & 0x3fffffff) + 1;  // never 0 (the word's initial value), no overflow
-    a.fin.seq = h->fin_seq;
+    fd.seq = h->fin_seq;
+    if (!rim_last) a.fin = fd;
   }
   if (int rc = timed_launch(h, a, dyn, uf64, ctrl)) return rc;
   if (dyn) h->cur ^= 1;
@@ -1158,7 +1165,9 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
     // the rim (or whole) kNN of the new state, then its rows to the host: page-locked
     // destinations by one copy kernel through their mapped addresses (a DMA copy costs
     // ~12 us of latency each), others by copies
-    if (int rc = launch_knn_cur(h, km, kdirect ? idx_m : nullptr, kdirect ? obs_m : nullptr)) return rc;
+    if (int rc = launch_knn_cur(h, km, kdirect ? idx_m : nullptr, kdirect ? obs_m : nullptr,
+                                (fin && rim_last) ? &fd : nullptr))
+      return rc;
     if (int rc = join_s2(h)) return rc;
     if (int rc = join_k(h)) return rc;
     if (kdirect) {

@@ -118,6 +118,7 @@ struct KnnArgs {
   int grid_cap;              // rim mode: workgroups (0: kKnnRimGrid)
   int diag;                  // ablation (fe_diag bits << 12, apart from the step's): 0x4000 no ranking on the neighbour path, 0x8000 no neighbour path,
                              // 0x1000 grid built but no search, 0x2000 no grid / scan, 0x0800 no outputs
+  DoneFlag fin;              // drop-in launch: the grid's completion flag (done_flag.h)
 };
 
 struct StatsArgs {

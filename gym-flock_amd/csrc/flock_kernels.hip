@@ -1838,6 +1838,7 @@ __global__ __launch_bounds__(kThreads) void flock_knn_kernel(KnnArgs a) {
   } else {
     knn_block<K, LDS>(a, xcd_remap(blockIdx.x, gridDim.x), smem);
   }
+  signal_done(a.fin);  // the drop-in step's rim kNN: the host waits for this, not the stream
 }
 
 // get_stats (:136-143): vel_diffs_i = |v_i - mean v|, min_dists_i = sqrt(min_j r2_ij)
