@@ -188,3 +188,77 @@ def test_steps_never_wait_behind_a_stuck_collective():
     assert 1.0 < waited < 15.0, waited
     np.testing.assert_array_equal(g.result(), np.array(hist))
     v.close()
+
+
+_ABORT_MID_RUN = r"""
+import sys, time
+import numpy as np
+sys.path[:0] = [{root!r}, {pkg!r}]
+from gym_flock import _native as nat
+from gym_flock.vec import VecFlockingRelative
+from gym_flock.shard import RcclRewardGather
+B, N = 3, 32
+v = VecFlockingRelative(B, N)
+v.reset(seed=5)
+g = RcclRewardGather(v.h, 1, 0, v.h.comm_unique_id(), timeout=3.0)
+u = np.random.RandomState(5).uniform(-1, 1, size=(B, N, 2)).astype(np.float32)
+for _ in range(8):
+    v.step(u)
+g.issue()
+print("FIRST_OK", g.result().shape)
+v.h.debug_comm_gate(True, max_seconds=25.0)
+try:
+    for _ in range(4):
+        v.step(u)
+    g.issue()  # queued behind the gate: it never completes within the timeout
+    t0 = time.monotonic()
+    try:
+        g.result()
+        print("RESULT_OK")
+    except nat.GymFlockError as e:
+        print("CODE", e.code, "SECONDS", round(time.monotonic() - t0, 2))
+        print("MSG", str(e).replace("\n", " "))
+    t1 = time.monotonic()
+    for _ in range(10):  # the handle keeps stepping, its rewards stay readable
+        v.step(u)
+        r = v.rewards()
+    print("STEPS_SECONDS", round(time.monotonic() - t1, 2), "STEP_OK", bool(np.isfinite(r[0]).all()))
+    try:
+        g.issue()
+        print("REISSUE_OK")
+    except nat.GymFlockError as e:
+        print("REISSUE", e.code, str(e).replace("\n", " "))
+finally:
+    v.h.debug_comm_gate(False)
+v.sync()
+v.close()
+print("DONE")
+"""
+
+
+def test_collective_timeout_aborts_mid_run():
+    """The mid-run abort path (comm_event_wait): a reward gather whose collective never
+    completes (queued behind the gate kernel on the side stream, as behind a dead peer)
+    fails with GF_ECOMM after the collective timeout (3 s here), the communicator is
+    aborted on the process's communicator worker, the handle keeps stepping with its
+    rewards readable, and the metrics path then reports why it is gone (GF_ESTATE). In a
+    child process (a fresh HIP context; the gate is released before it exits)."""
+    code = _ABORT_MID_RUN.format(root=ROOT, pkg=os.path.join(ROOT, "gym-flock_amd"))
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=120)
+    wall = time.monotonic() - t0
+    out = p.stdout.decode(errors="replace") + p.stderr.decode(errors="replace")
+    assert p.returncode == 0, out
+    fields = {}
+    for line in p.stdout.decode().splitlines():
+        k, _, rest = line.partition(" ")
+        fields[k] = rest
+    assert "FIRST_OK" in fields and "DONE" in fields, out
+    code_s, _, secs = fields["CODE"].partition(" SECONDS ")
+    assert int(code_s) == nat.GF_ECOMM, out
+    assert 2.5 < float(secs) < 15.0, out
+    assert "aborted" in fields["MSG"], out
+    steps_s, _, ok = fields["STEPS_SECONDS"].partition(" STEP_OK ")
+    assert ok == "True" and float(steps_s) < 5.0, out
+    assert fields["REISSUE"].split()[0] == str(nat.GF_ESTATE), out
+    print("collective timed out after %s s, communicator aborted (child wall %.1f s)" % (secs, wall))
