@@ -77,6 +77,18 @@ static void validation_paths() {
   CHECK(cov_create(&cc, &ch) != 0);
   CHECK(cov_destroy(nullptr) == 0);
   CHECK(gu_create(0, nullptr) != 0);
+  // round-5 entry points: null handles fail, the host-only query fills what it is given
+  CHECK(fe_set_params(nullptr, nullptr) != 0);
+  CHECK(fe_step_host(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0) != 0);
+  CHECK(fe_step_host_knn_ctrl(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0) != 0);
+  CHECK(cov_set_rng(nullptr, nullptr, nullptr) != 0);
+  CHECK(cov_get_rng(nullptr, nullptr, nullptr) != 0);
+  CHECK(cov_step_host(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, 0) != 0);
+  int32_t rt = -1, drv = -1, nccl = -1;
+  char hp[512], rp[512];
+  CHECK(fe_runtime_info(nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0) == 0);
+  CHECK(fe_runtime_info(&rt, &drv, &nccl, hp, sizeof hp, rp, sizeof rp) == 0 && rt > 0 && nccl > 0);
 }
 
 static bool have_device() {
@@ -145,6 +157,44 @@ static void flocking_session() {
   CHECK(fe_device_buffers(h, &bufs) == 0 && bufs.x != nullptr);
   CHECK(fe_sync(h) == 0);
   CHECK(fe_destroy(h) == 0);
+  // the one-call drop-in step of one env: pageable destinations (copies after the launch,
+  // the stream waited for) and page-locked ones (written by the kernel, its completion
+  // flag waited for), with the fused controller and the 7 nearest; then a parameter change
+  c = flock_cfg(N, 1, K);
+  CHECK(fe_create(&c, &h) == 0);
+  if (!h) return;
+  CHECK(fe_reset_synthetic(h, 12, 5.0) == 0);
+  std::vector<float> sv1((size_t)N * 6), net1((size_t)N * N), kobs((size_t)N * 4 * K);
+  std::vector<double> r1(1), c1((size_t)N * 2);
+  std::vector<int32_t> kidx((size_t)N * K);
+  CHECK(fe_step_host(h, u.data(), sv1.data(), net1.data(), r1.data(), c1.data(), 0) == 0);
+  CHECK(fe_step_host_knn_ctrl(h, u.data(), sv1.data(), net1.data(), r1.data(), c1.data(), kidx.data(), kobs.data(),
+                              0) == 0);
+  void* pin = nullptr;
+  const size_t nsv = (size_t)N * 6 * 4, nnet = (size_t)N * N * 4, nk = (size_t)N * K * 4;
+  const size_t bytes = nsv + nnet + 8 + (size_t)N * 16 + nk + 4 * nk;
+  CHECK(fe_host_alloc(bytes, &pin) == 0);
+  if (pin) {
+    unsigned char* b = static_cast<unsigned char*>(pin);
+    float* psv = reinterpret_cast<float*>(b);
+    float* pnet = reinterpret_cast<float*>(b + nsv);
+    double* pr = reinterpret_cast<double*>(b + nsv + nnet);
+    double* pc = reinterpret_cast<double*>(b + nsv + nnet + 8);
+    int32_t* pidx = reinterpret_cast<int32_t*>(b + nsv + nnet + 8 + (size_t)N * 16);
+    float* pobs = reinterpret_cast<float*>(b + nsv + nnet + 8 + (size_t)N * 16 + nk);
+    for (int s = 0; s < 3; ++s) {
+      CHECK(fe_step_host(h, u.data(), psv, pnet, pr, pc, 0) == 0);
+      CHECK(fe_step_host_knn_ctrl(h, u.data(), psv, pnet, pr, pc, pidx, pobs, 0) == 0);
+    }
+    for (int i = 0; i < N * K; ++i) CHECK(pidx[i] >= 0 && pidx[i] < N);
+    fe_config c2 = c;
+    c2.comm_radius = 1.2;
+    c2.centralized = 0;
+    CHECK(fe_set_params(h, &c2) == 0);
+    CHECK(fe_step_host(h, u.data(), psv, pnet, pr, pc, 0) == 0);
+    CHECK(fe_host_free(pin) == 0);
+  }
+  CHECK(fe_destroy(h) == 0);
 }
 
 static void coverage_session() {
@@ -194,6 +244,44 @@ static void coverage_session() {
   std::vector<int32_t> cost((size_t)T * T), prev((size_t)T * T);
   CHECK(cov_get_time_matrix(h, 0, cost.data(), prev.data()) == 0);
   CHECK(cov_get_obs(h, B, nodes.data(), edges.data(), snd.data(), rcv.data(), &step) != 0);
+  // the fused greedy step drawing the fallbacks from device np_random streams
+  std::vector<uint32_t> keys((size_t)B * 624);
+  std::vector<int32_t> pos(B, 624);
+  for (size_t i = 0; i < keys.size(); ++i) keys[i] = static_cast<uint32_t>(i * 2654435761u);
+  CHECK(cov_step(h, nullptr, COV_ACTIONS_GREEDY | COV_GREEDY_RNG) != 0);  // streams not set
+  CHECK(cov_set_rng(h, keys.data(), pos.data()) == 0);
+  for (int s = 0; s < 4; ++s) CHECK(cov_step(h, nullptr, COV_ACTIONS_GREEDY | COV_GREEDY_RNG) == 0);
+  CHECK(cov_get_rng(h, keys.data(), pos.data()) == 0);
+  for (int b = 0; b < B; ++b) CHECK(pos[b] >= 0 && pos[b] <= 624);
+  // the one-call drop-in step: pageable destinations, then page-locked ones
+  std::vector<float> bn((size_t)B * M * 3), be((size_t)B * 4 * M);
+  std::vector<int32_t> bs((size_t)B * 4 * M), br((size_t)B * 4 * M), bc((size_t)B * R), bnx((size_t)B * R);
+  std::vector<int64_t> bst(B);
+  std::vector<double> brw(B);
+  std::vector<uint8_t> bd(B), bnr((size_t)B * R);
+  for (int i = 0; i < B * R; ++i) act[i] = i % 4;
+  CHECK(cov_step_host(h, act.data(), bn.data(), be.data(), bs.data(), br.data(), bst.data(), brw.data(), bd.data(),
+                      bc.data(), bnx.data(), bnr.data(), COV_NEXT_GREEDY) == 0);
+  void* pin = nullptr;
+  const size_t nb = (size_t)B * M * 3 * 4 + 3 * (size_t)B * 4 * M * 4 + 64 + (size_t)B * R * 9;
+  CHECK(fe_host_alloc(nb + 64, &pin) == 0);
+  if (pin) {
+    unsigned char* p = static_cast<unsigned char*>(pin);
+    float* pn = reinterpret_cast<float*>(p);
+    float* pe = pn + (size_t)B * M * 3;
+    int32_t* ps = reinterpret_cast<int32_t*>(pe + (size_t)B * 4 * M);
+    int32_t* pr = ps + (size_t)B * 4 * M;
+    int64_t* pst = reinterpret_cast<int64_t*>(pr + (size_t)B * 4 * M);
+    double* prw = reinterpret_cast<double*>(pst + B);
+    int32_t* pc = reinterpret_cast<int32_t*>(prw + B);
+    int32_t* pnx = pc + (size_t)B * R;
+    uint8_t* pd = reinterpret_cast<uint8_t*>(pnx + (size_t)B * R);
+    uint8_t* pnr = pd + B;
+    for (int s = 0; s < 3; ++s)
+      CHECK(cov_step_host(h, act.data(), pn, pe, ps, pr, pst, prw, pd, pc, pnx, pnr, COV_NEXT_GREEDY) == 0);
+    for (int i = 0; i < B * R; ++i) CHECK(pnx[i] >= 0 && pnx[i] < 4);
+    CHECK(fe_host_free(pin) == 0);
+  }
   CHECK(cov_sync(h) == 0);
   CHECK(cov_destroy(h) == 0);
 }
