@@ -129,7 +129,7 @@ struct fe_handle {
   // waits for that copy on the host, bounded by comm_timeout (next_reward_slot); normally
   // the copy finished long before (the slot was written kRewardSlots steps ago).
   double* gsend = nullptr;              // kRewardSlots x max_envs: the gathered steps, padded
-  std::string comm_lost;                // why a step call tore the metrics path down
+  std::string comm_lost;                // why the metrics path was torn down (a timed-out wait)
   double* gather = nullptr;             // nranks x kRewardSlots x max_envs
   hipEvent_t step_ev = nullptr;
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
@@ -1667,8 +1667,10 @@ int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what) {
     const bool err = st != ncclSuccess && st != ncclInProgress;
     if (err || Clock::now() > deadline) {
       comm_release(h, true);
-      if (err) return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(st));
-      return fail(GF_ECOMM, std::string(what) + ": timed out (a rank stopped responding); communicator aborted");
+      h->comm_lost = std::string(what) + ": " +
+                     (err ? std::string(ncclGetErrorString(st)) : std::string("timed out (a rank stopped responding)")) +
+                     "; communicator aborted";
+      return fail(GF_ECOMM, h->comm_lost);
     }
     if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
@@ -1679,7 +1681,8 @@ int comm_enqueued(fe_handle* h, ncclResult_t r, const char* what) {
   if (r == ncclInProgress) return comm_wait(h, deadline_in(h->comm_timeout), what);
   if (r != ncclSuccess) {
     comm_release(h, true);
-    return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(r));
+    h->comm_lost = std::string(what) + ": " + ncclGetErrorString(r) + "; communicator aborted";
+    return fail(GF_ECOMM, h->comm_lost);
   }
   return GF_OK;
 }
@@ -1992,13 +1995,13 @@ extern "C" {
 
 int fe_debug_comm_gate(fe_handle* h, int close, double max_seconds) {
   if (!h) return fail(GF_EINVAL, "null handle");
-  if (!h->comm || !h->comm_stream) return fail(GF_ESTATE, "no communicator (fe_comm_init first)");
   unsigned* f = gate_flag();
   if (!f) return fail(GF_ENOMEM, "gate flag: hipHostMalloc failed");
-  if (!close) {
+  if (!close) {  // also after the communicator was aborted (its side stream abandoned)
     __atomic_store_n(f, 1u, __ATOMIC_SEQ_CST);
     return GF_OK;
   }
+  if (!h->comm || !h->comm_stream) return fail(GF_ESTATE, "no communicator (fe_comm_init first)");
   if (!(max_seconds > 0) || max_seconds > 120) return fail(GF_EINVAL, "max_seconds must be in (0, 120]");
   GF_HIP(hipSetDevice(h->cfg.device));
   int khz = 0;

@@ -261,4 +261,5 @@ def test_collective_timeout_aborts_mid_run():
     steps_s, _, ok = fields["STEPS_SECONDS"].partition(" STEP_OK ")
     assert ok == "True" and float(steps_s) < 5.0, out
     assert fields["REISSUE"].split()[0] == str(nat.GF_ESTATE), out
+    assert "timed out" in fields["REISSUE"], out  # the reason the metrics path is gone
     print("collective timed out after %s s, communicator aborted (child wall %.1f s)" % (secs, wall))
