@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 
@@ -97,6 +98,28 @@ int main() {
     CK(hipStreamSynchronize(s));
     const double all = 1e6 * std::chrono::duration<double>(clk::now() - t0).count() / iters;
     std::printf("enqueue     rep %d: %.2f us host per launch, %.2f us per launch with the drain\n", rep, enq, all);
+  }
+  // two streams: one thread enqueueing to both alternately, then two threads, one per stream
+  hipStream_t s2;
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  for (int rep = 0; rep < 2; ++rep) {
+    auto t0 = clk::now();
+    for (int it = 0; it < iters; ++it) {
+      hipLaunchKernelGGL(work, dim3(1), dim3(256), 0, s, d, hd, 64, nullptr, 0);
+      hipLaunchKernelGGL(work, dim3(1), dim3(256), 0, s2, d + 64, hd + 64, 64, nullptr, 0);
+    }
+    const double one = 1e6 * std::chrono::duration<double>(clk::now() - t0).count() / iters;
+    CK(hipDeviceSynchronize());
+    t0 = clk::now();
+    std::thread other([&] {
+      for (int it = 0; it < iters; ++it) hipLaunchKernelGGL(work, dim3(1), dim3(256), 0, s2, d + 64, hd + 64, 64, nullptr, 0);
+    });
+    for (int it = 0; it < iters; ++it) hipLaunchKernelGGL(work, dim3(1), dim3(256), 0, s, d, hd, 64, nullptr, 0);
+    other.join();
+    const double two = 1e6 * std::chrono::duration<double>(clk::now() - t0).count() / iters;
+    CK(hipDeviceSynchronize());
+    std::printf("2 streams   rep %d: %.2f us host per launch pair from one thread, %.2f us from two threads\n", rep,
+                one, two);
   }
   return 0;
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A round-5 measurement set in one GPU session: the GPU suite, smoke, the default bench line
-# (driver window and 200 steps), the Coverage workload (with the greedy expert), a rocprofv3
+# (driver window and 200 steps), the Coverage workload (with the greedy expert), the
+# multi-rank path at one rank (--force-dist: the RCCL reward and stats gathers), a rocprofv3
 # kernel trace + stats of a 100-step bench with its per-grid kernel stats and step periods
 # (scripts/trace_by_grid.py), and PMC HBM traffic (FETCH_SIZE and WRITE_SIZE passes) of every
 # bench sub-line's kernel (summarised here by scripts/pmc_all.sh).
@@ -20,6 +21,8 @@ timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench200.json 2> $O/ben
 echo "bench200 ok"
 timeout -k 10 300 python bench.py --workload coverage --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_cov.json 2> $O/bench_cov.err || { tail $O/bench_cov.err; exit 1; }
 echo "bench_cov ok"
+timeout -k 10 400 python bench.py --force-dist --steps 20 --warmup 5 --no-cpu-baseline --no-other-configs > $O/bench_forcedist.json 2> $O/bench_forcedist.err || { tail $O/bench_forcedist.err; exit 1; }
+echo "bench_forcedist ok"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o trace -- python3 $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $O/rocprof_trace.log 2>&1 || { tail $O/rocprof_trace.log; exit 1; }
 cd $R
