@@ -66,6 +66,9 @@ def cpu_model():
     return "unknown"
 
 
+REWARM_STEPS = 512  # multi-rank runs: steps (with gathers) between RCCL init and the timed loop
+
+
 def clock_warmup(step, sync, ms):
     """Steps until `ms` of wall time have passed, synchronising every 8 steps, so the
     GPU's clocks have left their idle state before anything is timed.
@@ -920,6 +923,19 @@ def main():
         if gather is not None and (s + 1) % args.metrics_every == 0:
             gather.issue()  # every step since the previous issue, in one collective
             ungathered[0] = 0
+    if gather is not None:
+        # RCCL's initialisation leaves the GPU idle long enough for its clocks to drop back
+        # (the timed window then ran ~20 % slower at one rank, profiles/r05/forcedist_rewarm.txt):
+        # step again, gathering as the timed loop does, a fixed count on every rank (the
+        # collectives must match), then restore the synthetic init
+        for s in range(REWARM_STEPS):
+            plain(s)
+        if ungathered[0]:  # the next gather must not span more than the ring's 64 steps
+            gather.issue()
+            ungathered[0] = 0
+        env.sync()
+        env.set_state(x_init)
+        warm["steps_after_comm_init"] = REWARM_STEPS
     for s in range(W):
         plain(s)
     per_rank = []
