@@ -335,6 +335,7 @@ def bench_config4(args, with_greedy=False):
                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("coverage_r200x512"),
                         "kernel": "cov_step_kernel",
                         "region_ms_per_step": kernel_ms, "algorithmic_bytes_per_step": B * per_env,
+                        "launches_per_step": 1,
                         "note": "latency-limited, not bandwidth-limited: one workgroup per env, two dependent "
                                 "global round trips and the claim resolution per step (DESIGN.md); traffic from "
                                 "PMC with the FETCH_SIZE x2 correction, which the guide calibrates for wide "

@@ -47,7 +47,9 @@ struct cov_handle {
   // makes `stream` wait for `stream2`.
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_s2 = nullptr, ev_main = nullptr;
-  int nsplit = 2;
+  // launches per step (cov_set_streams): 0 = auto, the greedy steps (COV_ACTIONS_GREEDY)
+  // split in two, every other step one launch; 1; 2
+  int nsplit = 0;
   bool s2_pending = false, main_dirty = true;
   bool other_work = true;  // non-step work since the last step: next step is one launch
   hipEvent_t tw[2] = {nullptr, nullptr};
@@ -508,7 +510,7 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     h->main_dirty = h->other_work = true;
     a.actions = h->actions;
   }
-  const bool split = h->nsplit > 1 && a.B >= 2 && !h->other_work;
+  const bool split = (h->nsplit == 2 || (h->nsplit == 0 && (flags & COV_ACTIONS_GREEDY))) && a.B >= 2 && !h->other_work;
   h->other_work = false;
   if (split) {
     if (h->main_dirty) {
@@ -531,8 +533,8 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
   }
   if (int rc = join_s2(h)) return rc;
   h->main_dirty = true;
-  if (h->timing && h->nsplit > 1) h->tw_steps++;  // the window counts every step
-  const bool sample = h->timing && (h->timing_count++ % h->timing_stride) == 0;
+  if (h->timing && h->nsplit != 1) h->tw_steps++;  // the window counts every step
+  const bool sample = h->timing && h->nsplit == 1 && (h->timing_count++ % h->timing_stride) == 0;
   if (sample) {
     if (h->ev_used + 2 > h->ev.size()) {
       for (int k = 0; k < 64; ++k) {
@@ -961,7 +963,7 @@ int cov_get_graphs_tuple(cov_handle* h, int32_t* n_node, float* nodes, int32_t* 
 }
 
 int cov_set_streams(cov_handle* h, int n) {
-  if (!h || (n != 1 && n != 2)) return cfail(GF_EINVAL, "n must be 1 or 2");
+  if (!h || n < 0 || n > 2) return cfail(GF_EINVAL, "n must be 0 (auto), 1 or 2");
   if (int rc = use(h)) return rc;
   h->nsplit = n;
   return GF_OK;

@@ -837,8 +837,9 @@ class CoverageHandle:
         check(self.lib.cov_sync(self.h))
 
     def set_streams(self, n):
-        """Launches per step: 2 (default) splits the env batch over two HIP streams; 1
-        keeps every step on the handle's stream (cov_set_streams)."""
+        """Launches per step (cov_set_streams): 0 (default) splits the fused greedy steps
+        over two HIP streams and launches every other step once; 2 splits every step; 1
+        keeps every step on the handle's stream."""
         check(self.lib.cov_set_streams(self.h, int(n)))
 
     def controller_greedy(self, fetch=True):

@@ -353,9 +353,11 @@ int cov_get_rewards(cov_handle* h, double* reward, uint8_t* done);   /* (B), (B)
 int cov_get_robots(cov_handle* h, int env, double* xr, int32_t* nodes); /* closest_targets :427 */
 int cov_get_visited(cov_handle* h, int env, uint8_t* visited); /* (max_nodes - R): reset()'s layout */
 int cov_get_n_motion(cov_handle* h, int32_t* n_motion);
-/* Back-to-back cov_step calls go out as two half-batch launches on two streams (as
- * fe_set_streams; cov_set_streams(h, 1) for one); every other call, cov_sync
- * included, first orders the handle's stream after both. */
+/* Launches per cov_step. n = 0 (the default): fused greedy steps (COV_ACTIONS_GREEDY) go
+ * out as two half-batch launches on two streams (as fe_set_streams), every other step as
+ * one launch, which the device, not the host, bounds (scripts/cov_launch_probe.py); n = 2
+ * splits every step, n = 1 none. Every other call, cov_sync included, first orders the
+ * handle's stream after both. */
 int cov_sync(cov_handle* h);
 int cov_set_streams(cov_handle* h, int n);
 /* Greedy expert, controller(greedy=True) :800-872. On first use after cov_set_targets

@@ -31,7 +31,7 @@ def main():
     v.h.controller_greedy(fetch=False)
     v.sync()
     out = {"time_matrix_ms": 1e3 * (time.perf_counter() - t0), "n_targets": len(targets)}
-    streams = int(os.environ.get("STREAMS", "2"))
+    streams = int(os.environ.get("STREAMS", "0"))
     v.h.set_streams(streams)
     out["streams"] = streams
 

@@ -27,7 +27,7 @@ def main():
     v.set_actions(np.random.RandomState(7).randint(0, 4, size=(B, R)))
     step = v.h._step_resident
     out = {}
-    for streams in (2, 1, 2, 1):
+    for streams in (2, 1) * int(os.environ.get("REPS", "2")):
         v.h.set_streams(streams)
         for _ in range(2000):  # clocks up
             step()
