@@ -1275,3 +1275,36 @@ def test_allgather_stats_one_rank_equals_local_summary():
     h.step(u, 0)  # a new summary waits for the pending gather before overwriting its source
     h.allgather_stats()
     np.testing.assert_array_equal(h.gathered_stats()[0], h.stats_summary())
+
+
+@pytest.mark.parametrize("n", [100, 300])
+def test_step_host_flag_and_stream_waits_agree(n):
+    """fe_step_host_knn_ctrl into page-locked destinations (written by the kernels in place;
+    the host waits for the last kernel's completion flag: the step's at N=100, the rim
+    kNN's at N=300) and into pageable numpy arrays (copies after the launches; the host
+    waits for the stream), on two handles from the same state and actions: every output
+    equal at each of 30 steps, and the first step's against the oracle."""
+    B, K = 1, 7
+    hs = [nat.FlockHandle(n, B, n_neighbors=K) for _ in range(2)]
+    x0 = synthetic_batch(B, n, seed0=21)
+    for h in hs:
+        h.set_state(x0)
+    pool = nat.host_pool()
+    shapes = dict(sv=((B, n, 6), np.float32), net=((B, n, n), np.float32), rew=((B,), np.float64),
+                  ctrl=((B, n, 2), np.float64), idx=((B, n, K), np.int32), obs=((B, n, 4 * K), np.float32))
+    pinned = {k: pool.array(*v) for k, v in shapes.items()}
+    plain = {k: np.empty(*v) for k, v in shapes.items()}
+    rs = np.random.RandomState(3)
+    for t in range(30):
+        u = rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
+        for h, o in ((hs[0], pinned), (hs[1], plain)):
+            h.step_host_knn(u.ctypes.data, False, o["sv"].ctypes.data, o["net"].ctypes.data, o["rew"].ctypes.data,
+                            o["idx"].ctypes.data, o["obs"].ctypes.data, ctrl=o["ctrl"].ctypes.data)
+        for k in shapes:
+            np.testing.assert_array_equal(pinned[k], plain[k], err_msg="%s at step %d" % (k, t))
+        if t == 0:
+            want = orc.step(x0[0], u[0])
+            np.testing.assert_array_equal(pinned["net"][0], np.asarray(want["network"], np.float32))
+            np.testing.assert_array_equal(pinned["idx"][0], orc.knn_observation(want["x"], K)[0])
+    for h in hs:
+        h.close()
