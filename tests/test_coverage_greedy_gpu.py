@@ -551,3 +551,51 @@ def test_device_rng_argument_checks():
     with pytest.raises(nat.GymFlockError, match="624"):
         h.set_rng([np.random.RandomState(1)])
     h.close()
+
+
+def test_device_rng_config4_batch_sampled_vs_oracle():
+    """The bench's config-4 shape (R=200, the map of seed 8, max_nodes 1000) at 64 envs: a
+    whole episode (75 steps, EPISODE_LENGTH) of VecCoverage.step(greedy=True) with the
+    fallback draws on the device, every env stepping in the same two half-batch launches;
+    envs 0, 31 and 63 checked against the oracle's expert with their own RandomStates at
+    every step (actions, nodes, rewards and done flags), and their streams at the end."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    R, B, M = 200, 64, 1000
+    np.random.seed(8)
+    targets = generate_targets()
+    T = len(targets)
+    v = VecCoverage(B, R, max_nodes=M)
+    v.set_targets(targets)
+    start, visited = v.reset(seed=0)
+    o0 = oc.CoverageOracle(targets, R, M)
+    cost, prev = oc.time_matrix(T, o0.motion[0] - R, o0.motion[1] - R)
+    picks = (0, 31, 63)
+    orcs, rngs = {}, {}
+    for b in picks:
+        o = oc.CoverageOracle(targets, R, M)
+        o.reset(start[b], np.nonzero(visited[b, :T] == 0)[0] + R)
+        orcs[b] = o
+        rngs[b] = _reset_stream(b, T, R)
+    draws = 0
+    for t in range(75):
+        v.step(greedy=True)
+        ga, gr = v.h.actions()
+        r, d = v.rewards()
+        for b in picks:
+            o = orcs[b]
+            cur = o.closest()
+            ea, er = oc.greedy_actions(cost, prev, cur, o.visited[R:], oc.action_receivers(cur, o.nbr, o.cnt, R), R)
+            k = np.nonzero(er)[0]
+            ea[k] = rngs[b].choice(4, size=len(k))
+            draws += len(k)
+            np.testing.assert_array_equal(gr[b], er, err_msg="env %d step %d" % (b, t))
+            np.testing.assert_array_equal(ga[b], ea, err_msg="env %d step %d" % (b, t))
+            _, rr, dd = o.step(ea)
+            assert r[b] == rr and d[b] == dd, (b, t)
+            np.testing.assert_array_equal(v.h.robots(b)[1], o.closest())
+    assert draws > 624  # the sampled streams pass a key regeneration
+    for b in picks:
+        st, want = v.np_random(b).get_state(), rngs[b].get_state()
+        assert st[2] == want[2]
+        np.testing.assert_array_equal(st[1], want[1])
+    v.close()
