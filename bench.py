@@ -603,7 +603,16 @@ def bench_greedy(v, targets, R, M, B, K, args):
         fa_t += time.perf_counter() - t0
         fa_k += 75
     del state
+    # an episode's reset for all envs: its random draws on the device (the default), and
+    # the same draws by RandomState loops on the host (bit-identical, tests)
+    t0 = time.perf_counter()
+    v.reset(seed=500)
+    reset_dev = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    v.reset(seed=500, draws="host")
+    reset_host = time.perf_counter() - t0
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
+           "reset_ms_all_envs": 1e3 * reset_dev, "reset_ms_all_envs_host_draws": 1e3 * reset_host,
            "expert_step_ms_in_episodes": 1e3 * ep_t / ep_k,
            "expert_robot_steps_per_s_in_episodes": R * B * ep_k / ep_t,
            "expert_step_ms_in_episodes_fallback_action0": 1e3 * z_t / ep_k,

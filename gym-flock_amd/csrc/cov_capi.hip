@@ -424,6 +424,34 @@ int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited) {
   return GF_OK;
 }
 
+int cov_reset_seeded(cov_handle* h, uint64_t seed, double frac_active, int32_t* start_out, uint8_t* visited_out) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (!h->has_graph) return cfail(GF_ESTATE, "set the target graph of every env first (cov_set_targets)");
+  const size_t B = h->cfg.n_envs, R = h->cfg.n_robots, Tm = h->a.Tmax;
+  if (seed + B > 0x100000000ull) return cfail(GF_EINVAL, "seed + n_envs must fit in 32 bits (RandomState seeds)");
+  if (!(frac_active >= 0.0 && frac_active <= 1.0)) return cfail(GF_EINVAL, "frac_active must be in [0, 1]");
+  if (int rc = use(h)) return rc;
+  if (!h->mt_key) {
+    int rc;
+    if ((rc = calloc_dev(&h->mt_key, B * gf::kMtN)) || (rc = calloc_dev(&h->mt_pos, B))) return rc;
+  }
+  gf::CovArgs a = h->a;
+  a.mt_key = h->mt_key;
+  a.mt_pos = h->mt_pos;
+  hipError_t e = gf::launch_cov_seed_reset(a, static_cast<uint32_t>(seed), frac_active, h->start, h->visited0, h->stream);
+  if (e == hipSuccess) e = gf::launch_cov_reset(h->a, h->start, h->visited0, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_reset_seeded: ") + hipGetErrorString(e));
+  a = h->a;
+  a.actions = nullptr;
+  e = gf::launch_cov_step(a, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_kernel: ") + hipGetErrorString(e));
+  if (start_out) CV_HIP(hipMemcpyAsync(start_out, h->start, B * R * 4, hipMemcpyDeviceToHost, h->stream));
+  if (visited_out) CV_HIP(hipMemcpyAsync(visited_out, h->visited0, B * Tm, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
+  h->has_state = true;
+  return GF_OK;
+}
+
 int cov_set_actions(cov_handle* h, const int32_t* actions) {
   if (!h || !actions) return cfail(GF_EINVAL, "null argument");
   if (int rc = use(h)) return rc;

@@ -294,6 +294,10 @@ hipError_t launch_cov_graphs(const CovArgs& a, const int64_t* off, bool mask_all
                              int32_t* rcv, hipStream_t s);
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s);
 hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_t* visited0, hipStream_t s);
+// reset()'s random draws on the device for envs seeded seed0 + b (start (B,R), visited0
+// (B,Tmax)), the streams left in a.mt_key / a.mt_pos
+hipError_t launch_cov_seed_reset(const CovArgs& a, uint32_t seed0, double frac, int32_t* start, uint8_t* visited0,
+                                 hipStream_t s);
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s);
 // the step with a.actions read from `u` (host memory, copied into the kernel arguments;
 // B * R * 4 <= kCovUInlineBytes)

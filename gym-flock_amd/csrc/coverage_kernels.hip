@@ -716,6 +716,74 @@ __global__ __launch_bounds__(kCovThreads) void cov_reset_kernel(CovArgs a, const
   }
 }
 
+// reset()'s draws (coverage.py:405-424) for env b as a reference env whose np_random was
+// seeded seed0 + b: RandomState(seed) (mt19937_seed: the generator's init_genrand), then
+// choice(arange(T), R, replace=False) for the start targets and choice(arange(T) + R,
+// int(T * frac), replace=False) for the unvisited ones, each numpy's legacy permutation of
+// the stream (Fisher-Yates from the top, random_interval's masked rejection: oracle/
+// mt19937.py). The stream is left in mt_key / mt_pos for the fallback draws
+// (COV_GREEDY_RNG). One wave per env: the draws and swaps form one chain, which every lane
+// runs (lane 0 swaps); the key regenerations take the whole wave.
+__global__ __launch_bounds__(64) void cov_seed_reset_kernel(CovArgs a, uint32_t seed0, double frac, int32_t* start,
+                                                            uint8_t* visited0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* key = reinterpret_cast<uint32_t*>(smem);
+  int32_t* perm = reinterpret_cast<int32_t*>(key + kMtN);
+  uint8_t* vis = reinterpret_cast<uint8_t*>(perm + a.Tmax);
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int R = a.R, Tm = a.Tmax, T = a.ntg[b];
+  if (lane == 0) {
+    uint32_t s = seed0 + static_cast<uint32_t>(b);
+    for (int p = 0; p < kMtN; ++p) {
+      key[p] = s;
+      s = 1812433253u * (s ^ (s >> 30)) + static_cast<uint32_t>(p + 1);
+    }
+  }
+  __syncthreads();
+  int pos = kMtN;  // wave-uniform
+  auto next = [&]() {
+    if (pos == kMtN) {
+      mt_regen<64>(key);
+      pos = 0;
+    }
+    return mt_temper(key[pos++]);
+  };
+  auto permute = [&](int n) {  // RandomState.permutation(n) into perm[0, n)
+    for (int k = lane; k < n; k += 64) perm[k] = k;
+    __syncthreads();
+    for (int i = n - 1; i >= 1; --i) {
+      uint32_t mask = static_cast<uint32_t>(i);
+      mask |= mask >> 1;
+      mask |= mask >> 2;
+      mask |= mask >> 4;
+      mask |= mask >> 8;
+      mask |= mask >> 16;
+      uint32_t v;
+      do {
+        v = next() & mask;
+      } while (v > static_cast<uint32_t>(i));
+      if (lane == 0) {  // one lane: its LDS reads and writes stay in program order
+        const int t = perm[i];
+        perm[i] = perm[v];
+        perm[v] = t;
+      }
+    }
+    __syncthreads();
+  };
+  permute(T);
+  for (int k = lane; k < R; k += 64) start[(size_t)b * R + k] = perm[k];
+  __syncthreads();
+  permute(T);
+  const int kdrop = static_cast<int>(static_cast<double>(T) * frac);  // Python's int(T * frac)
+  for (int t = lane; t < Tm; t += 64) vis[t] = 1;
+  __syncthreads();
+  for (int k = lane; k < kdrop; k += 64) vis[perm[k]] = 0;
+  __syncthreads();
+  for (int t = lane; t < Tm; t += 64) visited0[(size_t)b * Tm + t] = vis[t];
+  for (int k = lane; k < kMtN; k += 64) a.mt_key[(size_t)b * kMtN + k] = key[k];
+  if (lane == 0) a.mt_pos[b] = pos;
+}
+
 // FlattenDictWrapper order (reference test.py:33, keys coverage.py:90): nodes (M,3),
 // edges (4M,1), senders (4M), receivers (4M), step (1,1), concatenated per env. The
 // wrapper's np.concatenate promotes to float64; every value here is exact in float32
@@ -802,6 +870,13 @@ size_t cov_step_lds_bytes(int R, int M) {
 
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {
   hipLaunchKernelGGL(cov_graph_kernel, dim3(n), dim3(kCovThreads), 0, s, a, envs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_cov_seed_reset(const CovArgs& a, uint32_t seed0, double frac, int32_t* start, uint8_t* visited0,
+                                 hipStream_t s) {
+  const size_t lds = (size_t)kMtN * 4 + (size_t)a.Tmax * 5;
+  hipLaunchKernelGGL(cov_seed_reset_kernel, dim3(a.B), dim3(64), lds, s, a, seed0, frac, start, visited0);
   return hipGetLastError();
 }
 

@@ -133,6 +133,7 @@ SIGNATURES = {
     "cov_destroy": [_P],
     "cov_set_targets": [_P, _I, _I, _P],
     "cov_reset": [_P, _P, _P],
+    "cov_reset_seeded": [_P, ctypes.c_uint64, ctypes.c_double, _P, _P],
     "cov_step": [_P, _P, _I],
     "cov_set_actions": [_P, _P],
     "cov_set_rng": [_P, _P, _P],
@@ -738,6 +739,17 @@ class CoverageHandle:
         assert st.shape == (self.n_envs, self.n_robots), st.shape
         assert vi.shape == (self.n_envs, self.t_max), vi.shape
         check(self.lib.cov_reset(self.h, ptr(st), ptr(vi)))
+
+    def reset_seeded(self, seed, frac_active=0.5, fetch=True):
+        """reset() with its random draws on the device (cov_reset_seeded): env b draws from
+        RandomState(seed + b) as the reference's reset does; the streams stay on the device
+        for the greedy expert's fallback draws. Returns (start (B,R), visited (B,t_max)) or,
+        with fetch=False, None."""
+        st = np.empty((self.n_envs, self.n_robots), np.int32) if fetch else None
+        vi = np.empty((self.n_envs, self.t_max), np.uint8) if fetch else None
+        check(self.lib.cov_reset_seeded(self.h, int(seed), float(frac_active), ptr(st) if fetch else None,
+                                        ptr(vi) if fetch else None))
+        return (st, vi) if fetch else None
 
     def step(self, actions=None, resident=False, greedy=False, rng=False):
         """actions (B,R) host ints; or resident=True (the last set/greedy actions); or

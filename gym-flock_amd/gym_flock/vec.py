@@ -156,10 +156,15 @@ class VecCoverage:
         else:
             self.n_targets[env] = len(targets)
 
-    def reset(self, seed=0):
+    def reset(self, seed=0, draws="device"):
         """Env b is a reference env whose np_random was seeded seed + env_offset + b: its
-        reset draws here, and its stream then continues on the device for the greedy
-        expert's fallback draws (step(greedy=True)); np_random(b) reads it back."""
+        reset draws (coverage.py:405-424), then its stream continues on the device for the
+        greedy expert's fallback draws (step(greedy=True)); np_random(b) reads it back.
+        draws="device" (cov_reset_seeded): the draws run on the device, one wave per env;
+        "host": RandomState loops here (~0.5 ms per env), then cov_reset and cov_set_rng.
+        Both return (start (B,R) target-local, visited (B, max_nodes-R)), bit-identical."""
+        if draws == "device":
+            return self.h.reset_seeded(seed + self.env_offset, self.frac)
         R, tmax = self.n_robots, self.h.t_max
         start = np.empty((self.n_envs, R), np.int32)
         visited = np.ones((self.n_envs, tmax), np.uint8)

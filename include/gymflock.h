@@ -317,6 +317,13 @@ int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets
 /* reset() after its random draws (:405-424): start[B][R] target-local start nodes,
  * visited[B][max_nodes-R] (1 = visited); computes reset's observation (:424). */
 int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited);
+/* reset() with its random draws on the device (:405-424): env b as a reference env whose
+ * np_random was seeded seed + b, RandomState(seed + b)'s choice(arange(T), R,
+ * replace=False) for the start targets and choice(arange(T) + R, int(T * frac_active),
+ * replace=False) for the unvisited ones, bit-exact; the envs' streams then continue on the
+ * device for COV_GREEDY_RNG (as after cov_set_rng). start_out (B,R) and visited_out
+ * (B, max_nodes - R) may be NULL; otherwise they receive the draws, in cov_reset's layout. */
+int cov_reset_seeded(cov_handle* h, uint64_t seed, double frac_active, int32_t* start_out, uint8_t* visited_out);
 /* step(action) (:174-204, :234-364): actions[B][R] in [0,4). */
 int cov_step(cov_handle* h, const int32_t* actions, int flags);
 int cov_set_actions(cov_handle* h, const int32_t* actions);

@@ -10,7 +10,11 @@ mt_regen / mt_temper): choice(4) with uniform p is randint(0, 4), one tempered 3
 output masked to 2 bits (no rejection: the mask equals the range); the 624-word key is
 regenerated when the position reaches 624. Pinned against numpy.random.RandomState
 itself (tests/test_oracle_mt19937.py), whose state layout (get_state: key words and
-position) is also the C-ABI's (cov_set_rng).
+position) is also the C-ABI's (cov_set_rng). Also restated: RandomState(seed)'s seeding
+(mt19937_seed, the generator's init_genrand) and the legacy permutation / choice without
+replacement (Fisher-Yates from the top, random_interval's masked rejection), which
+VecCoverage.reset's draws (coverage.py:405-424) use and the device reset
+(cov_reset_seeded) restates.
 """
 N, M = 624, 397
 UPPER, LOWER, MATRIX_A = 0x80000000, 0x7FFFFFFF, 0x9908B0DF
@@ -43,3 +47,39 @@ def choice4(key, pos, n):
         out.append(temper(key[pos]) & 3)
         pos += 1
     return out, key, pos
+
+
+def seed(s):
+    """RandomState(s)'s state for an integer seed in [0, 2**32): (key, pos = 624)."""
+    key = [0] * N
+    s &= 0xFFFFFFFF
+    for p in range(N):
+        key[p] = s
+        s = (1812433253 * (s ^ (s >> 30)) + p + 1) & 0xFFFFFFFF
+    return key, N
+
+
+def _next(state):
+    key, pos = state
+    if pos == N:
+        regenerate(key)
+        pos = 0
+    state[1] = pos + 1
+    return temper(key[pos])
+
+
+def permutation(key, pos, n):
+    """RandomState.permutation(n) from the stream (key, pos): (perm, key, pos).
+    choice(a, size, replace=False) is a[permutation(len(a))[:size]]."""
+    state = [[int(k) for k in key], pos]
+    x = list(range(n))
+    for i in range(n - 1, 0, -1):
+        mask = i
+        for sh in (1, 2, 4, 8, 16):
+            mask |= mask >> sh
+        while True:
+            v = _next(state) & mask
+            if v <= i:
+                break
+        x[i], x[v] = x[v], x[i]
+    return x, state[0], state[1]

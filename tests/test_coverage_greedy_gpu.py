@@ -599,3 +599,44 @@ def test_device_rng_config4_batch_sampled_vs_oracle():
         assert st[2] == want[2]
         np.testing.assert_array_equal(st[1], want[1])
     v.close()
+
+
+@pytest.mark.parametrize("R", [6, 200])
+def test_device_reset_draws_equal_host_draws(R):
+    """VecCoverage.reset on the device (cov_reset_seeded: RandomState(seed + b)'s two
+    choices without replacement, one wave per env) against the host draws (RandomState
+    loops, cov_reset + cov_set_rng): starts, visited flags, the observations reset()
+    returns and the envs' streams equal, for envs with different maps (target counts), and
+    the first greedy steps after it take the same actions."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    B, M = 5, 1000
+    maps = []
+    for b in range(B):
+        np.random.seed(600 + b)
+        maps.append(generate_targets())
+    vs = [VecCoverage(B, R, max_nodes=M, env_offset=3) for _ in range(2)]
+    for v in vs:
+        for b in range(B):
+            v.set_targets(maps[b], env=b)
+    sd, vd = vs[0].reset(seed=77)
+    sh, vh = vs[1].reset(seed=77, draws="host")
+    np.testing.assert_array_equal(sd, sh)
+    np.testing.assert_array_equal(vd, vh)
+    kd, pd = vs[0].h.get_rng()
+    kh, ph = vs[1].h.get_rng()
+    np.testing.assert_array_equal(kd, kh)
+    np.testing.assert_array_equal(pd, ph)
+    for b in range(B):
+        od, oh = vs[0].obs(b), vs[1].obs(b)
+        for k in od:
+            np.testing.assert_array_equal(od[k], oh[k])
+    for t in range(10):
+        for v in vs:
+            v.step(greedy=True)
+        np.testing.assert_array_equal(vs[0].h.actions()[0], vs[1].h.actions()[0])
+    # and the host RandomState of env 2 (seed 77 + 3 + 2) matches the device stream after reset
+    rs = np.random.RandomState(77 + 3 + 2)
+    T = len(maps[2])
+    np.testing.assert_array_equal(sd[2], rs.choice(np.arange(T), size=(R,), replace=False))
+    for v in vs:
+        v.close()

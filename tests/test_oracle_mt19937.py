@@ -39,3 +39,29 @@ def test_reset_draws_then_fallbacks():
     _, key, pos, _, _ = rs.get_state()
     got, _, _ = mt.choice4(key, pos, 50)
     assert got == [rs.choice(4) for _ in range(50)]
+
+
+@pytest.mark.parametrize("s", [0, 1, 40, 2 ** 32 - 1])
+def test_seed_matches_randomstate(s):
+    key, pos = mt.seed(s)
+    st = np.random.RandomState(s).get_state()
+    np.testing.assert_array_equal(np.array(key, np.uint32), st[1])
+    assert pos == st[2]
+
+
+@pytest.mark.parametrize("s,n", [(0, 552), (7, 1), (7, 2), (13, 90), (40, 1000)])
+def test_permutation_and_choice_without_replacement(s, n):
+    """The reset's draws: two choices without replacement from one stream
+    (VecCoverage.reset, coverage.py:405-424), then the stream state."""
+    rs = np.random.RandomState(s)
+    key, pos = mt.seed(s)
+    r = max(1, n // 3)
+    want1 = rs.choice(np.arange(n), size=(r,), replace=False)
+    want2 = rs.choice(np.arange(n) + 5, size=(int(n * 0.5),), replace=False)
+    p1, key, pos = mt.permutation(key, pos, n)
+    p2, key, pos = mt.permutation(key, pos, n)
+    np.testing.assert_array_equal(np.array(p1[:r]), want1)
+    np.testing.assert_array_equal(np.array(p2[:int(n * 0.5)]) + 5, want2)
+    st = rs.get_state()
+    assert pos == st[2]
+    np.testing.assert_array_equal(np.array(key, np.uint32), st[1])
