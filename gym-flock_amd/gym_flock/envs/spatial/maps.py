@@ -43,9 +43,12 @@ def road_waypoints(n_cities, world_radius, road_radius, rng=np.random):
     return np.vstack([points[0], np.vstack(points[1:])])
 
 
-def _pairwise_norm(a, b):
-    d = a[:, None, :] - b[None, :, :]
-    return np.linalg.norm(d, axis=2)
+def _pairwise_sq(a, b):
+    """Squared distances as np.linalg.norm(a[:, None] - b[None], axis=2) sums them before
+    its sqrt (d0*d0 + d1*d1), without the (n, m, 2) temporaries."""
+    dx = a[:, None, 0] - b[None, :, 0]
+    dy = a[:, None, 1] - b[None, :, 1]
+    return dx * dx + dy * dy
 
 
 def generate_targets(xmax=120, ymax=120, res=5.5, motion_radius=None, n_cities=12, rng=np.random):
@@ -54,9 +57,11 @@ def generate_targets(xmax=120, ymax=120, res=5.5, motion_radius=None, n_cities=1
         motion_radius = res * 1.2
     lattice = square_lattice(-xmax, xmax, -ymax, ymax, res)
     roads = road_waypoints(n_cities, xmax, motion_radius, rng)
-    near = np.min(_pairwise_norm(lattice, roads), axis=1) <= (motion_radius / 1.4)
+    # min over roads of the norms = sqrt of the min squared norm (sqrt is monotone and
+    # correctly rounded), so one sqrt per lattice point decides the same set
+    near = np.sqrt(np.min(_pairwise_sq(lattice, roads), axis=1)) <= (motion_radius / 1.4)
     targets = lattice[near, :]
-    r = _pairwise_norm(targets, targets)
+    r = np.sqrt(_pairwise_sq(targets, targets))
     r[r > motion_radius] = 0
     _, labels = connected_components(csgraph=csr_matrix(r), directed=False, return_labels=True)
     return targets[labels == np.argmax(np.bincount(labels)), :]
