@@ -1144,6 +1144,7 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
     h->fin_seq = (h->fin_seq & 0x3fffffff) + 1;  // never 0 (the word's initial value), no overflow
     fd.seq = h->fin_seq;
     if (!rim_last) a.fin = fd;
+    else a.fin.fence = 1;  // the step's page-locked writes land before the rim kNN's flag
   }
   if (int rc = timed_launch(h, a, dyn, uf64, ctrl)) return rc;
   if (dyn) h->cur ^= 1;

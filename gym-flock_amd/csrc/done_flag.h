@@ -17,13 +17,15 @@ struct DoneFlag {
   int32_t* cnt;   // device word, 0 between launches: workgroups finished
   int32_t* host;  // mapped address of the page-locked word, or nullptr: no flag
   int32_t seq;    // value stored when the whole grid is done
-  int32_t pad;
+  int32_t fence;  // host == nullptr: still make this launch's results visible system-wide
+                  // before it ends (a later launch of the same call carries the flag)
 };
 
 // Every thread of every workgroup calls it as its last action (uniform branch).
 __device__ __forceinline__ void signal_done(const DoneFlag& f) {
-  if (!f.host) return;
+  if (!f.host && !f.fence) return;
   __threadfence_system();  // this thread's results, system-wide, before the count
+  if (!f.host) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nb = static_cast<int>(gridDim.x * gridDim.y * gridDim.z);
