@@ -1283,7 +1283,7 @@ def test_step_host_flag_and_stream_waits_agree(n):
     the host waits for the last kernel's completion flag: the step's at N=100, the rim
     kNN's at N=300) and into pageable numpy arrays (copies after the launches; the host
     waits for the stream), on two handles from the same state and actions: every output
-    equal at each of 30 steps, and the first step's against the oracle."""
+    equal at each of 300 steps, and the first step's against the oracle."""
     B, K = 1, 7
     hs = [nat.FlockHandle(n, B, n_neighbors=K) for _ in range(2)]
     x0 = synthetic_batch(B, n, seed0=21)
@@ -1295,7 +1295,7 @@ def test_step_host_flag_and_stream_waits_agree(n):
     pinned = {k: pool.array(*v) for k, v in shapes.items()}
     plain = {k: np.empty(*v) for k, v in shapes.items()}
     rs = np.random.RandomState(3)
-    for t in range(30):
+    for t in range(300):
         u = rs.uniform(-1, 1, size=(B, n, 2)).astype(np.float32)
         for h, o in ((hs[0], pinned), (hs[1], plain)):
             h.step_host_knn(u.ctypes.data, False, o["sv"].ctypes.data, o["net"].ctypes.data, o["rew"].ctypes.data,
