@@ -41,3 +41,6 @@ pmc knn pmc_step.py KNN=1 &&
 pmc n8192 pmc_step.py N=8192 B=32 &&
 pmc cov pmc_cov.py
 echo "pmc rc=$?"
+# the GPU suite once more, after everything above (flakiness check)
+cd $R
+timeout -k 10 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 180 --timeout-method thread > $O/pytest_gpu_again.log 2>&1; echo "second suite rc=$?"; tail -1 $O/pytest_gpu_again.log
