@@ -640,3 +640,22 @@ def test_device_reset_draws_equal_host_draws(R):
     np.testing.assert_array_equal(sd[2], rs.choice(np.arange(T), size=(R,), replace=False))
     for v in vs:
         v.close()
+
+
+@pytest.mark.parametrize("frac", [0.0, 0.3, 1.0])
+def test_device_reset_fraction_edges(frac):
+    """cov_reset_seeded at the ends of frac_active_targets (nothing unvisited, everything
+    unvisited) and between: the draws and visited flags equal the host loops'."""
+    from gym_flock.envs.spatial.maps import generate_targets
+    np.random.seed(31)
+    targets = generate_targets()
+    vs = [VecCoverage(3, 8, max_nodes=800, frac_active_targets=frac) for _ in range(2)]
+    for v in vs:
+        v.set_targets(targets)
+    sd, vd = vs[0].reset(seed=5)
+    sh, vh = vs[1].reset(seed=5, draws="host")
+    np.testing.assert_array_equal(sd, sh)
+    np.testing.assert_array_equal(vd, vh)
+    np.testing.assert_array_equal(vs[0].h.get_rng()[0], vs[1].h.get_rng()[0])
+    for v in vs:
+        v.close()
