@@ -608,11 +608,22 @@ def bench_greedy(v, targets, R, M, B, K, args):
     t0 = time.perf_counter()
     v.reset(seed=500)
     reset_dev = time.perf_counter() - t0
+    # whole expert episodes as a data-collection loop runs them: reset (draws on the
+    # device) + 75 fused expert steps, for all envs, back to back
+    v.sync()
+    t0 = time.perf_counter()
+    for e in range(4):
+        v.reset(seed=600 + e)
+        for _ in range(75):
+            v.step(greedy=True)
+    v.sync()
+    episode = (time.perf_counter() - t0) / 4
     t0 = time.perf_counter()
     v.reset(seed=500, draws="host")
     reset_host = time.perf_counter() - t0
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
            "reset_ms_all_envs": 1e3 * reset_dev, "reset_ms_all_envs_host_draws": 1e3 * reset_host,
+           "expert_episode_ms_all_envs": 1e3 * episode, "expert_env_episodes_per_s": B / episode,
            "expert_step_ms_in_episodes": 1e3 * ep_t / ep_k,
            "expert_robot_steps_per_s_in_episodes": R * B * ep_k / ep_t,
            "expert_step_ms_in_episodes_fallback_action0": 1e3 * z_t / ep_k,
