@@ -430,6 +430,8 @@ int cov_reset_seeded(cov_handle* h, uint64_t seed, double frac_active, int32_t* 
   const size_t B = h->cfg.n_envs, R = h->cfg.n_robots, Tm = h->a.Tmax;
   if (seed + B > 0x100000000ull) return cfail(GF_EINVAL, "seed + n_envs must fit in 32 bits (RandomState seeds)");
   if (!(frac_active >= 0.0 && frac_active <= 1.0)) return cfail(GF_EINVAL, "frac_active must be in [0, 1]");
+  if ((size_t)gf::kMtN * 4 + Tm * 5 > 65536)  // the draw kernel's LDS: key, permutation, flags
+    return cfail(GF_EINVAL, "max_nodes - n_robots too large for the device reset draws (draw on the host)");
   if (int rc = use(h)) return rc;
   if (!h->mt_key) {
     int rc;
