@@ -106,6 +106,7 @@ struct fe_handle {
   bool obs_on_host = false;             // the last launch wrote state_values / network to
                                         // host arrays only (fe_step_host): device copies stale
   int R = 0, T = 0, bpe = 0;
+  int knn_exact = 0;                    // the fused kNN is exact in the step (gf::step_knn_exact)
   size_t BN = 0;
   int diag = 0;                         // ablation switches (diagnostic build only, fe_diag)
   int prefetch = 0;                     // tile loads one tile ahead (N >= 16 tiles)
@@ -555,6 +556,7 @@ int prepare_outputs(fe_handle* h, int flags, gf::StepArgs& a, int xw) {
 
 gf::StepArgs base_args(fe_handle* h) {
   gf::StepArgs a{};
+  a.knn_exact = h->knn_exact;
   a.dt = h->cfg.dt;
   a.action_scalar = h->cfg.action_scalar;
   a.cr = h->cfg.comm_radius;
@@ -695,7 +697,7 @@ int launch_knn_cur(fe_handle* h, int mode, int32_t* idx_to = nullptr, float* obs
   }
 #endif
   auto& r = h->kread[h->cur];
-  if (mode == 2 && gf::step_knn_exact(h->cfg.n_agents, h->T)) {
+  if (mode == 2 && h->knn_exact) {
     // envs this small: the fused step ranks every row exactly itself (KX), none is left
     // to the rim kernel, so it is not launched
     r.live = false;
@@ -820,6 +822,12 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   h->BN = B * N;
   h->R = gf::step_rows_per_block(cfg->n_agents);
   h->T = gf::step_tile(cfg->n_agents);
+  // a Flocking-v0 handle of one env (the drop-in step): one tile holds the whole env, which
+  // the step then ranks exactly (no keys in the feature pass, no rim kernel; 32 KiB of LDS
+  // at N = 1024, which one env's few workgroups afford)
+  if (B == 1 && cfg->n_neighbors > 0 && N <= (size_t)gf::kStepExactKnnMaxOneEnv)
+    h->T = static_cast<int>((N + 63) / 64 * 64);
+  h->knn_exact = gf::step_knn_exact(cfg->n_agents, h->T, cfg->n_envs) ? 1 : 0;
   // tile loads issued a tile ahead: 1604 -> 1527 us at N=8192 (16 tiles); no gain at 2-8
   // tiles, where its registers cost occupancy instead
   h->prefetch = (cfg->n_agents + h->T - 1) / h->T >= 16 ? 1 : 0;
@@ -1077,7 +1085,7 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
   // copied to the device first
   // (the fused kNN step with the controller has an inline-actions form only for envs
   // ranked exactly in the step, gf::step_knn_exact)
-  const bool uin = dyn && !(knn && ctrl && !gf::step_knn_exact(h->cfg.n_agents, h->T)) && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
+  const bool uin = dyn && !(knn && ctrl && !h->knn_exact) && h->cfg.n_envs == 1 && h->cfg.n_agents <= h->T && !h->has_variant && !h->dt_per_env &&
                    h->BN * 2 * (uf64 ? 8 : 4) <= (size_t)gf::kUInlineBytes;
   if (uin) {
     up = u;
@@ -1126,7 +1134,7 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
   // stream (done_flag.h: ~8 us sooner)
   const bool fin = (!state_values || sv_m) && (!network || net_m) && (!rewards || rw_m) && (!ctrl || ct_m) &&
                    (!knn || kdirect);
-  const bool rim_last = knn && !gf::step_knn_exact(h->cfg.n_agents, h->T);
+  const bool rim_last = knn && !h->knn_exact;
   gf::DoneFlag fd{};
   if (fin) {
     if (!h->fin_cnt) {

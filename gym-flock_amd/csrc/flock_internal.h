@@ -27,6 +27,8 @@ constexpr int kStoreTab = 16;      // network rows: float4 table entries per wav
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
 constexpr int kStepExactKnnMax = 128;  // fused kNN: envs up to this size are ranked exactly in
                                        // the step (KX: one tile in LDS, no rim kernel)
+constexpr int kStepExactKnnMaxOneEnv = 1024;  // the same for a handle of one env (the drop-in
+                                              // step: its tile then holds the whole env)
 constexpr int kKnnRimGrid = 256;     // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnRimHalfGrid = kKnnRimGrid / 2;  // the same per half-batch launch
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
@@ -92,6 +94,7 @@ struct StepArgs {
   unsigned knn_qmax;      // 2^qbits - 2
   double knn_qmaxd;       // the same as a double (compared with r2 * scale)
   int knn_jbits;          // bits of the agent index (qbits = 32 - jbits)
+  int knn_exact;          // the handle's fused selection is exact in the step (step_knn_exact)
   DoneFlag fin;           // drop-in launch: the grid's completion flag (done_flag.h)
 };
 
@@ -140,9 +143,10 @@ hipError_t launch_step(const StepArgs& a, bool dyn, bool u_f64, bool ctrl, hipSt
 // Whether a step of this geometry can carry the fused k-nearest selection (K ==
 // kStepFusedK, no variant, no tile prefetch, at least K word-slices per row).
 bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch);
-// Whether the fused selection of an env of N agents (tile T) ranks every row exactly in
-// the step (the KX instantiation: one tile, N <= kStepExactKnnMax): no rim kernel follows.
-bool step_knn_exact(int N, int T);
+// Whether the fused selection of a handle of B envs of N agents (tile T) ranks every row
+// exactly in the step (the KX instantiation: one tile, N <= kStepExactKnnMax, or one env of
+// up to kStepExactKnnMaxOneEnv agents): no rim kernel follows.
+bool step_knn_exact(int N, int T, int B);
 hipError_t launch_knn(const KnnArgs& a, hipStream_t s);
 hipError_t launch_stats(const StatsArgs& a, hipStream_t s);
 // per env: mean vel_diffs, mean min_dists of launch_stats' outputs -> out (B,2)

@@ -1998,12 +1998,14 @@ bool step_fused_knn_ok(int N, int R, int K, bool variant, bool prefetch) {
   return K == kStepFusedK && !variant && !prefetch && kThreads / R >= K && N <= 65536;
 }
 
-bool step_knn_exact(int N, int T) { return N <= kStepExactKnnMax && N <= T; }
+bool step_knn_exact(int N, int T, int B) {
+  return N <= T && (N <= kStepExactKnnMax || (B == 1 && N <= kStepExactKnnMaxOneEnv));
+}
 
 template <bool DYN, bool UF64, bool CTRL>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s) {
   if constexpr (DYN) {
-    const bool exact = a.knn_idx && step_knn_exact(a.N, a.T);
+    const bool exact = a.knn_idx && a.knn_exact;
     if (a.u_inline) {
       if (a.variant) return hipErrorInvalidValue;
       if (a.knn_idx) {  // the drop-in Flocking-v0 step (fe_step_host_knn*)
