@@ -822,9 +822,9 @@ int fe_create(const fe_config* cfg, fe_handle** out) {
   h->BN = B * N;
   h->R = gf::step_rows_per_block(cfg->n_agents);
   h->T = gf::step_tile(cfg->n_agents);
-  // a Flocking-v0 handle of one env (the drop-in step): one tile holds the whole env, which
-  // the step then ranks exactly (no keys in the feature pass, no rim kernel; 32 KiB of LDS
-  // at N = 1024, which one env's few workgroups afford)
+  // a Flocking-v0 handle of one env (the drop-in step) of up to kStepExactKnnMaxOneEnv
+  // agents: one tile holds the whole env, which the step then ranks exactly (no keys in the
+  // feature pass, no rim kernel)
   if (B == 1 && cfg->n_neighbors > 0 && N <= (size_t)gf::kStepExactKnnMaxOneEnv)
     h->T = static_cast<int>((N + 63) / 64 * 64);
   h->knn_exact = gf::step_knn_exact(cfg->n_agents, h->T, cfg->n_envs) ? 1 : 0;

@@ -27,8 +27,10 @@ constexpr int kStoreTab = 16;      // network rows: float4 table entries per wav
 constexpr int kStepInlineRim = 2;  // fused kNN: unranked rows a wave ranks itself (more: rim kernel)
 constexpr int kStepExactKnnMax = 128;  // fused kNN: envs up to this size are ranked exactly in
                                        // the step (KX: one tile in LDS, no rim kernel)
-constexpr int kStepExactKnnMaxOneEnv = 1024;  // the same for a handle of one env (the drop-in
-                                              // step: its tile then holds the whole env)
+constexpr int kStepExactKnnMaxOneEnv = 192;  // the same for a handle of one env (the drop-in
+                                             // step: its tile then holds the whole env); beyond
+                                             // it the per-row scan costs more than the rim
+                                             // kernel it saves (profiles/r05/ab_dropin_exact_one_env.txt)
 constexpr int kKnnRimGrid = 256;     // rim kNN: workgroups walking the flagged blocks
 constexpr int kKnnRimHalfGrid = kKnnRimGrid / 2;  // the same per half-batch launch
 constexpr int kKnnFewSlow = 16;     // kNN: up to this many rows to scan per workgroup are
