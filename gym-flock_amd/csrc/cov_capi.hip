@@ -501,6 +501,8 @@ int cov_step(cov_handle* h, const int32_t* actions, int flags) {
     return cfail(GF_EINVAL, "COV_GREEDY_RNG needs COV_ACTIONS_GREEDY");
   if ((flags & COV_GREEDY_RNG) && !h->mt_key)
     return cfail(GF_ESTATE, "COV_GREEDY_RNG: set the envs' np_random streams first (cov_set_rng)");
+  if ((flags & COV_GREEDY_RNG) && h->cfg.n_robots > gf::kMtN)
+    return cfail(GF_EINVAL, "COV_GREEDY_RNG needs n_robots <= 624 (one key regeneration per step)");
   if (flags & COV_ACTIONS_GREEDY) {
     // controller(greedy=True) in the step's own launch, from the greedy lists
     if (!h->tm_ready || !h->tm_glist) {

@@ -177,7 +177,7 @@ class VecCoverage:
             visited[b, drop - R] = 0
             rngs.append(rs)
         self.h.reset(start, visited)
-        if R <= 624:  # cov_set_rng: one key regeneration per step at most
+        if R <= 624:  # device draws (COV_GREEDY_RNG): one key regeneration per step at most
             self.h.set_rng(rngs)
         return start, visited
 
@@ -193,8 +193,9 @@ class VecCoverage:
         """actions (B,R); or resident=True (the last set/greedy actions); or greedy=True
         (controller(greedy=True), coverage.py:800-872, computed in the step's own launch).
         fallback: robots the reference hands to np_random.choice(4) (:861-864) draw it from
-        their env's stream on the device ("draw", the reference's semantics) or take
-        action 0 ("zero"); include/gymflock.h COV_ACTIONS_GREEDY, COV_GREEDY_RNG."""
+        their env's stream on the device ("draw", the reference's semantics; needs
+        n_robots <= 624) or take action 0 ("zero"); include/gymflock.h COV_ACTIONS_GREEDY,
+        COV_GREEDY_RNG."""
         if resident or greedy:
             if greedy:
                 rc = self.h._step_greedy_rng() if fallback == "draw" else self.h._step_greedy()
