@@ -551,7 +551,7 @@ def test_device_rng_argument_checks():
     with pytest.raises(nat.GymFlockError, match="624"):
         h.set_rng([np.random.RandomState(1)])
     # streams from the device reset do not lift the limit either
-    xs, ys = np.meshgrid(np.arange(30) * 5.5, np.arange(30) * 5.5)
+    xs, ys = np.meshgrid(np.arange(28) * 5.5, np.arange(28) * 5.5)  # 784 targets: >= 700 robots, <= 800
     h.set_targets(np.stack([xs.ravel(), ys.ravel()], axis=1), env=0)
     h.reset_seeded(3)
     with pytest.raises(nat.GymFlockError, match="624"):
