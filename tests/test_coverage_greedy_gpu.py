@@ -547,11 +547,11 @@ def test_device_rng_argument_checks():
     with pytest.raises(nat.GymFlockError, match="position"):
         h.set_rng([tuple(st)])
     h.close()
-    h = nat.CoverageHandle(700, 1, 1500)
+    h = nat.CoverageHandle(700, 1, 2400)  # room for 8 * 700 action edges beside the motion graph
     with pytest.raises(nat.GymFlockError, match="624"):
         h.set_rng([np.random.RandomState(1)])
     # streams from the device reset do not lift the limit either
-    xs, ys = np.meshgrid(np.arange(28) * 5.5, np.arange(28) * 5.5)  # 784 targets: >= 700 robots, <= 800
+    xs, ys = np.meshgrid(np.arange(28) * 5.5, np.arange(28) * 5.5)  # 784 targets >= 700 robots
     h.set_targets(np.stack([xs.ravel(), ys.ravel()], axis=1), env=0)
     h.reset_seeded(3)
     with pytest.raises(nat.GymFlockError, match="624"):
