@@ -41,6 +41,16 @@ pmc knn pmc_step.py KNN=1 &&
 pmc n8192 pmc_step.py N=8192 B=32 &&
 pmc cov pmc_cov.py
 echo "pmc rc=$?"
+# run-to-run spread of the headline on this box: three more driver-window lines
+cd $R
+for r in 1 2 3; do timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-other-configs > $O/bench20_rep$r.json 2>/dev/null; done
+python - $O <<'PY'
+import json, sys
+for r in (1, 2, 3):
+    d = json.loads(open("%s/bench20_rep%d.json" % (sys.argv[1], r)).read().strip().splitlines()[-1])
+    print("rep", r, round(d["ms_per_step"] * 1e3, 2), "us", round(d["roofline"]["frac"], 3),
+          "knn", round(d["flocking_v0_knn7"]["ms_per_step"] * 1e3, 2), round(d["flocking_v0_knn7"]["ratio_to_plain_step"], 3))
+PY
 # the GPU suite once more, after everything above (flakiness check)
 cd $R
 timeout -k 10 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 180 --timeout-method thread > $O/pytest_gpu_again.log 2>&1; echo "second suite rc=$?"; tail -1 $O/pytest_gpu_again.log
