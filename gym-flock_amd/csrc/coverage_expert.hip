@@ -31,48 +31,73 @@ namespace gf {
 namespace {
 
 constexpr int kTmLanes = 64;            // sources per wave (one wave per workgroup)
-constexpr int kBatch = 8;               // independent edges per batch
+constexpr int kBatch = 8;               // independent edges per batch (16 measured slower)
 constexpr uint32_t kInf = 0xFFFF;  // uint16 cost matrix: unreachable
 constexpr int kMaxCost = 1000;          // MAX_COST :68
 
 // Conflict levels of one env's motion-edge list, then the batched schedule: sched[b]
 // holds nslots[b] (a multiple of kBatch) words s | q << 16 (target-local), level by
-// level, edges of a level in list order, no-op slots s = q = T (the dummy column).
+// level, no-op slots s = q = T (the dummy column). The levels are one serial pass over
+// the list (lane 0, everything in LDS: each edge is one round of four LDS loads); the
+// counts, offsets and the scatter run on the whole wave. Edges of one level are mutually
+// independent, so their order inside the level does not change any result.
 __global__ __launch_bounds__(64) void cov_tm_schedule_kernel(CovTmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = a.envs[blockIdx.x];
   const int T = a.ntg[b], E = a.n_motion[b], R = a.R, E4 = 4 * a.M;
-  int* lw = reinterpret_cast<int*>(smem);  // [T] last level writing the column
-  int* lr = lw + T;                          // [T] last level reading it
-  int* level = lr + T;                       // [E]
-  int* fill = level + E;                     // [E + 1] per-level counts, then offsets
+  const int lane = threadIdx.x;
+  int* shared2 = reinterpret_cast<int*>(smem);  // the level count, the slot count
+  int* lw = shared2 + 2;                          // [T] last level writing the column
+  int* lr = lw + T;                               // [T] last level reading it
+  uint32_t* sq = reinterpret_cast<uint32_t*>(lr + T);  // [E] the edges, s | q << 16
+  int* level = reinterpret_cast<int*>(sq + E);          // [E]
+  int* fill = level + E;                                // [E + 1] per-level counts, then offsets
+  int* base = fill + E + 1;                             // [E + 1] the levels' padded offsets
   const int32_t* snd = a.senders + (size_t)b * E4;
   const int32_t* rcv = a.receivers + (size_t)b * E4;
-  for (int k = threadIdx.x; k < T; k += 64) lw[k] = lr[k] = 0;
-  for (int k = threadIdx.x; k <= E; k += 64) fill[k] = 0;
+  for (int k = lane; k < T; k += 64) lw[k] = lr[k] = 0;
+  for (int k = lane; k <= E; k += 64) fill[k] = 0;
+  for (int e = lane; e < E; e += 64) sq[e] = (uint32_t)(snd[e] - R) | ((uint32_t)(rcv[e] - R) << 16);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     int nlev = 0;
     for (int e = 0; e < E; ++e) {
-      const int s = snd[e] - R, q = rcv[e] - R;
-      const int L = max(max(lw[s], lw[q]), lr[q]) + 1;  // after every conflicting edge
+      const uint32_t w = sq[e];
+      const int s = w & 0xFFFF, q = w >> 16;
+      const int ws = lw[s], wq = lw[q], rq = lr[q], rs = lr[s];
+      const int L = max(max(ws, wq), rq) + 1;  // after every conflicting edge
       level[e] = L;
-      lw[q] = max(lw[q], L);
-      lr[s] = max(lr[s], L);
-      lr[q] = max(lr[q], L);
-      fill[L - 1] += 1;
+      lw[q] = L;  // L > lw[q], lr[q]
+      lr[q] = L;
+      lr[s] = max(rs, L);  // (s == q never: no self edges; the store to q comes first)
       nlev = max(nlev, L);
     }
+    shared2[0] = nlev;
+  }
+  __syncthreads();
+  const int nlev = shared2[0];
+  for (int e = lane; e < E; e += 64) atomicAdd(&fill[level[e] - 1], 1);
+  __syncthreads();
+  if (lane == 0) {
     int off = 0;
     for (int L = 0; L < nlev; ++L) {
       const int n = fill[L];
-      fill[L] = off;
+      fill[L] = base[L] = off;
       off += (n + kBatch - 1) / kBatch * kBatch;
     }
-    uint32_t* out = a.sched + (size_t)b * a.sched_stride;
-    const uint32_t noop = (uint32_t)T | ((uint32_t)T << 16);
-    for (int k = 0; k < off; ++k) out[k] = noop;
-    for (int e = 0; e < E; ++e) out[fill[level[e] - 1]++] = (uint32_t)(snd[e] - R) | ((uint32_t)(rcv[e] - R) << 16);
+    base[nlev] = off;
+    shared2[1] = off;
+  }
+  __syncthreads();
+  const int off = shared2[1];
+  uint32_t* out = a.sched + (size_t)b * a.sched_stride;
+  for (int e = lane; e < E; e += 64) out[atomicAdd(&fill[level[e] - 1], 1)] = sq[e];
+  __syncthreads();
+  // each level's padding (past its edges) holds no-ops: words no edge was stored to
+  const uint32_t noop = (uint32_t)T | ((uint32_t)T << 16);
+  for (int L = lane; L < nlev; L += 64)
+    for (int k = fill[L]; k < base[L + 1]; ++k) out[k] = noop;
+  if (lane == 0) {
     a.nslots[b] = off;
     a.nlev[b] = nlev;
     a.overflow[b] = 0;
@@ -425,7 +450,7 @@ __global__ __launch_bounds__(256) void cov_greedy_kernel(CovGreedyArgs a) {
 
 size_t cov_time_matrix_lds_bytes(int t_lds, bool wide) { return (size_t)(t_lds + 1) * kTmLanes * (wide ? 2 : 1); }
 
-size_t cov_tm_schedule_lds_bytes(int t_lds, int e_max) { return (size_t)(2 * t_lds + 2 * e_max + 1) * 4; }
+size_t cov_tm_schedule_lds_bytes(int t_lds, int e_max) { return (size_t)(2 * t_lds + 4 * e_max + 4) * 4; }
 
 hipError_t launch_cov_tm_schedule(const CovTmArgs& a, int n_envs_sel, int e_max, hipStream_t s) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cov_tm_schedule_kernel),
