@@ -77,6 +77,7 @@ struct cov_handle {
   uint8_t* needs_random = nullptr;
   int32_t* tm_envsel = nullptr;
   uint32_t* tm_sched = nullptr;
+  int32_t* tm_lev = nullptr;  // (B, 4 * Tmax + 2): the schedule levels' slot offsets
   int32_t* tm_nslots = nullptr;
   int32_t* tm_nlev = nullptr;
   uint8_t* tm_overflow = nullptr;
@@ -136,7 +137,7 @@ void cov_release(cov_handle* h) {
   void* bufs[] = {h->ntg, h->tgt, a.nbr, a.cnt, a.n_motion, a.xr, a.cur, a.visited, a.nvisited,
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
                   a.receivers, a.obs_step, a.axy, a.nrec, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT, h->tm_glist, h->tm_glen,
-                  h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
+                  h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_lev, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
                   h->goff, h->mt_key, h->mt_pos};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -185,6 +186,7 @@ int ensure_time_matrix(cov_handle* h) {
         (rc = calloc_dev(&h->tm_flags, (size_t)B * nchunk * kcap)) ||
         (rc = calloc_dev(&h->needs_random, (size_t)B * h->cfg.n_robots)) || (rc = calloc_dev(&h->tm_envsel, (size_t)B)) ||
         (rc = calloc_dev(&h->tm_sched, (size_t)B * sched_stride)) || (rc = calloc_dev(&h->tm_nslots, (size_t)B)) ||
+        (rc = calloc_dev(&h->tm_lev, (size_t)B * (4 * Tm + 2))) ||
         (rc = calloc_dev(&h->tm_nlev, (size_t)B)) || (rc = calloc_dev(&h->tm_overflow, (size_t)B)) ||
         (rc = calloc_dev(&h->tm_cost8, (size_t)B * Tm * Tm)) || (rc = calloc_dev(&h->tm_wide, (size_t)B)))
       return rc;
@@ -232,6 +234,8 @@ int ensure_time_matrix(cov_handle* h) {
   t.nlev = h->tm_nlev;
   t.overflow = h->tm_overflow;
   t.sched_stride = sched_stride;
+  t.lev_off = h->tm_lev;
+  t.lev_stride = 4 * Tm + 2;  // levels <= motion edges <= 4 per target, + the end offset
   CV_HIP(hipMemcpyAsync(h->tm_envsel, sel.data(), sel.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
   hipError_t e = gf::launch_cov_tm_schedule(t, (int)sel.size(), e_max, h->stream);
   if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_tm_schedule_kernel: ") + hipGetErrorString(e));

@@ -97,6 +97,8 @@ __global__ __launch_bounds__(64) void cov_tm_schedule_kernel(CovTmArgs a) {
   const uint32_t noop = (uint32_t)T | ((uint32_t)T << 16);
   for (int L = lane; L < nlev; L += 64)
     for (int k = fill[L]; k < base[L + 1]; ++k) out[k] = noop;
+  if (a.lev_off)  // the levels' slot offsets (cov_time_matrix_mw_kernel)
+    for (int L = lane; L <= nlev; L += 64) a.lev_off[(size_t)b * a.lev_stride + L] = base[L];
   if (lane == 0) {
     a.nslots[b] = off;
     a.nlev[b] = nlev;
@@ -238,6 +240,142 @@ __global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, 
           *reinterpret_cast<uint64_t*>(row8 + t) = w;
         }
       for (; t < T; ++t) row8[t] = (uint8_t)col[t * kTmLanes + lane];
+    }
+  }
+}
+
+// The same passes with kTmWaves waves per 64-source chunk, for launches of few chunks
+// (the drop-in env's map: one env, ~9 chunks, where one wave per chunk leaves the sweep a
+// chain of ~230 dependent batches). The waves split each conflict level's batches (its
+// edges are mutually independent: disjoint written columns, none read by another) and
+// meet at a barrier between levels; the sweep's flags and the row scan are combined over
+// the workgroup. The predecessors are kept in LDS too (the waves' global stores to one
+// entry would not be ordered by the barriers) and written out at the end. Same results
+// as cov_time_matrix_kernel.
+constexpr int kTmWaves = 4;
+constexpr size_t kTmFewChunks = 256;  // launches of at most this many chunks (one per CU) take it
+
+template <typename V, bool PASS_B>
+__global__ __launch_bounds__(kTmLanes * kTmWaves) void cov_time_matrix_mw_kernel(CovTmArgs a, const uint32_t* __restrict__ sched_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr uint32_t inf = (V)~(V)0;
+  const int b = a.envs[blockIdx.y];
+  const int chunk = blockIdx.x;
+  const int T = a.ntg[b];
+  const int src0 = chunk * kTmLanes;
+  if (src0 >= T) return;  // uniform
+  const int Tm = a.Tmax;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int src = src0 + lane;
+  const bool valid = src < T;
+  const int kmax = a.horizon > -1 ? a.horizon + 1 : a.kcap;
+  const int nlev = a.nlev[b];
+  uint8_t* flags = a.flags + ((size_t)b * a.nchunk + chunk) * a.kcap;
+  int K = T > 1 ? kmax : 0;
+  if (PASS_B) {
+    if (a.overflow[b]) return;
+    const uint8_t* fenv = a.flags + (size_t)b * a.nchunk * a.kcap;
+    const int nch = (T + kTmLanes - 1) / kTmLanes;
+    for (int k = 0; k < kmax && K == kmax && T > 1; ++k) {
+      int f = 0;
+      for (int c = 0; c < nch; ++c) f |= fenv[(size_t)c * a.kcap + k];
+      if (!(f & 1) || !(f & 2)) K = k + 1;
+    }
+    int kvalid = kmax;
+    for (int k = 0; k < kmax; ++k)
+      if (!(flags[k] & 1)) {
+        kvalid = k;
+        break;
+      }
+    if (T <= 1 || K >= kvalid) return;
+  }
+  V* col = reinterpret_cast<V*>(smem);  // [T + 1][64], column T = dummy inf
+  const size_t col_bytes = ((size_t)(a.t_lds + 1) * kTmLanes * sizeof(V) + 15) & ~(size_t)15;
+  int16_t* pl = reinterpret_cast<int16_t*>(smem + col_bytes);  // [T + 1][64] predecessors
+  int* loff = reinterpret_cast<int*>(smem + col_bytes + ((((size_t)a.t_lds + 1) * kTmLanes * 2 + 15) & ~(size_t)15));
+  for (int t = wv; t <= T; t += kTmWaves) {
+    col[t * kTmLanes + lane] = (t == src) ? 0 : (V)inf;
+    pl[t * kTmLanes + lane] = -1;
+  }
+  for (int k = tid; k <= nlev; k += kTmLanes * kTmWaves) loff[k] = a.lev_off[(size_t)b * a.lev_stride + k];
+  const uint32_t* sched = sched_all + (size_t)b * a.sched_stride;
+  __syncthreads();
+  uint32_t mx = 0;  // this wave's share of the lane's row (columns wv, wv + kTmWaves, ...)
+  for (int sweep = 0; sweep < K; ++sweep) {
+    if (sizeof(V) == 1 && __syncthreads_or(mx + (uint32_t)nlev >= inf)) {
+      if (tid == 0) a.overflow[b] = 1;
+      return;
+    }
+    int changed = 0;
+    for (int L = 0; L < nlev; ++L) {
+      const int s0 = __builtin_amdgcn_readfirstlane(loff[L]), s1 = __builtin_amdgcn_readfirstlane(loff[L + 1]);
+      for (int j = s0 + wv * kBatch; j < s1; j += kBatch * kTmWaves) {
+        uint32_t w[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sched[j + k]);
+        uint32_t vs[kBatch], vq[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+          vs[k] = col[(w[k] & 0xFFFF) * kTmLanes + lane];
+          vq[k] = col[(w[k] >> 16) * kTmLanes + lane];
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+          const uint32_t via = vs[k] + 1u;
+          const bool better = via < vq[k];
+          col[(w[k] >> 16) * kTmLanes + lane] = (V)(via < vq[k] ? via : vq[k]);
+          changed |= better ? 1 : 0;
+          if (better) pl[(w[k] >> 16) * kTmLanes + lane] = (int16_t)(w[k] & 0xFFFF);
+        }
+      }
+      __syncthreads();  // the next level reads what this one wrote
+    }
+    if (!PASS_B || sizeof(V) == 1) {
+      bool any_inf_lane = false;
+      mx = 0;
+      if (valid)
+        for (int t = wv; t < T; t += kTmWaves) {
+          const uint32_t v = col[t * kTmLanes + lane];
+          any_inf_lane = any_inf_lane || v == inf;
+          mx = v != inf && v > mx ? v : mx;
+        }
+      if (!PASS_B) {
+        const bool any_changed = __syncthreads_or(changed) != 0;
+        const bool any_inf = __syncthreads_or(any_inf_lane) != 0;
+        if (tid == 0) flags[sweep] = (any_changed ? 1 : 0) | (any_inf ? 2 : 0);
+        if (!any_changed) {
+          for (int k = sweep + 1 + tid; k < a.kcap; k += kTmLanes * kTmWaves) flags[k] = any_inf ? 2 : 0;
+          break;
+        }
+      }
+    }
+  }
+  // predecessors [q][src] (consecutive sources per wave: one 128-byte row piece per q)
+  // and cost rows, row-major [src][t] as uint16 (inf = 0xFFFF); the waves take groups of
+  // 4 (uint8 copy: 8) entries in turn
+  if (valid) {
+    int16_t* prevT = a.prevT + (size_t)b * Tm * Tm;
+    for (int q = wv; q < T; q += kTmWaves) prevT[(size_t)q * Tm + src] = pl[q * kTmLanes + lane];
+    auto ent = [&](int t) -> uint64_t {
+      const uint32_t v = col[t * kTmLanes + lane];
+      return v == inf ? 0xFFFFull : (uint64_t)v;
+    };
+    uint16_t* row = a.cost + ((size_t)b * Tm + src) * Tm;
+    const int t4 = (Tm & 3) == 0 ? (T & ~3) : 0;
+    for (int t = 4 * wv; t < t4; t += 4 * kTmWaves)
+      *reinterpret_cast<uint64_t*>(row + t) = ent(t) | (ent(t + 1) << 16) | (ent(t + 2) << 32) | (ent(t + 3) << 48);
+    for (int t = t4 + wv; t < T; t += kTmWaves) row[t] = (uint16_t)ent(t);
+    if (sizeof(V) == 1 && a.cost8) {
+      uint8_t* row8 = a.cost8 + ((size_t)b * Tm + src) * Tm;
+      const int t8 = (Tm & 7) == 0 ? (T & ~7) : 0;
+      for (int t = 8 * wv; t < t8; t += 8 * kTmWaves) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w |= (uint64_t)col[(t + k) * kTmLanes + lane] << (8 * k);
+        *reinterpret_cast<uint64_t*>(row8 + t) = w;
+      }
+      for (int t = t8 + wv; t < T; t += kTmWaves) row8[t] = (uint8_t)col[t * kTmLanes + lane];
     }
   }
 }
@@ -464,6 +602,22 @@ template <typename V>
 static hipError_t launch_tm_passes(const CovTmArgs& a, int n_envs_sel, hipStream_t s) {
   const dim3 grid((a.t_lds + kTmLanes - 1) / kTmLanes, n_envs_sel);
   const size_t lds = cov_time_matrix_lds_bytes(a.t_lds, sizeof(V) == 2);
+  const size_t lds_mw = ((lds + 15) & ~(size_t)15) + ((((size_t)a.t_lds + 1) * kTmLanes * 2 + 15) & ~(size_t)15) +
+                        (size_t)a.lev_stride * sizeof(int32_t);
+  // (pass A's block-wide reductions take 256 bytes of static LDS)
+  if (a.lev_off && (size_t)grid.x * grid.y <= kTmFewChunks && lds_mw <= 160 * 1024 - 256) {
+    // few chunks (the drop-in env): kTmWaves waves per chunk, the levels' offsets in LDS
+    for (const void* f : {reinterpret_cast<const void*>(&cov_time_matrix_mw_kernel<V, false>),
+                          reinterpret_cast<const void*>(&cov_time_matrix_mw_kernel<V, true>)}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((cov_time_matrix_mw_kernel<V, false>), grid, dim3(kTmLanes * kTmWaves), lds_mw, s, a, a.sched);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((cov_time_matrix_mw_kernel<V, true>), grid, dim3(kTmLanes * kTmWaves), lds_mw, s, a, a.sched);
+    return hipGetLastError();
+  }
   for (const void* f : {reinterpret_cast<const void*>(&cov_time_matrix_kernel<V, false>),
                         reinterpret_cast<const void*>(&cov_time_matrix_kernel<V, true>)}) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

@@ -244,6 +244,8 @@ struct CovTmArgs {
   int32_t* nlev;             // (B) schedule levels
   uint8_t* overflow;         // (B) the uint8 pass could not bound an entry: rerun wide
   int sched_stride;
+  int32_t* lev_off;          // (B,lev_stride) each level's first schedule slot, then nslots
+  int lev_stride;
   // greedy lists (cov_greedy_list_kernel), when Tmax <= kGreedyListMaxT
   const uint8_t* wide;       // (B) which cost form holds the env's matrix
   const int32_t* nbr;        // (B,Tmax,4)
