@@ -137,6 +137,39 @@ def test_time_matrix_horizons_vs_oracle(horizon, which):
     h.close()
 
 
+def _lattice(n):
+    xs, ys = np.meshgrid(np.arange(n) * 5.5, np.arange(n) * 5.5)
+    return np.stack([xs.ravel(), ys.ravel()], axis=1)
+
+
+@pytest.mark.parametrize("case", ["one_env_676", "one_env_900", "batch_28", "batch_30"])
+def test_time_matrix_wave_forms_vs_oracle(case):
+    """Both forms of the time-matrix passes against the oracle: four waves per 64-source
+    chunk when a launch has at most 256 chunks and their LDS fits (one env of 676 targets;
+    28 envs of a 552-target map: 252 chunks), one wave per chunk otherwise (900 targets: the
+    predecessors no longer fit in LDS beside the entries; 30 envs: 270 chunks)."""
+    if case.startswith("one_env"):
+        targets = _lattice(26 if case.endswith("676") else 30)
+        B = 1
+    else:
+        from gym_flock.envs.spatial.maps import generate_targets
+        np.random.seed(21)
+        targets = generate_targets()
+        B = int(case.split("_")[1])
+    T = len(targets)
+    R, M = 8, T + 8 + 2
+    h = nat.CoverageHandle(R, B, M, horizon=-1)
+    for b in range(B):
+        h.set_targets(targets, env=b)
+    o = oc.CoverageOracle(targets, R, M)
+    ec, ep = oc.time_matrix(T, o.motion[0] - R, o.motion[1] - R, horizon=-1)
+    for b in sorted({0, B - 1}):
+        cost, prev = h.time_matrix(b, T)
+        np.testing.assert_array_equal(cost, ec)
+        np.testing.assert_array_equal(prev, ep)
+    h.close()
+
+
 def _greedy_phase(v, maps, R, M, seed, steps):
     B = len(maps)
     start, visited = v.reset(seed=seed)
