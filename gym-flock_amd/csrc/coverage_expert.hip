@@ -37,10 +37,10 @@ constexpr int kMaxCost = 1000;          // MAX_COST :68
 
 // Conflict levels of one env's motion-edge list, then the batched schedule: sched[b]
 // holds nslots[b] (a multiple of kBatch) words s | q << 16 (target-local), level by
-// level, no-op slots s = q = T (the dummy column). The levels are one serial pass over
-// the list (lane 0, everything in LDS: each edge is one round of four LDS loads); the
-// counts, offsets and the scatter run on the whole wave. Edges of one level are mutually
-// independent, so their order inside the level does not change any result.
+// level, no-op slots s = q = T (the dummy column). The levels are computed 64 edges at a
+// time (below); the counts, offsets and the scatter run on the whole wave. Edges of one
+// level are mutually independent, so their order inside the level does not change any
+// result.
 __global__ __launch_bounds__(64) void cov_tm_schedule_kernel(CovTmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = a.envs[blockIdx.x];
@@ -59,21 +59,36 @@ __global__ __launch_bounds__(64) void cov_tm_schedule_kernel(CovTmArgs a) {
   for (int k = lane; k <= E; k += 64) fill[k] = 0;
   for (int e = lane; e < E; e += 64) sq[e] = (uint32_t)(snd[e] - R) | ((uint32_t)(rcv[e] - R) << 16);
   __syncthreads();
-  if (lane == 0) {
-    int nlev = 0;
-    for (int e = 0; e < E; ++e) {
-      const uint32_t w = sq[e];
-      const int s = w & 0xFFFF, q = w >> 16;
-      const int ws = lw[s], wq = lw[q], rq = lr[q], rs = lr[s];
-      const int L = max(max(ws, wq), rq) + 1;  // after every conflicting edge
-      level[e] = L;
-      lw[q] = L;  // L > lw[q], lr[q]
-      lr[q] = L;
-      lr[s] = max(rs, L);  // (s == q never: no self edges; the store to q comes first)
-      nlev = max(nlev, L);
+  // 64 edges at a time, lane i taking edge e0 + i: its level from the columns' state
+  // before the window, then raised past every earlier edge of the window it conflicts
+  // with, in window order (a broadcast per edge); the window's levels then go into the
+  // columns' state with LDS maxima (order-free). The same levels as one serial pass.
+  int nlev_w = 0;
+  for (int e0 = 0; e0 < E; e0 += 64) {
+    const int e = e0 + lane;
+    const bool ve = e < E;
+    const uint32_t w = ve ? sq[e] : 0xFFFEFFFFu;  // past E: columns no edge has
+    const int s = w & 0xFFFF, q = w >> 16;
+    int L = ve ? max(max(lw[s], lw[q]), lr[q]) + 1 : 0;
+    const int n = min(64, E - e0);
+    for (int j = 0; j + 1 < n; ++j) {
+      const int sj = __builtin_amdgcn_readlane(s, j), qj = __builtin_amdgcn_readlane(q, j);
+      const int Lj = __builtin_amdgcn_readlane(L, j);
+      // edge j writes a column this edge reads or writes, or reads the column it writes
+      if (lane > j && (qj == s || qj == q || sj == q)) L = max(L, Lj + 1);
     }
-    shared2[0] = nlev;
+    __syncthreads();  // every lane has read the state the window started from
+    if (ve) {
+      level[e] = L;
+      atomicMax(&lw[q], L);
+      atomicMax(&lr[s], L);
+      atomicMax(&lr[q], L);
+      nlev_w = max(nlev_w, L);
+    }
+    __syncthreads();
   }
+  for (int o = 32; o >= 1; o >>= 1) nlev_w = max(nlev_w, __shfl_xor(nlev_w, o));
+  if (lane == 0) shared2[0] = nlev_w;
   __syncthreads();
   const int nlev = shared2[0];
   for (int e = lane; e < E; e += 64) atomicAdd(&fill[level[e] - 1], 1);
