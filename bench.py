@@ -880,6 +880,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-controller-line", action="store_true")
     ap.add_argument("--no-packed-line", action="store_true")
+    ap.add_argument("--no-host-actions-line", action="store_true")
     ap.add_argument("--no-knn-line", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the configs[3] (Coverage) and configs[4] (N=8192) sub-objects")
@@ -1016,6 +1017,19 @@ def main():
                          "kernel": "flock_step_kernel<DYN,f32 u> (packed output)"},
             "note": "adjacency as bits (N*ceil(N/64)*8 B) + int32 degree per env instead of the dense "
                     "float32 network; the pair work, not HBM, bounds this mode"}
+
+    # the same step with host actions: the (B,N,2) float32 actions copied from pageable host
+    # memory every step (the PCIe-inclusive rate of a trainer that hands actions over per
+    # step; the headline keeps them resident in HBM)
+    if not args.no_host_actions_line:
+        env.reset(x=x_init)
+        env.step(u)
+        eh, _ = timed(env, ranks, K, lambda s: env.step(u))
+        extra["host_actions"] = {
+            "value": world * B * N * K / eh, "unit": "agent-steps/s", "ms_per_step": 1e3 * eh / K,
+            "ratio_to_plain_step": eh / elapsed, "action_bytes_per_step": int(u.nbytes),
+            "note": "PCIe-inclusive: env.step(u) with a host (B,N,2) float32 action array each step (copied to "
+                    "the device on the handle's stream before the launch); outputs stay in HBM"}
 
     # Flocking-v0 (§8f rank 1): the same step plus the 7-nearest-neighbour observation
     # (flocking.py:20-25), dense network kept; a second handle with n_neighbors=7. The
