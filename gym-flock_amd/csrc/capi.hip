@@ -136,14 +136,19 @@ struct fe_handle {
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
   hipEvent_t ag_ev = nullptr;           // completion of the latest reward all-gather
-  // ring slots a reward gather's staging copy still reads: steps [first, ...) until ev
-  // (an event on the side stream)
+  // ring slots a reward gather's staging copy still reads: steps [first, ...) until the
+  // copy kernel (on the side stream) has stored `seq` into the page-locked word stage_done
   struct RingRead {
     int64_t first;
-    hipEvent_t ev;
+    uint32_t seq;
   };
   std::deque<RingRead> ring_reads;
-  std::vector<hipEvent_t> ev_free;      // recycled RingRead events
+  // the staging copies' completion word: page-locked (mapped, coherent), written by the
+  // copy kernel with a system-scope release after its last read of the ring; never freed
+  // once a communicator was aborted (an abandoned copy may still store into it)
+  uint32_t* stage_done = nullptr;
+  uint32_t* stage_done_dev = nullptr;
+  uint32_t stage_seq = 0;
   int64_t gathered_upto = 0;            // steps before this one were shipped (or skipped)
   bool ag_issued = false;
   int last_count = 0;
@@ -155,6 +160,8 @@ struct fe_handle {
   // fe_debug_comm_gate: a bounded spin kernel on comm_stream, released by this page-locked
   // flag, stands in for a collective whose peer stopped responding (tests only)
   unsigned* gate_flag = nullptr;
+  // fe_debug_comm_state: what the ring-slot reuse and the gathers saw (tests only)
+  int32_t dbg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // fe_step_host*: the launch's completion flag (done_flag.h), allocated on first use: the
   // device counter, the page-locked word and its mapped address
   int32_t* fin_cnt = nullptr;
@@ -397,8 +404,8 @@ void comm_release(fe_handle* h, bool abort) {
     h->comm = nullptr;
     h->comm_stream = nullptr;
     h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = nullptr;
-    h->ring_reads.clear();  // events the side stream may still record: abandoned
-    h->ev_free.clear();
+    h->ring_reads.clear();  // copies the side stream may still run: abandoned, and so
+    h->stage_done = h->stage_done_dev = nullptr;  // is the word they would store into
     h->gsend = h->gather = h->ssend = h->stats_gather = nullptr;
   }
   if (h->comm) {
@@ -415,10 +422,7 @@ void comm_release(fe_handle* h, bool abort) {
       hipEventDestroy(*e);
       *e = nullptr;
     }
-  for (auto& r : h->ring_reads) hipEventDestroy(r.ev);
   h->ring_reads.clear();
-  for (hipEvent_t e : h->ev_free) hipEventDestroy(e);
-  h->ev_free.clear();
   for (double** p : {&h->gsend, &h->gather, &h->ssend, &h->stats_gather})
     if (*p) {
       hipFree(*p);
@@ -446,6 +450,7 @@ void release(fe_handle* h) {
     if (p) hipFree(p);
   if (h->fin_cnt) hipFree(h->fin_cnt);
   if (h->fin_host) hipHostFree(h->fin_host);
+  if (h->stage_done) hipHostFree(h->stage_done);  // (the side stream drained or was never used)
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
@@ -465,6 +470,13 @@ int check_env(const fe_handle* h, int env) {
 double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h->cfg.n_envs; }
 
 int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what);
+int stage_wait(fe_handle* h, uint32_t seq, const char* what);
+
+// Whether the reward gather's staging copy `seq` has finished reading the ring (the copies
+// run in order on the side stream, so the completion word only grows).
+bool stage_complete(const fe_handle* h, uint32_t seq) {
+  return static_cast<int32_t>(__atomic_load_n(h->stage_done, __ATOMIC_ACQUIRE) - seq) >= 0;
+}
 
 int no_comm(const fe_handle* h) {
   return fail(GF_ESTATE, "no communicator (fe_comm_init not called, or it was torn down" +
@@ -483,17 +495,20 @@ int next_reward_slot(fe_handle* h) {
   const int64_t s = h->steps_written;
   h->rslot = static_cast<int>(s % kRewardSlots);
   while (!h->ring_reads.empty() && h->ring_reads.front().first <= s - kRewardSlots) {
-    const hipEvent_t e = h->ring_reads.front().ev;
-    const hipError_t q = hipEventQuery(e);
-    if (q != hipSuccess) {
-      if (q != hipErrorNotReady) return fail_hip("reward gather staging copy", q);
-      if (comm_event_wait(h, e, "reward all-gather staging copy (ring slot reuse)") != GF_OK) {
+    const uint32_t seq = h->ring_reads.front().seq;
+    const bool done = stage_complete(h, seq);
+    h->dbg[0]++;
+    h->dbg[1] = done ? 1 : 0;
+    h->dbg[2] = -1;
+    if (!done) {
+      h->dbg[2] = stage_wait(h, seq, "reward all-gather staging copy (ring slot reuse)");
+      if (h->dbg[2] == GF_ECOMM) {
         h->comm_lost = g_err;  // comm_release emptied ring_reads: the step goes on
         break;
       }
+      if (h->dbg[2] != GF_OK) return h->dbg[2];
     }
     h->ring_reads.pop_front();
-    h->ev_free.push_back(e);
   }
   h->steps_written = s + 1;
   return GF_OK;
@@ -1667,12 +1682,44 @@ int comm_wait(fe_handle* h, Clock::time_point deadline, const char* what) {
 int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what) {
   const auto deadline = deadline_in(h->comm_timeout);
   for (int spin = 0;; ++spin) {
+    h->dbg[7] = spin;
     const hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return GF_OK;
     if (q != hipErrorNotReady) return fail_hip(what, q);
     ncclResult_t st = ncclSuccess;
     ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
     if (r != ncclSuccess) st = r;
+    if (spin == 0) h->dbg[3] = static_cast<int32_t>(st);
+    const bool err = st != ncclSuccess && st != ncclInProgress;
+    if (err || Clock::now() > deadline) {
+      comm_release(h, true);
+      h->comm_lost = std::string(what) + ": " +
+                     (err ? std::string(ncclGetErrorString(st)) : std::string("timed out (a rank stopped responding)")) +
+                     "; communicator aborted";
+      return fail(GF_ECOMM, h->comm_lost);
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+// Wait for the reward gather's staging copy `seq` (its completion word), bounded like
+// comm_event_wait: on expiry or a communicator error the metrics path is torn down
+// (GF_ECOMM); a side stream that finished without the word is a HIP error.
+int stage_wait(fe_handle* h, uint32_t seq, const char* what) {
+  const auto deadline = deadline_in(h->comm_timeout);
+  for (int spin = 0;; ++spin) {
+    h->dbg[7] = spin;
+    if (stage_complete(h, seq)) return GF_OK;
+    if ((spin & 63) == 63) {
+      const hipError_t q = hipStreamQuery(h->comm_stream);
+      if (q == hipSuccess && !stage_complete(h, seq))
+        return fail(GF_EHIP, std::string(what) + ": the side stream finished without the copy's completion word");
+      if (q != hipSuccess && q != hipErrorNotReady) return fail_hip(what, q);
+    }
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
+    if (r != ncclSuccess) st = r;
+    if (spin == 0) h->dbg[3] = static_cast<int32_t>(st);
     const bool err = st != ncclSuccess && st != ncclInProgress;
     if (err || Clock::now() > deadline) {
       comm_release(h, true);
@@ -1709,6 +1756,15 @@ int comm_alloc(fe_handle* h, T** p, size_t count) {
 // and the gather buffers. On failure the caller tears everything down.
 int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
   GF_HIP(hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking));
+  if (!h->stage_done) {
+    void* p = nullptr;
+    GF_HIP(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    h->stage_done = static_cast<uint32_t*>(p);
+    __atomic_store_n(h->stage_done, h->stage_seq, __ATOMIC_SEQ_CST);  // every earlier copy: done
+    void* d = nullptr;
+    GF_HIP(hipHostGetDevicePointer(&d, p, 0));
+    h->stage_done_dev = static_cast<uint32_t*>(d);
+  }
   // every rank's shard size, before any gather pads to the largest
   int32_t* dsz = nullptr;
   if (int rc = dalloc(&dsz, (size_t)nranks)) return rc;
@@ -1860,6 +1916,29 @@ int fe_comm_shard_sizes(fe_handle* h, int32_t* sizes, int32_t* max_envs) {
   return GF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// A reward gather's staging copy on the side stream: steps [s0, s0 + count) of the ring
+// (wrapping) into the padded send block, then `seq` into the page-locked completion word
+// with a system-scope release once every read of the ring has returned.
+__global__ __launch_bounds__(256) void ring_stage_kernel(const double* ring, int B, int s0, int count, double* gs,
+                                                         int W, uint32_t* done, uint32_t seq) {
+  const int n = count * B;
+  for (int k = threadIdx.x; k < n; k += 256) {
+    const int t = k / B, e = k - t * B;
+    gs[(size_t)t * W + e] = ring[(size_t)((s0 + t) % kRewardSlots) * B + e];
+  }
+  __syncthreads();  // every thread's loads returned (its stores used them)
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+}  // namespace
+
+extern "C" {
+
 int fe_allgather_rewards(fe_handle* h) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->comm) return no_comm(h);
@@ -1888,23 +1967,17 @@ int fe_allgather_rewards(fe_handle* h) {
   }
   // the steps' ring slots (two runs when they wrap) into the padded send block, behind
   // the previous collective (which read it) on the same stream
+  // and their completion into the page-locked word the ring-slot reuse polls: the copy
+  // kernel's own store, not an event query ("a step that did not wait")
   double* gs = h->gsend;
   const int s0 = static_cast<int>(first % kRewardSlots);
-  const int n1 = static_cast<int>(std::min<int64_t>(count, kRewardSlots - s0));
-  GF_HIP(hipMemcpy2DAsync(gs, W * 8, h->reward_ring + (size_t)s0 * B, B * 8, B * 8, n1, hipMemcpyDeviceToDevice,
-                          h->comm_stream));
-  if (n1 < count)
-    GF_HIP(hipMemcpy2DAsync(gs + (size_t)n1 * W, W * 8, h->reward_ring, B * 8, B * 8, count - n1,
-                            hipMemcpyDeviceToDevice, h->comm_stream));
-  hipEvent_t rd = nullptr;  // the copy's completion: the slots are free again
-  if (!h->ev_free.empty()) {
-    rd = h->ev_free.back();
-    h->ev_free.pop_back();
-  } else {
-    GF_HIP(hipEventCreateWithFlags(&rd, hipEventDisableTiming));
-  }
-  h->ring_reads.push_back({first, rd});
-  GF_HIP(hipEventRecord(rd, h->comm_stream));
+  const uint32_t seq = ++h->stage_seq;
+  hipLaunchKernelGGL(ring_stage_kernel, dim3(1), dim3(256), 0, h->comm_stream, static_cast<const double*>(h->reward_ring),
+                     static_cast<int>(B), s0, static_cast<int>(count), gs, static_cast<int>(W), h->stage_done_dev, seq);
+  GF_HIP(hipGetLastError());
+  h->ring_reads.push_back({first, seq});
+  h->dbg[4] = static_cast<int32_t>(h->ring_reads.size());
+  h->dbg[5] = stage_complete(h, seq) ? 1 : 0;
   if (int rc = comm_enqueued(h, ncclAllGather(gs, h->gather, (size_t)count * W, ncclFloat64, h->comm, h->comm_stream),
                              "ncclAllGather (rewards)"))
     return rc;
@@ -1971,12 +2044,19 @@ int fe_comm_destroy(fe_handle* h) {
 namespace {
 // fe_debug_comm_gate's kernel: one wave that sleeps until the page-locked flag turns
 // non-zero or `ticks` of the device's wall clock pass (always bounded).
-__global__ __launch_bounds__(64) void comm_gate_kernel(const unsigned* flag, unsigned long long ticks) {
+// flag[1] = 1 once it runs, flag[2] = 1 (opened) or 2 (timed out) as it ends.
+__global__ __launch_bounds__(64) void comm_gate_kernel(unsigned* flag, unsigned long long ticks) {
   const unsigned long long t0 = wall_clock64();
+  if (threadIdx.x == 0) __hip_atomic_store(flag + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned why = 1u;
   while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
-    if (wall_clock64() - t0 > ticks) break;
+    if (wall_clock64() - t0 > ticks) {
+      why = 2u;
+      break;
+    }
     __builtin_amdgcn_s_sleep(127);
   }
+  if (threadIdx.x == 0) __hip_atomic_store(flag + 2, why, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // one process-wide gate flag (fine-grained page-locked memory), never freed: a gate
@@ -2017,10 +2097,24 @@ int fe_debug_comm_gate(fe_handle* h, int close, double max_seconds) {
   GF_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->cfg.device));
   void* df = nullptr;
   GF_HIP(hipHostGetDevicePointer(&df, f, 0));
+  __atomic_store_n(f + 1, 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(f + 2, 0u, __ATOMIC_SEQ_CST);
   __atomic_store_n(f, 0u, __ATOMIC_SEQ_CST);
   const unsigned long long ticks = static_cast<unsigned long long>(max_seconds * 1000.0 * (khz > 0 ? khz : 100000));
-  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, h->comm_stream, static_cast<const unsigned*>(df), ticks);
+  hipLaunchKernelGGL(comm_gate_kernel, dim3(1), dim3(64), 0, h->comm_stream, static_cast<unsigned*>(df), ticks);
   GF_HIP(hipGetLastError());
+  h->dbg[6] = static_cast<int32_t>(hipStreamQuery(h->comm_stream));
+  return GF_OK;
+}
+
+int fe_debug_comm_state(fe_handle* h, int32_t* out) {
+  if (!h || !out) return fail(GF_EINVAL, "null argument");
+  for (int k = 0; k < 8; ++k) out[k] = h->dbg[k];
+  unsigned* f = gate_flag();
+  out[8] = f ? static_cast<int32_t>(__atomic_load_n(f + 1, __ATOMIC_SEQ_CST)) : -1;
+  out[9] = f ? static_cast<int32_t>(__atomic_load_n(f + 2, __ATOMIC_SEQ_CST)) : -1;
+  out[10] = h->comm ? 1 : 0;
+  out[11] = static_cast<int32_t>(h->ring_reads.size());
   return GF_OK;
 }
 

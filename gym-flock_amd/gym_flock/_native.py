@@ -125,6 +125,7 @@ SIGNATURES = {
     "fe_get_gathered_stats": [_P, _P],
     "fe_comm_destroy": [_P],
     "fe_debug_comm_gate": [_P, _I, ctypes.c_double],
+    "fe_debug_comm_state": [_P, _P],
     "fe_runtime_info": [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                         ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, _I, ctypes.c_char_p, _I],
     "fe_set_variant": [_P, _P],
@@ -662,6 +663,16 @@ class FlockHandle:
         """Tests only: hold (close=True) or release the collectives' side stream with a
         bounded spin kernel, as a collective stuck on a dead peer would (fe_debug_comm_gate)."""
         check(self.lib.fe_debug_comm_gate(self.h, int(bool(close)), float(max_seconds)))
+
+    _COMM_STATE = ("reuse_checks", "reuse_copy_done", "reuse_wait_rc", "reuse_async_state", "listed_after_gather",
+                   "gather_copy_done", "gate_stream_query", "wait_polls", "gate_started", "gate_ended",
+                   "comm_live", "listed_now")
+
+    def debug_comm_state(self):
+        """Tests only: what the metrics path saw (fe_debug_comm_state) as a dict."""
+        out = np.zeros(12, np.int32)
+        check(self.lib.fe_debug_comm_state(self.h, ptr(out)))
+        return dict(zip(self._COMM_STATE, (int(v) for v in out)))
 
     def allgather_rewards(self):
         """Enqueue the all-gather of every step's rewards since the previous one."""

@@ -270,6 +270,16 @@ int fe_comm_destroy(fe_handle* h);
  * spins (s_sleep) until close = 0 is called or max_seconds pass, standing in for a
  * collective whose peer stopped responding; close = 0 releases it. Needs fe_comm_init. */
 int fe_debug_comm_gate(fe_handle* h, int close, double max_seconds);
+/* Tests only: what the metrics path saw, out[12]: [0] ring-slot reuse checks that found
+ * a gather's staging copy still listed, [1] whether that copy had stored its completion
+ * word at the last one (1) or not (0), [2] its bounded wait's status (-1: no wait), [3]
+ * the communicator's async state at that wait's first poll, [4] staging copies listed
+ * after the last reward gather, [5] whether its copy was complete right after the
+ * gather was enqueued, [6] hipStreamQuery of the side stream right after the last gate
+ * launch, [7] polls of the last bounded wait, [8] the gate kernel has started (1), [9]
+ * how it ended (0 running, 1 opened, 2 timed out), [10] a communicator is live, [11]
+ * staging copies listed now. */
+int fe_debug_comm_state(fe_handle* h, int32_t* out);
 /* The HIP runtime and RCCL this library is bound to in this process (a process that
  * loaded another copy of either first, e.g. PyTorch's bundled ones, binds that copy):
  * hipRuntimeGetVersion, hipDriverGetVersion (0 without a driver), ncclGetVersion, and the
@@ -314,6 +324,50 @@ int cov_destroy(cov_handle* h);
 /* Targets of one env (env < 0: every env) and its motion graph + static observation
  * (_initialize_graph :529-594, utils._get_graph_edges :8-24), built on the device. */
 int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets);
+
+/* Per-episode target maps, _generate_targets (coverage.py:516-527) as every reset() calls
+ * it (:378-397), with generate_lattice (make_map.py:30-67) and generate_geometric_roads
+ * (make_map.py:207-231). The reference's values: arena (-120, 120, -120, 120) (XMAX/YMAX
+ * :75-76), lattice_spacing DELTA = 5.5 (:61, the lattice vectors :125-128), 12 cities,
+ * world_radius x_max, road_radius and link_radius motion_radius (= res * 1.2), near_radius
+ * motion_radius / 1.4. */
+typedef struct cov_map_config {
+  double x_min, x_max, y_min, y_max; /* the arena: generate_lattice's free_region           */
+  double lattice_spacing;            /* square lattice vectors (-s, 0), (0, -s)             */
+  double world_radius;               /* cities U(-r, r)^2 (make_map.py:208)                 */
+  double road_radius;                /* waypoint spacing along each Delaunay road (:228-229) */
+  double near_radius;                /* lattice points within it of a waypoint (:521)       */
+  double link_radius;                /* the target graph's radius (:523-524)                */
+  int32_t n_cities;                  /* 12 (:518); at most 32                               */
+} cov_map_config;
+#define COV_MAP_SEED   0x1 /* seed env b's map stream as np.random.seed(map_seed + b) first;
+                              otherwise the streams continue from the previous maps, as the
+                              reference's global np.random does from one reset to the next */
+#define COV_MAP_CITIES 0x2 /* the cities are given (host (n_sel, n_cities, 2), the drop-in
+                              env draws them from np.random itself); no stream is used      */
+/* status_out bits (per env) */
+#define COV_MAP_NEAR_DEGENERATE 0x1 /* an orientation or incircle sign of the cities fell
+                                       inside its rounding bound: Qhull decides such sets by
+                                       its own precision handling (parity unpinned)         */
+#define COV_MAP_TOO_MANY        0x2 /* more targets than max_nodes - n_robots              */
+#define COV_MAP_TOO_FEW         0x4 /* fewer targets than robots                           */
+#define COV_MAP_OVERFLOW        0x8 /* more waypoints than the kernel holds                */
+/* New maps on the device for env `env` (env < 0: every env): the cities (drawn on the
+ * device from each env's stream, numpy's legacy uniform, or given), their Delaunay roads,
+ * the lattice points near them and the largest connected component of their radius
+ * graph; then the motion graph and static observation as cov_set_targets builds them.
+ * n_targets_out, status_out (n_sel) and cities_out (n_sel, n_cities, 2) may be NULL. A
+ * map that cannot be used (TOO_MANY / TOO_FEW / OVERFLOW) fails the call with GF_EINVAL,
+ * that env left without a graph; NEAR_DEGENERATE maps are used and reported. */
+int cov_generate_maps(cov_handle* h, const cov_map_config* mc, int env, uint64_t map_seed, const double* cities,
+                      int flags, int32_t* n_targets_out, int32_t* status_out, double* cities_out);
+/* The targets (n_targets, 2) of env `env`'s current map. */
+int cov_get_targets(cov_handle* h, int env, double* targets);
+/* Host only (no device): generate_lattice's points (make_map.py:30-67) for mc, [y, x]
+ * columns in its order, into xy (capacity *n points; *n receives the count, also when
+ * the capacity is short, which fails with GF_EINVAL). xy may be NULL to query *n. */
+int cov_map_lattice(const cov_map_config* mc, double* xy, int32_t* n);
+
 /* reset() after its random draws (:405-424): start[B][R] target-local start nodes,
  * visited[B][max_nodes-R] (1 = visited); computes reset's observation (:424). */
 int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited);

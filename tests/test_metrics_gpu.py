@@ -164,11 +164,16 @@ def test_steps_never_wait_behind_a_stuck_collective():
     v.h.debug_comm_gate(True, max_seconds=30.0)
     opener = None
     try:
+        t_gate = time.monotonic()  # the gate kernel runs before anything is queued behind it
+        while v.h.debug_comm_state()["gate_started"] != 1 and time.monotonic() - t_gate < 10.0:
+            time.sleep(0.001)
+        st_gate = v.h.debug_comm_state()
         hist = []
         for _ in range(8):  # steps 8-15
             v.step(u)
             hist.append(v.rewards())
         g.issue()  # its staging copy and collective queue behind the gate
+        st_issue = v.h.debug_comm_state()
         t0 = time.monotonic()
         for _ in range(56):  # steps 16-71: no ring slot of the pending gather is reused
             v.step(u)
@@ -180,10 +185,17 @@ def test_steps_never_wait_behind_a_stuck_collective():
         v.step(u)  # step 72 reuses step 8's slot: waits (host, bounded) for the staging copy
         v.rewards()
         waited = time.monotonic() - t1
+        st_reuse = v.h.debug_comm_state()
     finally:
         if opener is not None:
             opener.join()
         v.h.debug_comm_gate(False)
+    print("gate:", st_gate, "\nissue:", st_issue, "\nreuse:", st_reuse, "\nwaited %.3f s" % waited)
+    assert st_gate["gate_started"] == 1 and st_gate["gate_ended"] == 0, st_gate
+    assert st_issue["gather_copy_done"] == 0, st_issue     # queued behind the gate
+    assert st_reuse["reuse_copy_done"] == 0, st_reuse      # still behind it 56 steps on
+    assert st_reuse["reuse_wait_rc"] == 0 and st_reuse["comm_live"] == 1, st_reuse
+    assert st_reuse["gate_ended"] == 1, st_reuse
     assert free_run < 5.0, "steps waited %.1f s behind the gated collective" % free_run
     assert 1.0 < waited < 15.0, waited
     np.testing.assert_array_equal(g.result(), np.array(hist))
