@@ -303,7 +303,7 @@ def bench_config4(args, with_greedy=False):
     max_nodes 1000 (the reference needs nearby_starts=False and max_nodes=1000 at this
     size, SURVEY.md finding 7). All envs share one generated map (global seed 8);
     starts, unvisited sets and actions differ per env; actions stay resident in HBM."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     from gym_flock.vec import VecCoverage
     # a Coverage step is ~9 us of latency-bound work: at least 1000 steps and 20 warm-up
     # steps per window, so neither the window's fixed start/end cost (~0.1 ms) nor the
@@ -345,7 +345,57 @@ def bench_config4(args, with_greedy=False):
     if with_greedy:
         out["greedy_expert"] = bench_greedy(v, targets, R, M, B, K, args)
     v.close()
+    out["distinct_maps"] = bench_config4_distinct_maps(args, R, B, M)
     return out
+
+
+def bench_config4_distinct_maps(args, R, B, M, episodes=8):
+    """Config 4 as the reference's reset() semantics imply: every env its own map (drawn on
+    the device, cov_generate_maps, env b's stream seeded np.random.seed(8 + b)), episodes of
+    the reference's EPISODE_LENGTH = 75 steps with random actions resident in HBM, each
+    episode's reset (new starts and unvisited sets; the maps stay) outside the timed
+    windows; then the same windows with one map shared by every env (the headline's
+    workload) for the comparison. Also: a new map for all envs, timed."""
+    from gym_flock.vec import VecCoverage
+    rs = np.random.RandomState(7)
+
+    def episodes_ms(v):
+        v.reset(seed=0)
+        v.set_actions(rs.randint(0, 4, size=(B, R)))
+        clock_warmup(lambda: v.step(resident=True), v.sync, 50.0)
+        el, k = 0.0, 0
+        for e in range(episodes):
+            v.reset(seed=1 + e)
+            v.set_actions(rs.randint(0, 4, size=(B, R)))
+            v.sync()
+            t0 = time.perf_counter()
+            for _ in range(75):
+                v.step(resident=True)
+            v.sync()
+            el += time.perf_counter() - t0
+            k += 75
+        return 1e3 * el / k
+
+    v = VecCoverage(B, R, max_nodes=M, episode_length=75)
+    n, st = v.generate_maps(map_seed=8)
+    v.sync()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        v.generate_maps()  # the next map of every stream: what each reference reset() draws
+    map_ms = 1e3 * (time.perf_counter() - t0) / 3
+    n, st = v.generate_maps(map_seed=8)
+    distinct = episodes_ms(v)
+    v.set_targets(v.h.targets(0, int(n[0])))  # env 0's map for every env
+    shared = episodes_ms(v)
+    v.close()
+    return {"step_ms_distinct_maps": distinct, "step_ms_shared_map": shared,
+            "robot_steps_per_s_distinct_maps": R * B / (distinct * 1e-3),
+            "n_targets_min_mean_max": [int(n.min()), float(n.mean()), int(n.max())],
+            "map_ms_all_envs": map_ms, "episodes": episodes,
+            "note": "per step, %d episodes of 75 resident-action steps, resets untimed; distinct: env b's map from "
+                    "np.random.seed(8 + b)'s stream; shared: env 0's map for all; map_ms_all_envs: one new map "
+                    "for all %d envs (cities, Delaunay roads, lattice filter, largest component and the motion "
+                    "graph, on the device)" % (episodes, B)}
 
 
 def bench_dropin(args):
@@ -481,9 +531,12 @@ def bench_dropin_coverage(args):
                 env = CoverageEnv(n_robots=R, nearby_starts=nearby, max_nodes=M)
                 env.fetch_mode = mode
                 env.seed(3)
-                steps, el, first, el_first = 0, 0.0, 0, 0.0
+                steps, el, first, el_first, el_reset = 0, 0.0, 0, 0.0, 0.0
                 for ep in range(episodes + 1):  # the first episode warms up (not counted)
-                    env.reset()
+                    t0 = time.perf_counter()
+                    env.reset()  # a new map (cities from np.random, the rest on the device)
+                    if ep > 0:
+                        el_reset += time.perf_counter() - t0
                     done, k = False, 0
                     while not done:
                         t0 = time.perf_counter()
@@ -498,7 +551,8 @@ def bench_dropin_coverage(args):
                                 el_first += dt
                         k += 1
                 env.close()
-                r = {"step_ms": 1e3 * el / steps, "steps": steps}
+                r = {"step_ms": 1e3 * el / steps, "steps": steps, "reset_ms": 1e3 * el_reset / episodes,
+                     "episode_ms_with_reset": 1e3 * (el + el_reset) / episodes}
                 if pol == "greedy":  # the first step of an episode builds the new map's time matrix
                     r["step_ms_after_first"] = 1e3 * (el - el_first) / max(1, steps - first)
                     r["first_step_ms"] = 1e3 * el_first / max(1, first)
@@ -506,7 +560,7 @@ def bench_dropin_coverage(args):
         if not args.no_cpu_baseline:
             from oracle import coverage as oc
             from oracle.cpu_ref_coverage import CpuCoverage
-            from gym_flock.envs.spatial.maps import generate_targets
+            from oracle.maps_host import generate_targets
             np.random.seed(8)
             targets = generate_targets()
             T = len(targets)
@@ -534,9 +588,11 @@ def bench_dropin_coverage(args):
                                             "kind": "port (oracle/coverage.py, NumPy, 1 thread)"}
         out["r%d" % R] = row
     out["note"] = ("per call of env.step(env.controller(...)) on one CoverageEnv, whole episodes after one warm-up "
-                   "episode, resets untimed; the map is regenerated at every reset as in the reference, so a greedy "
-                   "episode's first step builds its time matrix (first_step_ms); max_nodes 1000 (the generated maps "
-                   "hold up to ~560 targets)")
+                   "episode; step_ms leaves the resets out, reset_ms is reset() alone (a new map: its cities from "
+                   "np.random, the roads, targets and motion graph on the device; then the start draws) and "
+                   "episode_ms_with_reset the whole episode as the reference's driver loop (test.py:43-74) runs it; "
+                   "a greedy episode's first step builds the new map's time matrix (first_step_ms); max_nodes 1000 "
+                   "(the generated maps hold up to ~650 targets)")
     return out
 
 
@@ -621,9 +677,32 @@ def bench_greedy(v, targets, R, M, B, K, args):
     t0 = time.perf_counter()
     v.reset(seed=500, draws="host")
     reset_host = time.perf_counter() - t0
+    # the same episodes with a new map for every env at every reset, as each reference
+    # reset() draws one (coverage.py:378-397): the maps, their motion graphs and time
+    # matrices (built on the episode's first expert step), the reset draws and 75 expert
+    # steps, for 512 distinct maps per episode
+    v.generate_maps(map_seed=8)
+    v.reset(seed=699)
+    v.step(greedy=True)
+    v.sync()
+    t0 = time.perf_counter()
+    for e in range(3):
+        v.reset(seed=700 + e, new_maps=True)
+        for _ in range(75):
+            v.step(greedy=True)
+    v.sync()
+    episode_new = (time.perf_counter() - t0) / 3
+    t0 = time.perf_counter()
+    v.reset(seed=710, new_maps=True)
+    v.h.controller_greedy(fetch=False)  # the time matrices and greedy lists of the new maps
+    v.sync()
+    reset_tm_new = time.perf_counter() - t0
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
            "reset_ms_all_envs": 1e3 * reset_dev, "reset_ms_all_envs_host_draws": 1e3 * reset_host,
            "expert_episode_ms_all_envs": 1e3 * episode, "expert_env_episodes_per_s": B / episode,
+           "expert_episode_ms_all_envs_new_maps": 1e3 * episode_new,
+           "expert_env_episodes_per_s_new_maps": B / episode_new,
+           "new_maps_reset_and_time_matrices_ms_all_envs": 1e3 * reset_tm_new,
            "expert_step_ms_in_episodes": 1e3 * ep_t / ep_k,
            "expert_robot_steps_per_s_in_episodes": R * B * ep_k / ep_t,
            "expert_step_ms_in_episodes_fallback_action0": 1e3 * z_t / ep_k,

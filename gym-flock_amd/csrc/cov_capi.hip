@@ -105,6 +105,20 @@ struct cov_handle {
   // COV_GREEDY_RNG: every env's np_random stream (cov_set_rng; allocated on first use)
   uint32_t* mt_key = nullptr;  // (B,624)
   int32_t* mt_pos = nullptr;   // (B)
+  // cov_generate_maps (allocated on first use): each env's map stream (the reference's
+  // global np.random), its cities, the kernel's per-env outputs, and the lattice of the
+  // last map configuration (the same for every env)
+  uint32_t* map_key = nullptr;   // (B,624)
+  int32_t* map_pos = nullptr;    // (B)
+  bool map_seeded = false;
+  double* map_cities = nullptr;  // (B, kMapMaxCities, 2)
+  int32_t* map_nraw = nullptr;   // (B)
+  int32_t* map_status = nullptr; // (B)
+  double2* lat = nullptr;        // (L)
+  int32_t* lat_cell = nullptr;   // (L)
+  int32_t* lat_grid = nullptr;   // (NI * NJ)
+  int lat_L = 0, lat_NI = 0, lat_NJ = 0;
+  double lat_key[5] = {0, 0, 0, 0, 0};  // x_min, x_max, y_min, y_max, spacing of `lat`
 };
 
 namespace {
@@ -138,7 +152,8 @@ void cov_release(cov_handle* h) {
                   a.step_counter, a.dirty, h->actions, a.reward, a.done, a.nodes, a.edges, a.senders,
                   a.receivers, a.obs_step, a.axy, a.nrec, h->err, h->start, h->visited0, h->envsel, h->tm_cost, h->tm_cost8, h->tm_wide, h->tm_prevT, h->tm_glist, h->tm_glen,
                   h->tm_flags, h->needs_random, h->tm_envsel, h->tm_sched, h->tm_lev, h->tm_nslots, h->tm_nlev, h->tm_overflow, h->scratch,
-                  h->goff, h->mt_key, h->mt_pos};
+                  h->goff, h->mt_key, h->mt_pos, h->map_key, h->map_pos, h->map_cities, h->map_nraw,
+                  h->map_status, h->lat, h->lat_cell, h->lat_grid};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
@@ -308,6 +323,86 @@ void graph_sizes(const cov_handle* h, bool mask_all, std::vector<int32_t>& ne, s
   }
 }
 
+// Python's float floor division (numpy floor_divide on float64), for generate_lattice's
+// `//` (make_map.py:40, :45-46).
+double py_floordiv(double a, double b) {
+  double mod = std::fmod(a, b);
+  double div = (a - mod) / b;
+  if (mod != 0.0 && ((b < 0) != (mod < 0))) div -= 1.0;
+  if (div == 0.0) return std::copysign(0.0, a / b);
+  double fl = std::floor(div);
+  if (div - fl > 0.5) fl += 1.0;
+  return fl;
+}
+
+int check_map_config(const cov_map_config* mc) {
+  if (!mc) return cfail(GF_EINVAL, "null map configuration");
+  if (!(mc->x_max > mc->x_min) || !(mc->y_max > mc->y_min)) return cfail(GF_EINVAL, "map: empty arena");
+  if (!(mc->lattice_spacing > 0) || !(mc->world_radius > 0) || !(mc->road_radius > 0) || !(mc->near_radius > 0) ||
+      !(mc->link_radius > 0))
+    return cfail(GF_EINVAL, "map: spacing and radii must be positive");
+  if (mc->n_cities < 3 || mc->n_cities > gf::kMapMaxCities) return cfail(GF_EINVAL, "map: n_cities must be in [3, 32]");
+  return GF_OK;
+}
+
+// generate_lattice (make_map.py:30-67) with the square lattice vectors (-s, 0), (0, -s)
+// (coverage.py:125-128): the points in its order as [y, x], and each point's cell
+// i * NJ + j in the (arange(-nx, nx), arange(-ny, nx)) grid it sheared.
+void build_lattice(const cov_map_config* mc, std::vector<double>& xy, std::vector<int32_t>& cell, int* NI, int* NJ) {
+  const double s = mc->lattice_spacing;
+  const double w = mc->x_max - mc->x_min, hgt = mc->y_max - mc->y_min;
+  const double cx = py_floordiv(w, 2.0), cy = py_floordiv(hgt, 2.0);
+  const double nx = py_floordiv(w, s), ny = py_floordiv(hgt, s);
+  const int ni = static_cast<int>(std::ceil(nx - -nx)), nj = static_cast<int>(std::ceil(nx - -ny));  // np.arange lengths
+  xy.clear();
+  cell.clear();
+  for (int i = 0; i < ni; ++i) {
+    const double xs = -nx + i;
+    for (int j = 0; j < nj; ++j) {
+      const double ys = -ny + j;
+      const double xl = -s * xs + 0.0 * ys, yl = 0.0 * xs + -s * ys;
+      if (xl < w / 2.0 && xl > -w / 2.0 && yl < hgt / 2.0 && yl > -hgt / 2.0) {
+        xy.push_back(yl + (cy + mc->y_min));
+        xy.push_back(xl + (cx + mc->x_min));
+        cell.push_back(i * nj + j);
+      }
+    }
+  }
+  *NI = ni;
+  *NJ = nj;
+}
+
+// The lattice of mc on the device (rebuilt when the arena or spacing changes).
+int ensure_lattice(cov_handle* h, const cov_map_config* mc) {
+  const double key[5] = {mc->x_min, mc->x_max, mc->y_min, mc->y_max, mc->lattice_spacing};
+  if (h->lat && std::memcmp(key, h->lat_key, sizeof(key)) == 0) return GF_OK;
+  std::vector<double> xy;
+  std::vector<int32_t> cell;
+  int NI = 0, NJ = 0;
+  build_lattice(mc, xy, cell, &NI, &NJ);
+  const int L = static_cast<int>(cell.size());
+  if (L < 1) return cfail(GF_EINVAL, "map: the lattice has no point in the arena");
+  if ((size_t)NI * NJ > (size_t)1 << 26) return cfail(GF_EINVAL, "map: lattice grid too large");
+  for (void* p : {static_cast<void*>(h->lat), static_cast<void*>(h->lat_cell), static_cast<void*>(h->lat_grid)})
+    if (p) CV_HIP(hipFree(p));
+  h->lat = nullptr;
+  h->lat_cell = h->lat_grid = nullptr;
+  std::vector<int32_t> grid((size_t)NI * NJ, -1);
+  for (int l = 0; l < L; ++l) grid[cell[l]] = l;
+  int rc;
+  if ((rc = calloc_dev(&h->lat, (size_t)L)) || (rc = calloc_dev(&h->lat_cell, (size_t)L)) ||
+      (rc = calloc_dev(&h->lat_grid, (size_t)NI * NJ)))
+    return rc;
+  CV_HIP(hipMemcpy(h->lat, xy.data(), (size_t)L * 16, hipMemcpyHostToDevice));
+  CV_HIP(hipMemcpy(h->lat_cell, cell.data(), (size_t)L * 4, hipMemcpyHostToDevice));
+  CV_HIP(hipMemcpy(h->lat_grid, grid.data(), grid.size() * 4, hipMemcpyHostToDevice));
+  h->lat_L = L;
+  h->lat_NI = NI;
+  h->lat_NJ = NJ;
+  std::memcpy(h->lat_key, key, sizeof(key));
+  return GF_OK;
+}
+
 int put(cov_handle* h, void* dst, const void* src, size_t bytes, bool dev_dst, bool dev_src) {
   if (!dst || !bytes) return GF_OK;
   const hipMemcpyKind k = dev_dst ? (dev_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
@@ -404,6 +499,139 @@ int cov_set_targets(cov_handle* h, int env, int n_targets, const double* targets
   h->tm_ready = false;
   h->has_graph = true;
   for (int b = 0; b < B; ++b) h->has_graph = h->has_graph && h->ntg_host[b] > 0;
+  return GF_OK;
+}
+
+int cov_map_lattice(const cov_map_config* mc, double* xy, int32_t* n) {
+  if (!n) return cfail(GF_EINVAL, "null count");
+  if (int rc = check_map_config(mc)) return rc;
+  std::vector<double> pts;
+  std::vector<int32_t> cell;
+  int NI = 0, NJ = 0;
+  build_lattice(mc, pts, cell, &NI, &NJ);
+  const int32_t cap = *n;
+  *n = static_cast<int32_t>(cell.size());
+  if (!xy) return GF_OK;
+  if (cap < *n) return cfail(GF_EINVAL, "lattice: the output holds fewer points than the lattice has");
+  std::memcpy(xy, pts.data(), pts.size() * sizeof(double));
+  return GF_OK;
+}
+
+int cov_generate_maps(cov_handle* h, const cov_map_config* mc, int env, uint64_t map_seed, const double* cities,
+                      int flags, int32_t* n_targets_out, int32_t* status_out, double* cities_out) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (int rc = check_map_config(mc)) return rc;
+  if (flags & ~(COV_MAP_SEED | COV_MAP_CITIES)) return cfail(GF_EINVAL, "flags: COV_MAP_SEED | COV_MAP_CITIES");
+  const bool given = flags & COV_MAP_CITIES;
+  if (given && !cities) return cfail(GF_EINVAL, "COV_MAP_CITIES needs the cities");
+  const int B = h->cfg.n_envs, NC = mc->n_cities;
+  if (env >= B) return cfail(GF_EINVAL, "env index out of range");
+  if (!given && (flags & COV_MAP_SEED) && map_seed + (uint64_t)B > 0x100000000ull)
+    return cfail(GF_EINVAL, "map_seed + n_envs must fit in 32 bits (np.random.seed)");
+  if (!given && !(flags & COV_MAP_SEED) && !h->map_seeded)
+    return cfail(GF_ESTATE, "the envs' map streams were never seeded (COV_MAP_SEED)");
+  if (int rc = use(h)) return rc;
+  int rc;
+  if (!h->map_cities) {
+    if ((rc = calloc_dev(&h->map_key, (size_t)B * gf::kMtN)) || (rc = calloc_dev(&h->map_pos, (size_t)B)) ||
+        (rc = calloc_dev(&h->map_cities, (size_t)B * gf::kMapMaxCities * 2)) || (rc = calloc_dev(&h->map_nraw, (size_t)B)) ||
+        (rc = calloc_dev(&h->map_status, (size_t)B)))
+      return rc;
+  }
+  if ((rc = ensure_lattice(h, mc))) return rc;
+  // waypoints: the cities plus at most int(dist / road_radius) per Delaunay edge (at most
+  // 3 NC - 6 of them, none longer than the cities' square's diagonal), within the LDS left
+  const double diag = 2.0 * std::sqrt(2.0) * mc->world_radius;
+  const double wbound = NC + (3.0 * NC - 6.0) * (std::floor(diag / mc->road_radius) + 1.0);
+  const size_t lds_free = 150 * 1024 - (size_t)h->lat_L * 12;
+  if ((size_t)h->lat_L * 12 + 64 * 16 > 150 * 1024) return cfail(GF_EINVAL, "map: lattice too large for the LDS");
+  const int wcap = static_cast<int>(std::min<double>(wbound, (double)(lds_free / 16)));
+  const int b0 = env < 0 ? 0 : env, b1 = env < 0 ? B : env + 1, nsel = b1 - b0;
+  std::vector<int32_t> sel;
+  for (int b = b0; b < b1; ++b) sel.push_back(b);
+  CV_HIP(hipMemcpyAsync(h->envsel, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, h->stream));
+  gf::CovMapArgs m{};
+  m.n_sel = nsel;
+  m.envs = h->envsel;
+  m.R = h->a.R;
+  m.Tmax = h->a.Tmax;
+  m.NC = NC;
+  m.lo = -mc->world_radius;
+  m.range = mc->world_radius - -mc->world_radius;  // uniform(low, high): high - low
+  m.road_radius = mc->road_radius;
+  m.near_radius = mc->near_radius;
+  m.link_radius = mc->link_radius;
+  m.L = h->lat_L;
+  m.lat = h->lat;
+  m.lat_cell = h->lat_cell;
+  m.cell = h->lat_grid;
+  m.NI = h->lat_NI;
+  m.NJ = h->lat_NJ;
+  m.K = static_cast<int>(std::floor(mc->link_radius / mc->lattice_spacing)) + 1;
+  m.wcap = wcap;
+  m.cities = h->map_cities;
+  m.mt_key = h->map_key;
+  m.mt_pos = h->map_pos;
+  m.seed0 = static_cast<uint32_t>(map_seed);
+  m.seed = (flags & COV_MAP_SEED) ? 1 : 0;
+  m.tgt = h->tgt;
+  m.ntg = h->ntg;
+  m.nraw = h->map_nraw;
+  m.status = h->map_status;
+  hipError_t e = hipSuccess;
+  if (given) {
+    CV_HIP(hipMemcpy2DAsync(h->map_cities + (size_t)b0 * gf::kMapMaxCities * 2, gf::kMapMaxCities * 16, cities,
+                            (size_t)NC * 16, (size_t)NC * 16, nsel, hipMemcpyHostToDevice, h->stream));
+  } else {
+    e = gf::launch_cov_map_cities(m, h->stream);
+    if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_map_cities_kernel: ") + hipGetErrorString(e));
+    if (flags & COV_MAP_SEED) h->map_seeded = true;
+  }
+  e = gf::launch_cov_map(m, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_map_kernel: ") + hipGetErrorString(e));
+  e = gf::launch_cov_graph(h->a, h->envsel, nsel, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_graph_kernel: ") + hipGetErrorString(e));
+  std::vector<int32_t> nraw(nsel), st(nsel), ntg(B);
+  CV_HIP(hipMemcpyAsync(nraw.data(), h->map_nraw + b0, nsel * 4, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipMemcpyAsync(st.data(), h->map_status + b0, nsel * 4, hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipMemcpyAsync(ntg.data(), h->ntg, B * 4, hipMemcpyDeviceToHost, h->stream));
+  if (cities_out)
+    CV_HIP(hipMemcpy2DAsync(cities_out, (size_t)NC * 16, h->map_cities + (size_t)b0 * gf::kMapMaxCities * 2,
+                            gf::kMapMaxCities * 16, (size_t)NC * 16, nsel, hipMemcpyDeviceToHost, h->stream));
+  if (int rc2 = check_err(h)) return rc2;  // synchronises; motion-graph errors (degree > 4, edges)
+  CV_HIP(hipMemcpy(h->n_motion_host.data(), h->a.n_motion, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::string bad;
+  for (int k = 0; k < nsel; ++k) {
+    const int b = b0 + k;
+    h->ntg_host[b] = ntg[b];
+    h->tm_valid[b] = 0;
+    if (n_targets_out) n_targets_out[k] = nraw[k];
+    if (status_out) status_out[k] = st[k];
+    if (bad.empty() && (st[k] & (gf::kMapTooMany | gf::kMapTooFew | gf::kMapOverflow))) {
+      bad = "env " + std::to_string(b) + ": ";
+      if (st[k] & gf::kMapTooMany)
+        bad += "the map has " + std::to_string(nraw[k]) + " targets, more than max_nodes - n_robots = " +
+               std::to_string(h->a.Tmax) + " (the reference's padded observation cannot hold them)";
+      else if (st[k] & gf::kMapTooFew)
+        bad += "the map has " + std::to_string(nraw[k]) + " targets, fewer than the robots";
+      else
+        bad += "more road waypoints than the map kernel holds";
+    }
+  }
+  h->tm_ready = false;
+  h->has_graph = true;
+  for (int b = 0; b < B; ++b) h->has_graph = h->has_graph && h->ntg_host[b] > 0;
+  if (!bad.empty()) return cfail(GF_EINVAL, "cov_generate_maps: " + bad);
+  return GF_OK;
+}
+
+int cov_get_targets(cov_handle* h, int env, double* targets) {
+  if (!h || !targets || env < 0 || env >= h->cfg.n_envs) return cfail(GF_EINVAL, "bad argument");
+  if (h->ntg_host[env] < 1) return cfail(GF_ESTATE, "the env has no target map");
+  if (int rc = use(h)) return rc;
+  CV_HIP(hipMemcpyAsync(targets, h->tgt + (size_t)env * h->a.Tmax * 2, (size_t)h->ntg_host[env] * 16,
+                        hipMemcpyDeviceToHost, h->stream));
+  CV_HIP(hipStreamSynchronize(h->stream));
   return GF_OK;
 }
 

@@ -288,6 +288,39 @@ hipError_t launch_cov_greedy(const CovGreedyArgs& a, hipStream_t s);
 // the greedy lists of the selected envs (after their time matrices)
 hipError_t launch_cov_greedy_lists(const CovTmArgs& a, int n_envs_sel, hipStream_t s);
 
+// Per-episode target maps (coverage_maps.hip; coverage.py:516-527, make_map.py:30-67,
+// :207-231). One workgroup per selected env.
+struct CovMapArgs {
+  int n_sel;
+  const int32_t* envs;       // (n_sel) env of each workgroup
+  int R, Tmax;
+  int NC;                    // cities per map (<= kMapMaxCities)
+  double lo, range;          // cities: lo + range * random_sample (np.random.uniform)
+  double road_radius;        // waypoint spacing along each road (motion_radius)
+  double near_radius;        // lattice points within it of a waypoint (motion_radius / 1.4)
+  double link_radius;        // target radius graph (motion_radius)
+  int L;                     // lattice points
+  const double2* lat;        // (L) generate_lattice's points, [y, x] columns
+  const int32_t* lat_cell;   // (L) each point's cell gi * NJ + gj
+  const int32_t* cell;       // (NI * NJ) the lattice point of each cell, or -1
+  int NI, NJ, K;             // cell grid, cells searched either side for a link
+  int wcap;                  // waypoints the LDS holds
+  double* cities;            // (B, kMapMaxCities, 2): drawn by cov_map_cities_kernel or uploaded
+  uint32_t* mt_key;          // (B, 624) each env's map stream (the reference's global np.random)
+  int32_t* mt_pos;           // (B)
+  uint32_t seed0;            // seed: stream b := RandomState(seed0 + b)
+  int seed;
+  double* tgt;               // (B, Tmax, 2) out: the largest component's points, lattice order
+  int32_t* ntg;              // (B) out: targets (0 when the map is refused)
+  int32_t* nraw;             // (B) out: the largest component's size
+  int32_t* status;           // (B) out: kMapNearDegenerate | kMapTooMany | kMapTooFew | kMapOverflow
+};
+constexpr int kMapMaxCities = 32;
+constexpr int32_t kMapNearDegenerate = 1, kMapTooMany = 2, kMapTooFew = 4, kMapOverflow = 8;
+size_t cov_map_lds_bytes(int L, int wcap);
+hipError_t launch_cov_map_cities(const CovMapArgs& a, hipStream_t s);
+hipError_t launch_cov_map(const CovMapArgs& a, hipStream_t s);
+
 size_t cov_step_lds_bytes(int R, int M);
 // Observation wire formats: the flat FlattenDictWrapper rows (B, 15M+1) and the
 // batched unpack_obs graph tuple (edges compacted at off[b]).

@@ -59,6 +59,41 @@ class CovConfig(ctypes.Structure):
                 ("device", ctypes.c_int32), ("horizon", ctypes.c_int32)]
 
 
+class CovMapConfig(ctypes.Structure):
+    _fields_ = [("x_min", ctypes.c_double), ("x_max", ctypes.c_double), ("y_min", ctypes.c_double),
+                ("y_max", ctypes.c_double), ("lattice_spacing", ctypes.c_double),
+                ("world_radius", ctypes.c_double), ("road_radius", ctypes.c_double),
+                ("near_radius", ctypes.c_double), ("link_radius", ctypes.c_double),
+                ("n_cities", ctypes.c_int32)]
+
+
+def map_config_default(motion_radius=5.5 * 1.2, xmax=120, ymax=120, n_cities=12, spacing=5.5):
+    """The reference's map parameters (coverage.py:516-527): arena (-xmax, xmax, -ymax,
+    ymax), lattice vectors of DELTA = 5.5, 12 cities U(-xmax, xmax)^2, roads and target
+    links at motion_radius, lattice points within motion_radius / 1.4 of a road."""
+    return CovMapConfig(-float(xmax), float(xmax), -float(ymax), float(ymax), float(spacing), float(xmax),
+                        float(motion_radius), float(motion_radius) / 1.4, float(motion_radius), int(n_cities))
+
+
+def map_lattice(mc=None):
+    """generate_lattice's points (make_map.py:30-67) for a map configuration, computed by
+    the library's host code (cov_map_lattice, no device needed): (n, 2) [y, x]."""
+    mc = mc or map_config_default()
+    lib = load()
+    n = ctypes.c_int32(0)
+    check(lib.cov_map_lattice(ctypes.byref(mc), None, ctypes.byref(n)))
+    out = np.empty((n.value, 2), np.float64)
+    check(lib.cov_map_lattice(ctypes.byref(mc), ptr(out), ctypes.byref(n)))
+    return out
+
+
+COV_MAP_SEED = 0x1
+COV_MAP_CITIES = 0x2
+COV_MAP_NEAR_DEGENERATE = 0x1
+COV_MAP_TOO_MANY = 0x2
+COV_MAP_TOO_FEW = 0x4
+COV_MAP_OVERFLOW = 0x8
+
 COV_ACTIONS_DEVICE = 0x1
 COV_ACTIONS_RESIDENT = 0x2
 COV_ACTIONS_GREEDY = 0x20
@@ -133,6 +168,9 @@ SIGNATURES = {
     "cov_create": [ctypes.POINTER(CovConfig), ctypes.POINTER(_P)],
     "cov_destroy": [_P],
     "cov_set_targets": [_P, _I, _I, _P],
+    "cov_generate_maps": [_P, _P, _I, ctypes.c_uint64, _P, _I, _P, _P, _P],
+    "cov_get_targets": [_P, _I, _P],
+    "cov_map_lattice": [_P, _P, _P],
     "cov_reset": [_P, _P, _P],
     "cov_reset_seeded": [_P, ctypes.c_uint64, ctypes.c_double, _P, _P],
     "cov_step": [_P, _P, _I],
@@ -742,6 +780,39 @@ class CoverageHandle:
         t = np.ascontiguousarray(targets, dtype=np.float64)
         assert t.ndim == 2 and t.shape[1] == 2, t.shape
         check(self.lib.cov_set_targets(self.h, int(env), int(t.shape[0]), ptr(t)))
+
+    def generate_maps(self, map_seed=None, cities=None, env=-1, map_config=None, fetch=True):
+        """New target maps on the device (cov_generate_maps, coverage.py:516-527) for env
+        `env` (-1: every env), then their motion graphs. cities=None: drawn from each env's
+        map stream, seeded np.random.seed(map_seed + b) when map_seed is given, else
+        continued from the previous maps; cities (n_sel, n_cities, 2): given. Returns
+        (n_targets, status, cities) per selected env (None with fetch=False)."""
+        mc = map_config or map_config_default(self.cfg.motion_radius)
+        nsel = self.n_envs if env < 0 else 1
+        flags = 0
+        c = None
+        if cities is not None:
+            c = np.ascontiguousarray(cities, dtype=np.float64).reshape(nsel, mc.n_cities, 2)
+            flags |= COV_MAP_CITIES
+        elif map_seed is not None:
+            flags |= COV_MAP_SEED
+        n = np.full(nsel, -1, np.int32) if fetch else None
+        st = np.zeros(nsel, np.int32) if fetch else None
+        co = np.empty((nsel, mc.n_cities, 2), np.float64) if fetch else None
+        rc = self.lib.cov_generate_maps(self.h, ctypes.byref(mc), int(env), int(map_seed or 0), ptr(c), flags,
+                                        ptr(n), ptr(st), ptr(co))
+        if rc:
+            err = GymFlockError(rc, self.lib.fe_last_error().decode(errors="replace"))
+            err.n_targets, err.status = n, st  # which envs' maps were refused, and why
+            raise err
+        return (n, st, co) if fetch else None
+
+    def targets(self, env, n_targets):
+        """The (n_targets, 2) targets of env `env`'s current map (n_targets: its size, as
+        generate_maps returned it)."""
+        out = np.empty((int(n_targets), 2), np.float64)
+        check(self.lib.cov_get_targets(self.h, int(env), ptr(out)))
+        return out
 
     def reset(self, start, visited):
         """start: (B,R) target-local start nodes; visited: (B, max_nodes-R) 0/1."""

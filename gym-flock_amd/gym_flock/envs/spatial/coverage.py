@@ -19,7 +19,6 @@ import numpy as np
 
 from ... import _native as nat
 from ..._spaces import Box, Dict, Env, MultiDiscrete, np_random
-from .maps import generate_targets
 
 N_NODE_FEAT = 3
 N_EDGE_FEAT = 1
@@ -36,6 +35,7 @@ FRAC_ACTIVE = 0.5
 NEARBY_STARTS = True
 NEARBY_DENSITY = 5
 DELTA = 5.5
+N_CITIES = 12  # coverage.py:518
 unvisited_regions = [(-100, 100, -100, 100)]
 start_regions = [(-100, 100, -100, 100)]
 
@@ -78,9 +78,16 @@ class CoverageEnv(Env):
         self.device = device
         self._h = nat.CoverageHandle(n_robots, 1, max_nodes, episode_length, res, self.motion_radius, device,
                                      horizon=horizon)
+        self._map_cfg = nat.map_config_default(self.motion_radius, xmax, ymax, N_CITIES, DELTA)
+        self.map_status = 0  # cov_generate_maps status bits of the current map
         if init_graph:
-            targets, _ = self._generate_targets()
-            self._initialize_graph(targets)
+            try:
+                targets, _ = self._generate_targets()
+                self._initialize_graph(targets, on_device=True)
+            except ValueError:
+                # the reference builds this map's arrays and only fails when an observation
+                # of it is taken (reset() draws a new map first)
+                self.n_targets = None
         self.episode_reward = 0
         self.step_counter = 0
         self.last_loc = None
@@ -102,16 +109,36 @@ class CoverageEnv(Env):
 
     # --------------------------------------------------------------- graph setup
     def _generate_targets(self):
-        """coverage.py:516-527 (host, global np.random)."""
-        return generate_targets(self.x_max, self.y_max, self.res, self.motion_radius), True
+        """coverage.py:516-527. The 12 cities come from the global np.random here, drawn
+        exactly as make_map.py:208 draws them; their Delaunay roads, the lattice points near
+        them and the largest component of those points' radius graph are computed on the
+        device, which then builds the motion graph too (cov_generate_maps). A map with more
+        targets than max_nodes - n_robots raises (the reference's padded arrays cannot hold
+        it either)."""
+        cities = np.random.uniform(-self.x_max, self.x_max, size=(N_CITIES, 2))
+        try:
+            n, st, _ = self._h.generate_maps(cities=cities[None], env=0, map_config=self._map_cfg)
+        except nat.GymFlockError as e:
+            st = getattr(e, "status", None)
+            if st is None or not st[0] & (nat.COV_MAP_TOO_MANY | nat.COV_MAP_TOO_FEW):
+                raise
+            self.map_status = int(st[0])
+            # the reference fails here too, in _get_obs_reward (:325) with a ValueError: its
+            # padded (max_nodes, 3) arrays cannot take n_targets + n_robots nodes
+            raise ValueError("could not fit a map of %d targets and %d robots into max_nodes = %d (%s)"
+                             % (int(e.n_targets[0]), self.n_robots, self.max_nodes, e)) from e
+        self.map_status = int(st[0])
+        return self._h.targets(0, int(n[0])), True
 
-    def _initialize_graph(self, targets):
-        """coverage.py:529-619; the motion graph itself is built on the device."""
+    def _initialize_graph(self, targets, on_device=False):
+        """coverage.py:529-619; the motion graph itself is built on the device
+        (on_device: it already was, by _generate_targets)."""
         self.targets = np.asarray(targets, dtype=np.float64)
         self.n_targets = self.targets.shape[0]
         self.n_agents = self.n_targets + self.n_robots
         self.max_edges = self.max_nodes * MAX_EDGES
-        self._h.set_targets(self.targets, env=0)
+        if not on_device:
+            self._h.set_targets(self.targets, env=0)
         self._closest = self._greedy_cache = None
         self.n_motion_edges = int(self._h.n_motion()[0])
         if self.nearby_starts:
@@ -152,7 +179,7 @@ class CoverageEnv(Env):
         self.last_loc = None
         targets, graph_changed = self._generate_targets()
         if graph_changed:
-            self._initialize_graph(targets)
+            self._initialize_graph(targets, on_device=True)
         starts = self.np_random.choice(np.arange(self.n_targets)[self.start_region], size=(self.n_robots,),
                                        replace=False)
         unvisited = np.arange(self.n_targets)[self.unvisited_region] + self.n_robots

@@ -148,6 +148,8 @@ class VecCoverage:
         self.env_offset = int(env_offset)
         self.h = nat.CoverageHandle(n_robots, n_envs, max_nodes, episode_length, res, None, device)
         self.n_targets = np.zeros(self.n_envs, np.int64)
+        self._rngs = None          # host-held np_random streams (else on the device)
+        self._dev_streams = False  # the device holds every env's np_random stream
 
     def set_targets(self, targets, env=-1):
         self.h.set_targets(targets, env)
@@ -156,15 +158,33 @@ class VecCoverage:
         else:
             self.n_targets[env] = len(targets)
 
-    def reset(self, seed=0, draws="device"):
+    def generate_maps(self, map_seed=None):
+        """A new target map for every env on the device (coverage.py:516-527, as each
+        reference reset() draws one): env b's cities come from its own map stream, seeded
+        np.random.seed(map_seed + env_offset + b) when map_seed is given, else continued
+        from its previous map, as the reference's global np.random continues from one
+        reset to the next. Returns (n_targets (B,), status (B,))."""
+        seed = None if map_seed is None else int(map_seed) + self.env_offset
+        n, st, _ = self.h.generate_maps(map_seed=seed)
+        self.n_targets[:] = n
+        return n, st
+
+    def reset(self, seed=0, draws="device", new_maps=False, map_seed=None):
         """Env b is a reference env whose np_random was seeded seed + env_offset + b: its
         reset draws (coverage.py:405-424), then its stream continues on the device for the
         greedy expert's fallback draws (step(greedy=True)); np_random(b) reads it back.
         draws="device" (cov_reset_seeded): the draws run on the device, one wave per env;
         "host": RandomState loops here (~0.5 ms per env), then cov_reset and cov_set_rng.
-        Both return (start (B,R) target-local, visited (B, max_nodes-R)), bit-identical."""
+        Both return (start (B,R) target-local, visited (B, max_nodes-R)), bit-identical.
+        new_maps: each env first draws a new map on the device (generate_maps(map_seed)),
+        as every reference reset() does (:378-397)."""
+        if new_maps:
+            self.generate_maps(map_seed)
+        self._rngs = None
         if draws == "device":
-            return self.h.reset_seeded(seed + self.env_offset, self.frac)
+            out = self.h.reset_seeded(seed + self.env_offset, self.frac)
+            self._dev_streams = True
+            return out
         R, tmax = self.n_robots, self.h.t_max
         start = np.empty((self.n_envs, R), np.int32)
         visited = np.ones((self.n_envs, tmax), np.uint8)
@@ -179,11 +199,38 @@ class VecCoverage:
         self.h.reset(start, visited)
         if R <= 624:  # device draws (COV_GREEDY_RNG): one key regeneration per step at most
             self.h.set_rng(rngs)
+            self._dev_streams = True
+        else:
+            self._rngs, self._dev_streams = rngs, False
         return start, visited
+
+    def _device_draws(self):
+        """Whether the fused greedy step can draw the fallback robots' np_random.choice(4)
+        on the device (COV_GREEDY_RNG): the streams live there, n_robots <= 624 (one key
+        regeneration per step) and the per-node greedy lists exist (max_nodes - n_robots
+        <= 1024)."""
+        return self._dev_streams and self._rngs is None and self.n_robots <= 624 and self.h.t_max <= 1024
+
+    def _host_rngs(self):
+        """The envs' np_random streams as host RandomStates (read back from the device the
+        first time; the host keeps them from then on, until the next reset)."""
+        if self._rngs is None:
+            if not self._dev_streams:
+                raise nat.GymFlockError(nat.GF_ESTATE, "reset first (no np_random streams)")
+            keys, pos = self.h.get_rng()
+            self._rngs = []
+            for b in range(self.n_envs):
+                rs = np.random.RandomState()
+                rs.set_state(("MT19937", keys[b], int(pos[b])))
+                self._rngs.append(rs)
+            self._dev_streams = False
+        return self._rngs
 
     def np_random(self, env):
         """Env `env`'s np_random after the fallback draws of the steps so far (a RandomState
-        continuing the device stream)."""
+        continuing the device stream, or the host one)."""
+        if self._rngs is not None:
+            return self._rngs[env]
         keys, pos = self.h.get_rng()
         rs = np.random.RandomState()
         rs.set_state(("MT19937", keys[env], int(pos[env])))
@@ -193,11 +240,21 @@ class VecCoverage:
         """actions (B,R); or resident=True (the last set/greedy actions); or greedy=True
         (controller(greedy=True), coverage.py:800-872, computed in the step's own launch).
         fallback: robots the reference hands to np_random.choice(4) (:861-864) draw it from
-        their env's stream on the device ("draw", the reference's semantics; needs
-        n_robots <= 624) or take action 0 ("zero"); include/gymflock.h COV_ACTIONS_GREEDY,
-        COV_GREEDY_RNG."""
+        their env's stream ("draw", the reference's semantics: on the device inside the
+        step when _device_draws(), else the greedy kernel, the draws on the host in robot
+        order and a resident step) or take action 0 ("zero"); include/gymflock.h
+        COV_ACTIONS_GREEDY, COV_GREEDY_RNG."""
         if resident or greedy:
-            if greedy:
+            if greedy and fallback == "draw" and not self._device_draws():
+                a, rnd = self.h.controller_greedy()
+                if rnd.any():
+                    rngs = self._host_rngs()
+                    for b in np.nonzero(rnd.any(axis=1))[0]:
+                        k = np.nonzero(rnd[b])[0]
+                        a[b, k] = rngs[b].choice(4, size=len(k))
+                    self.h.set_actions(a)
+                rc = self.h._step_resident()
+            elif greedy:
                 rc = self.h._step_greedy_rng() if fallback == "draw" else self.h._step_greedy()
             else:
                 rc = self.h._step_resident()

@@ -1,6 +1,9 @@
-"""Per-episode target maps for Coverage-v0 (host-side setup, not the step hot path).
+"""Per-episode target maps for Coverage-v0 on the host, with scipy as the reference uses.
 
-Same algorithm and random draws as the reference's map generation so a seeded global
+TEST INFRASTRUCTURE ONLY: imported by tests/ and bench.py's CPU baseline, never by the
+product (the product draws maps on the device, cov_generate_maps; oracle/coverage_maps.py
+restates that device algorithm). Same algorithm and random draws as the reference's map
+generation so a seeded global
 NumPy RNG yields the reference's target set: a square lattice over the arena
 (make_map.py:30-67), "roads" along the Delaunay edges of 12 random cities
 (make_map.py:207-231), lattice points within motion_radius/1.4 of a road, and the

@@ -190,6 +190,9 @@ if __name__ == "__main__":
     if "--coverage" in sys.argv or "--all" in sys.argv:
         from make_golden_coverage import gen_coverage  # noqa: E402
         gen_coverage()
+    elif "--maps" in sys.argv:
+        from make_golden_coverage import gen_maps  # noqa: E402
+        gen_maps()
     if "--graph-utils" in sys.argv or "--all" in sys.argv:
         from make_golden_graph_utils import gen_graph_utils  # noqa: E402
         gen_graph_utils()

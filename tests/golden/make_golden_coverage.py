@@ -58,13 +58,31 @@ def gen_coverage():
     _episode(cov, 6, 500, map_seed=5, env_seed=6, n_steps=30, policy="greedy", tag="r6_greedy")
     _episode(cov, 200, 1000, map_seed=8, env_seed=9, n_steps=12, policy="random", tag="r200_random")
     _episode(cov, 20, 700, map_seed=12, env_seed=13, n_steps=75, policy="greedy", tag="r20_greedy")
-    # the host map generator, pinned separately (coverage.py:516-527)
+    gen_maps()
+
+
+def gen_maps(n_seeds=100, n_next=10):
+    """The map generator, pinned separately (coverage.py:516-527): seeds 0-2 as target
+    arrays; seeds 0..n_seeds-1 as indices into the lattice (every target is a lattice
+    point), and for seeds 0..n_next-1 the second map the same global stream draws (the
+    next reset() after np.random.seed(s))."""
+    cov = importlib.import_module("gym_flock.envs.spatial.coverage")
     mm = importlib.import_module("gym_flock.envs.spatial.make_map")
-    maps = {}
-    for s in (0, 1, 2):
-        np.random.seed(s)
-        env = cov.CoverageEnv(n_robots=6, nearby_starts=False, max_nodes=1000, init_graph=False)
-        t, _ = env._generate_targets()
-        maps["targets_seed%d" % s] = t
     lat = mm.generate_lattice((-120, 120, -120, 120), [np.array([-5.5, 0.]), np.array([0., -5.5])])
-    np.savez_compressed(os.path.join(OUT, "coverage_maps.npz"), lattice=lat, **maps)
+    where = {tuple(p): k for k, p in enumerate(lat.tolist())}
+    env = cov.CoverageEnv(n_robots=6, nearby_starts=False, max_nodes=1000, init_graph=False)
+    maps = {}
+    many, nxt = [], []
+    for s in range(n_seeds):
+        np.random.seed(s)
+        t, _ = env._generate_targets()
+        if s < 3:
+            maps["targets_seed%d" % s] = t
+        many.append(np.array([where[tuple(p)] for p in t.tolist()], np.int16))
+        if s < n_next:
+            t2, _ = env._generate_targets()
+            nxt.append(np.array([where[tuple(p)] for p in t2.tolist()], np.int16))
+    np.savez_compressed(os.path.join(OUT, "coverage_maps.npz"), lattice=lat, **maps,
+                        many_len=np.array([len(m) for m in many], np.int32), many_idx=np.concatenate(many),
+                        next_len=np.array([len(m) for m in nxt], np.int32), next_idx=np.concatenate(nxt))
+    print("coverage maps: %d seeds, %d targets on average" % (n_seeds, int(np.mean([len(m) for m in many]))))

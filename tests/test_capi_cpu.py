@@ -145,7 +145,7 @@ def test_coverage_map_generation_matches_reference():
     """Host map generation (maps.py) reproduces the reference's target sets from the same
     global seeds (coverage.py:516-527, make_map.py:30-67, :207-231)."""
     from conftest import GOLDEN
-    from gym_flock.envs.spatial.maps import generate_targets, square_lattice
+    from oracle.maps_host import generate_targets, square_lattice
     f = np.load(os.path.join(GOLDEN, "coverage_maps.npz"))
     np.testing.assert_array_equal(square_lattice(-120, 120, -120, 120, 5.5), f["lattice"])
     for s in (0, 1, 2):

@@ -54,7 +54,7 @@ def test_episode_matches_reference_golden(path):
 
 def test_batched_envs_with_distinct_graphs_vs_oracle():
     """4 envs, each its own map and random actions, 20 steps against the oracle."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, R, M = 4, 12, 600
     maps = []
     for b in range(B):
@@ -239,7 +239,7 @@ def test_crowded_grid_claims_vs_oracle(R):
 def test_split_steps_match_single_stream():
     """Back-to-back resident steps go out as two half-batch launches on two streams;
     the observations, rewards and robots equal the one-launch-per-step run."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, R, M = 5, 12, 600
     np.random.seed(7)
     targets = generate_targets()
@@ -273,7 +273,7 @@ def test_full_config4_batch_properties_and_sampled_parity():
     oracle shows on the sampled envs), rewards are the newly visited counts (summed
     rewards = visited growth), and the observation tails name only robots and targets. Sampled envs (first, middle, last): full observations, rewards, robots and
     visited sets bit-exact against the oracle every step."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, R, M = 512, 200, 1000
     np.random.seed(8)
     targets = generate_targets()

@@ -119,7 +119,7 @@ def test_time_matrix_horizons_vs_oracle(horizon, which):
     and no change (disconnected graph), for several horizons including unbounded; the
     line exercises the wide (uint16) fallback."""
     if which == "map":
-        from gym_flock.envs.spatial.maps import generate_targets
+        from oracle.maps_host import generate_targets
         np.random.seed(21)
         targets = generate_targets()
     elif which == "clusters":
@@ -152,7 +152,7 @@ def test_time_matrix_wave_forms_vs_oracle(case):
         targets = _lattice(26 if case.endswith("676") else 30)
         B = 1
     else:
-        from gym_flock.envs.spatial.maps import generate_targets
+        from oracle.maps_host import generate_targets
         np.random.seed(21)
         targets = generate_targets()
         B = int(case.split("_")[1])
@@ -209,7 +209,7 @@ def test_batched_greedy_vs_oracle():
     """6 envs, each its own map (different target counts, so per-env chunk counts
     differ), greedy for 20 steps against the oracle with per-env fallback RNGs; then a
     new graph for env 2 (only its matrix is stale) and another phase."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, R, M = 6, 16, 800
     maps = []
     for b in range(B):
@@ -276,7 +276,7 @@ def test_fused_greedy_step_equals_separate():
     by a resident step, fallback robots taking action 0 in both. A batch of different
     maps over a whole episode (robots placed off-node in one env at step 10): the actions
     taken, needs_random, robots, rewards and observations are equal at every step."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, R, M = 4, 20, 800
     maps = []
     for b in range(B):
@@ -378,7 +378,7 @@ def test_cov_step_host_batched_matches_step_and_getters():
     after the launch) on odd steps, with COV_NEXT_GREEDY: every env's observation, step,
     reward, done, robot nodes and next greedy actions equal those of cov_step + the
     getters + cov_controller_greedy on a second handle stepped with the same actions."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, R, M = 3, 10, 700
     maps = []
     for b in range(B):
@@ -521,7 +521,7 @@ def test_device_rng_batched_vs_oracle(R):
     in robot order. At R=200 most robots fall back once the targets near them are visited,
     so each stream passes several key regenerations. Actions, fallback flags, rewards and
     nodes bit-exact every step; the device streams equal the host's at the end."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, M, steps = 4, 1000, 40
     maps = []
     for b in range(B):
@@ -598,7 +598,7 @@ def test_device_rng_config4_batch_sampled_vs_oracle():
     fallback draws on the device, every env stepping in the same two half-batch launches;
     envs 0, 31 and 63 checked against the oracle's expert with their own RandomStates at
     every step (actions, nodes, rewards and done flags), and their streams at the end."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     R, B, M = 200, 64, 1000
     np.random.seed(8)
     targets = generate_targets()
@@ -647,7 +647,7 @@ def test_device_reset_draws_equal_host_draws(R):
     loops, cov_reset + cov_set_rng): starts, visited flags, the observations reset()
     returns and the envs' streams equal, for envs with different maps (target counts), and
     the first greedy steps after it take the same actions."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     B, M = 5, 1000
     maps = []
     for b in range(B):
@@ -685,7 +685,7 @@ def test_device_reset_draws_equal_host_draws(R):
 def test_device_reset_fraction_edges(frac):
     """cov_reset_seeded at the ends of frac_active_targets (nothing unvisited, everything
     unvisited) and between: the draws and visited flags equal the host loops'."""
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     np.random.seed(31)
     targets = generate_targets()
     vs = [VecCoverage(3, 8, max_nodes=800, frac_active_targets=frac) for _ in range(2)]

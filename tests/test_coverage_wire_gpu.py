@@ -40,7 +40,7 @@ def test_flat_obs_matches_reference_episode():
 
 
 def _batch(B=3, R=10, M=700, steps=4):
-    from gym_flock.envs.spatial.maps import generate_targets
+    from oracle.maps_host import generate_targets
     maps = []
     for b in range(B):
         np.random.seed(400 + b)

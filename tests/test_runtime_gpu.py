@@ -49,7 +49,7 @@ sys.path[:0] = [{root!r}, {pkg!r}]
 from gym_flock import _native as nat
 from gym_flock.init_states import synthetic_batch
 from gym_flock.vec import VecCoverage
-from gym_flock.envs.spatial.maps import generate_targets
+from oracle.maps_host import generate_targets
 from oracle import flocking as orc
 from oracle import coverage as oc
 out = {{"runtime": nat.runtime_info()}}
