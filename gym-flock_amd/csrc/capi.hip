@@ -135,27 +135,26 @@ struct fe_handle {
   hipEvent_t step_ev = nullptr;
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
-  hipEvent_t ag_ev = nullptr;           // completion of the latest reward all-gather
   // ring slots a reward gather's staging copy still reads: steps [first, ...) until the
-  // copy kernel (on the side stream) has stored `seq` into the page-locked word stage_done
+  // copy kernel (on the side stream) has stored `seq` into completion word kWordRing
   struct RingRead {
     int64_t first;
     uint32_t seq;
   };
   std::deque<RingRead> ring_reads;
-  // the staging copies' completion word: page-locked (mapped, coherent), written by the
-  // copy kernel with a system-scope release after its last read of the ring; never freed
-  // once a communicator was aborted (an abandoned copy may still store into it)
+  // The side stream's completion words (kWord*): page-locked (mapped, coherent), each
+  // stored by a kernel on the side stream with a system-scope release once the work
+  // before it is done, and polled by the host instead of querying events; never freed
+  // once a communicator was aborted (an abandoned kernel may still store into them)
   uint32_t* stage_done = nullptr;
   uint32_t* stage_done_dev = nullptr;
-  uint32_t stage_seq = 0;
+  uint32_t stage_seq[4] = {0, 0, 0, 0};  // the last sequence number issued per word
   int64_t gathered_upto = 0;            // steps before this one were shipped (or skipped)
   bool ag_issued = false;
   int last_count = 0;
   double* stats_sum = nullptr;          // (B,2) get_stats means per env (fe_stats_summary)
   double* ssend = nullptr;              // (max_envs,2) the stats gather's padded send block
   double* stats_gather = nullptr;       // nranks x max_envs x 2 (fe_allgather_stats)
-  hipEvent_t sg_ev = nullptr;           // completion of the latest stats all-gather
   bool sg_pending = false;
   // fe_debug_comm_gate: a bounded spin kernel on comm_stream, released by this page-locked
   // flag, stands in for a collective whose peer stopped responding (tests only)
@@ -403,7 +402,7 @@ void comm_release(fe_handle* h, bool abort) {
     if (h->comm) abort_comm_later(h->comm, h->cfg.device);
     h->comm = nullptr;
     h->comm_stream = nullptr;
-    h->step_ev = h->step_ev2 = h->ag_ev = h->sg_ev = nullptr;
+    h->step_ev = h->step_ev2 = nullptr;
     h->ring_reads.clear();  // copies the side stream may still run: abandoned, and so
     h->stage_done = h->stage_done_dev = nullptr;  // is the word they would store into
     h->gsend = h->gather = h->ssend = h->stats_gather = nullptr;
@@ -417,7 +416,7 @@ void comm_release(fe_handle* h, bool abort) {
     hipStreamDestroy(h->comm_stream);
     h->comm_stream = nullptr;
   }
-  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev})
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2})
     if (*e) {
       hipEventDestroy(*e);
       *e = nullptr;
@@ -469,13 +468,14 @@ int check_env(const fe_handle* h, int env) {
 
 double* cur_reward(fe_handle* h) { return h->reward_ring + (size_t)h->rslot * h->cfg.n_envs; }
 
-int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what);
-int stage_wait(fe_handle* h, uint32_t seq, const char* what);
+// completion words of the side stream (fe_handle::stage_done)
+enum { kWordRing = 0, kWordStatsCopy = 1, kWordRewardGather = 2, kWordStatsGather = 3 };
+int stage_wait(fe_handle* h, int word, uint32_t seq, const char* what);
 
-// Whether the reward gather's staging copy `seq` has finished reading the ring (the copies
-// run in order on the side stream, so the completion word only grows).
-bool stage_complete(const fe_handle* h, uint32_t seq) {
-  return static_cast<int32_t>(__atomic_load_n(h->stage_done, __ATOMIC_ACQUIRE) - seq) >= 0;
+// Whether the side-stream work numbered `seq` on completion word `word` is done (each
+// word's kernels run in order on the side stream, so the word only grows).
+bool stage_complete(const fe_handle* h, int word, uint32_t seq) {
+  return static_cast<int32_t>(__atomic_load_n(h->stage_done + word, __ATOMIC_ACQUIRE) - seq) >= 0;
 }
 
 int no_comm(const fe_handle* h) {
@@ -496,12 +496,12 @@ int next_reward_slot(fe_handle* h) {
   h->rslot = static_cast<int>(s % kRewardSlots);
   while (!h->ring_reads.empty() && h->ring_reads.front().first <= s - kRewardSlots) {
     const uint32_t seq = h->ring_reads.front().seq;
-    const bool done = stage_complete(h, seq);
+    const bool done = stage_complete(h, kWordRing, seq);
     h->dbg[0]++;
     h->dbg[1] = done ? 1 : 0;
     h->dbg[2] = -1;
     if (!done) {
-      h->dbg[2] = stage_wait(h, seq, "reward all-gather staging copy (ring slot reuse)");
+      h->dbg[2] = stage_wait(h, kWordRing, seq, "reward all-gather staging copy (ring slot reuse)");
       if (h->dbg[2] == GF_ECOMM) {
         h->comm_lost = g_err;  // comm_release emptied ring_reads: the step goes on
         break;
@@ -923,6 +923,12 @@ int fe_set_params(fe_handle* h, const fe_config* cfg) {
   // forgotten (it only steers which rows the fused step ranks beyond their neighbours)
   if (int rc = use_dev(h)) return rc;
   GF_HIP(clear_knn_history(h));
+  // the controls on the device were computed under the old comm_radius / centralized /
+  // action_scalar (controller() reads them at call time, :194-226): FE_U_EXPERT and
+  // fe_get_controls need a new controller output first
+  if (cfg->comm_radius != h->cfg.comm_radius || cfg->centralized != h->cfg.centralized ||
+      cfg->action_scalar != h->cfg.action_scalar)
+    h->has_ctrl = false;
   h->cfg.comm_radius = cfg->comm_radius;
   h->cfg.dt = cfg->dt;
   h->cfg.action_scalar = cfg->action_scalar;
@@ -1147,16 +1153,18 @@ static int step_host_impl(fe_handle* h, const void* u, float* state_values, floa
   // page-locked memory (every output page-locked, no copy after it: the step, or the rim
   // kNN behind it), the host waits for that kernel's own completion flag, not for the
   // stream (done_flag.h: ~8 us sooner)
-  const bool fin = (!state_values || sv_m) && (!network || net_m) && (!rewards || rw_m) && (!ctrl || ct_m) &&
-                   (!knn || kdirect);
   const bool rim_last = knn && !h->knn_exact;
+  // (diagnostic build: the ablation that skips the rim kNN launch would drop the flag it
+  // carries; the host then waits for the stream)
+  const bool fin = (!state_values || sv_m) && (!network || net_m) && (!rewards || rw_m) && (!ctrl || ct_m) &&
+                   (!knn || kdirect) && !(rim_last && (h->diag & 0x80000));
   gf::DoneFlag fd{};
   if (fin) {
     if (!h->fin_cnt) {
       if (int rc = dalloc(&h->fin_cnt, 1)) return rc;
       GF_HIP(hipMemsetAsync(h->fin_cnt, 0, sizeof(int32_t), h->stream));
       void* p = nullptr;
-      GF_HIP(hipHostMalloc(&p, 64, hipHostMallocMapped));
+      GF_HIP(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
       h->fin_host = static_cast<int32_t*>(p);
       *h->fin_host = 0;
       h->fin_dev = static_cast<int32_t*>(mapped_ptr(p));
@@ -1343,11 +1351,10 @@ int stats_summary_dev(fe_handle* h) {
   }
   if (!h->stats_sum)
     if (int rc = dalloc(&h->stats_sum, (size_t)h->cfg.n_envs * 2)) return rc;
-  if (h->sg_pending && h->comm) {
-    const hipError_t q = hipEventQuery(h->sg_ev);
-    if (q != hipSuccess && q != hipErrorNotReady) return fail_hip("stats all-gather", q);
-    if (q == hipErrorNotReady && comm_event_wait(h, h->sg_ev, "stats all-gather (send block reuse)") != GF_OK)
-      h->comm_lost = g_err;
+  if (h->sg_pending && h->comm && !stage_complete(h, kWordStatsCopy, h->stage_seq[kWordStatsCopy])) {
+    const int rc = stage_wait(h, kWordStatsCopy, h->stage_seq[kWordStatsCopy], "stats all-gather (send block reuse)");
+    if (rc == GF_ECOMM) h->comm_lost = g_err;  // torn down: the summary goes on
+    else if (rc != GF_OK) return rc;
   }
   gf::StatsArgs s{h->x[h->cur], h->vel_diffs, h->min_dists, h->degree,
                   h->cfg.comm_radius * h->cfg.comm_radius, h->cfg.n_agents, h->cfg.n_envs};
@@ -1669,50 +1676,29 @@ int comm_wait(fe_handle* h, Clock::time_point deadline, const char* what) {
     if (st == ncclSuccess) return GF_OK;
     if (st != ncclInProgress || Clock::now() > deadline) {
       comm_release(h, true);
-      if (st != ncclInProgress) return fail(GF_ECOMM, std::string(what) + ": " + ncclGetErrorString(st));
-      return fail(GF_ECOMM, std::string(what) + ": timed out (a rank did not join or stopped responding)");
+      h->comm_lost = std::string(what) + ": " +
+                     (st != ncclInProgress ? std::string(ncclGetErrorString(st))
+                                           : std::string("timed out (a rank did not join or stopped responding)")) +
+                     "; communicator aborted";
+      return fail(GF_ECOMM, h->comm_lost);
     }
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
 }
 
-// Wait for an event recorded on the side stream behind a collective, bounded like
-// comm_wait: the communicator's async error is polled beside the event, and on expiry
-// (a rank that died mid-run never posts its part) the metrics path is torn down.
-int comm_event_wait(fe_handle* h, hipEvent_t ev, const char* what) {
+// Wait for side-stream work `seq` on completion word `word` (a gather's staging copy or
+// its collective), polling the communicator's async error beside it: on expiry of the
+// collective timeout (a rank that died mid-run never posts its part) or a communicator
+// error the metrics path is torn down (GF_ECOMM, comm_lost says why); a side stream that
+// finished without the word is a HIP error (the path stays up).
+int stage_wait(fe_handle* h, int word, uint32_t seq, const char* what) {
   const auto deadline = deadline_in(h->comm_timeout);
   for (int spin = 0;; ++spin) {
     h->dbg[7] = spin;
-    const hipError_t q = hipEventQuery(ev);
-    if (q == hipSuccess) return GF_OK;
-    if (q != hipErrorNotReady) return fail_hip(what, q);
-    ncclResult_t st = ncclSuccess;
-    ncclResult_t r = ncclCommGetAsyncError(h->comm, &st);
-    if (r != ncclSuccess) st = r;
-    if (spin == 0) h->dbg[3] = static_cast<int32_t>(st);
-    const bool err = st != ncclSuccess && st != ncclInProgress;
-    if (err || Clock::now() > deadline) {
-      comm_release(h, true);
-      h->comm_lost = std::string(what) + ": " +
-                     (err ? std::string(ncclGetErrorString(st)) : std::string("timed out (a rank stopped responding)")) +
-                     "; communicator aborted";
-      return fail(GF_ECOMM, h->comm_lost);
-    }
-    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
-  }
-}
-
-// Wait for the reward gather's staging copy `seq` (its completion word), bounded like
-// comm_event_wait: on expiry or a communicator error the metrics path is torn down
-// (GF_ECOMM); a side stream that finished without the word is a HIP error.
-int stage_wait(fe_handle* h, uint32_t seq, const char* what) {
-  const auto deadline = deadline_in(h->comm_timeout);
-  for (int spin = 0;; ++spin) {
-    h->dbg[7] = spin;
-    if (stage_complete(h, seq)) return GF_OK;
+    if (stage_complete(h, word, seq)) return GF_OK;
     if ((spin & 63) == 63) {
       const hipError_t q = hipStreamQuery(h->comm_stream);
-      if (q == hipSuccess && !stage_complete(h, seq))
+      if (q == hipSuccess && !stage_complete(h, word, seq))
         return fail(GF_EHIP, std::string(what) + ": the side stream finished without the copy's completion word");
       if (q != hipSuccess && q != hipErrorNotReady) return fail_hip(what, q);
     }
@@ -1760,7 +1746,8 @@ int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
     void* p = nullptr;
     GF_HIP(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
     h->stage_done = static_cast<uint32_t*>(p);
-    __atomic_store_n(h->stage_done, h->stage_seq, __ATOMIC_SEQ_CST);  // every earlier copy: done
+    for (int w = 0; w < 4; ++w)  // every earlier sequence number: done
+      __atomic_store_n(h->stage_done + w, h->stage_seq[w], __ATOMIC_SEQ_CST);
     void* d = nullptr;
     GF_HIP(hipHostGetDevicePointer(&d, p, 0));
     h->stage_done_dev = static_cast<uint32_t*>(d);
@@ -1801,7 +1788,7 @@ int comm_setup(fe_handle* h, int nranks, int rank, Clock::time_point deadline) {
   h->shard_sizes = sizes;
   h->max_envs = *std::max_element(sizes.begin(), sizes.end());
   const size_t W = h->max_envs;
-  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2, &h->ag_ev, &h->sg_ev})
+  for (hipEvent_t* e : {&h->step_ev, &h->step_ev2})
     GF_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   if ((rc = comm_alloc(h, &h->gsend, (size_t)kRewardSlots * W)) ||
       (rc = comm_alloc(h, &h->gather, (size_t)nranks * kRewardSlots * W)) || (rc = comm_alloc(h, &h->ssend, W * 2)) ||
@@ -1935,6 +1922,27 @@ __global__ __launch_bounds__(256) void ring_stage_kernel(const double* ring, int
     __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
+
+// After a collective on the side stream: `seq` into its completion word (the stream's
+// earlier work, the collective included, is complete when this runs).
+__global__ __launch_bounds__(64) void signal_kernel(uint32_t* done, uint32_t seq) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The stats gather's send block: n doubles from the summaries, then `seq` into the
+// completion word once every read of them has returned.
+__global__ __launch_bounds__(256) void copy_signal_kernel(const double* src, double* dst, int n, uint32_t* done,
+                                                          uint32_t seq) {
+  for (int k = threadIdx.x; k < n; k += 256) dst[k] = src[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -1971,17 +1979,20 @@ int fe_allgather_rewards(fe_handle* h) {
   // kernel's own store, not an event query ("a step that did not wait")
   double* gs = h->gsend;
   const int s0 = static_cast<int>(first % kRewardSlots);
-  const uint32_t seq = ++h->stage_seq;
+  const uint32_t seq = ++h->stage_seq[kWordRing];
   hipLaunchKernelGGL(ring_stage_kernel, dim3(1), dim3(256), 0, h->comm_stream, static_cast<const double*>(h->reward_ring),
-                     static_cast<int>(B), s0, static_cast<int>(count), gs, static_cast<int>(W), h->stage_done_dev, seq);
+                     static_cast<int>(B), s0, static_cast<int>(count), gs, static_cast<int>(W),
+                     h->stage_done_dev + kWordRing, seq);
   GF_HIP(hipGetLastError());
   h->ring_reads.push_back({first, seq});
   h->dbg[4] = static_cast<int32_t>(h->ring_reads.size());
-  h->dbg[5] = stage_complete(h, seq) ? 1 : 0;
+  h->dbg[5] = stage_complete(h, kWordRing, seq) ? 1 : 0;
   if (int rc = comm_enqueued(h, ncclAllGather(gs, h->gather, (size_t)count * W, ncclFloat64, h->comm, h->comm_stream),
                              "ncclAllGather (rewards)"))
     return rc;
-  GF_HIP(hipEventRecord(h->ag_ev, h->comm_stream));
+  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, h->comm_stream, h->stage_done_dev + kWordRewardGather,
+                     ++h->stage_seq[kWordRewardGather]);
+  GF_HIP(hipGetLastError());
   h->ag_issued = true;
   h->last_count = static_cast<int>(count);
   h->gathered_upto = h->steps_written;
@@ -1993,7 +2004,7 @@ int fe_get_gathered_rewards(fe_handle* h, double* dst) {
   if (!h->comm) return no_comm(h);
   if (!h->ag_issued) return fail(GF_ESTATE, "no all-gather issued");
   if (int rc = use_dev(h)) return rc;
-  if (int rc = comm_event_wait(h, h->ag_ev, "reward all-gather")) return rc;
+  if (int rc = stage_wait(h, kWordRewardGather, h->stage_seq[kWordRewardGather], "reward all-gather")) return rc;
   const size_t n = (size_t)h->nranks * h->last_count * h->max_envs;
   return d2h(h, dst, h->gather, n * 8);  // (on the handle's stream: no use of the null stream)
 }
@@ -2012,13 +2023,16 @@ int fe_allgather_stats(fe_handle* h) {
   GF_HIP(hipEventRecord(h->step_ev, h->stream));
   GF_HIP(hipStreamWaitEvent(h->comm_stream, h->step_ev, 0));
   // into the padded send block, on the side stream (after the previous stats gather)
-  GF_HIP(hipMemcpyAsync(h->ssend, h->stats_sum, (size_t)h->cfg.n_envs * 2 * sizeof(double), hipMemcpyDeviceToDevice,
-                        h->comm_stream));
+  hipLaunchKernelGGL(copy_signal_kernel, dim3(1), dim3(256), 0, h->comm_stream, static_cast<const double*>(h->stats_sum),
+                     h->ssend, h->cfg.n_envs * 2, h->stage_done_dev + kWordStatsCopy, ++h->stage_seq[kWordStatsCopy]);
+  GF_HIP(hipGetLastError());
   if (int rc = comm_enqueued(h, ncclAllGather(h->ssend, h->stats_gather, (size_t)h->max_envs * 2, ncclFloat64,
                                               h->comm, h->comm_stream),
                              "ncclAllGather (stats)"))
     return rc;
-  GF_HIP(hipEventRecord(h->sg_ev, h->comm_stream));
+  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, h->comm_stream, h->stage_done_dev + kWordStatsGather,
+                     ++h->stage_seq[kWordStatsGather]);
+  GF_HIP(hipGetLastError());
   h->sg_pending = true;
   return GF_OK;
 }
@@ -2028,7 +2042,7 @@ int fe_get_gathered_stats(fe_handle* h, double* dst) {
   if (!h->comm) return no_comm(h);
   if (!h->sg_pending) return fail(GF_ESTATE, "no stats all-gather issued");
   if (int rc = use_dev(h)) return rc;
-  if (int rc = comm_event_wait(h, h->sg_ev, "stats all-gather")) return rc;
+  if (int rc = stage_wait(h, kWordStatsGather, h->stage_seq[kWordStatsGather], "stats all-gather")) return rc;
   return d2h(h, dst, h->stats_gather, (size_t)h->nranks * h->max_envs * 2 * sizeof(double));
 }
 

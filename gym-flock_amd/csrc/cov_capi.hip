@@ -882,7 +882,7 @@ int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* ed
   // the device error word of each env as its workgroup ends, in page-locked scratch
   if (!h->herr) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, std::max<size_t>(B, 16) * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
+    if (hipHostMalloc(&p, std::max<size_t>(B, 16) * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return cfail(GF_ENOMEM, "hipHostMalloc (error words)");
     h->herr = static_cast<int32_t*>(p);
   }
@@ -898,7 +898,7 @@ int cov_step_host(cov_handle* h, const int32_t* actions, float* nodes, float* ed
     if (!h->fin_cnt) {
       if (int rc = calloc_dev(&h->fin_cnt, 1)) return rc;
       void* p = nullptr;
-      if (hipHostMalloc(&p, 64, hipHostMallocMapped) != hipSuccess)
+      if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return cfail(GF_ENOMEM, "hipHostMalloc (completion flag)");
       h->fin_host = static_cast<int32_t*>(p);
       *h->fin_host = 0;

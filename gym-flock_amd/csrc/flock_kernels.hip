@@ -261,11 +261,21 @@ __device__ __forceinline__ void knn_insert_asc(double (&kr)[K], int (&kj)[K], do
   }
 }
 
+// A NaN r2 (a non-finite state: e.g. the controller's division by zero for coincident
+// agents) enters as (inf, j + N): after every real (inf, j) and ordered by index, as the
+// exact small-env ranking orders NaN keys above +inf (r2_key) and argsort puts NaN last;
+// the writers map j + N back to j.
 template <int K>
 __device__ __forceinline__ void knn_consider(double (&kr)[K], int (&kj)[K], double pxi, double pyi, double2 p,
-                                             int j) {
+                                             int j, int N) {
   const double dx = pxi - p.x, dy = pyi - p.y;
-  knn_insert<K>(kr, kj, dx * dx + dy * dy, j);
+  const double r2 = dx * dx + dy * dy;
+  const bool nan = r2 != r2;
+  knn_insert<K>(kr, kj, nan ? __builtin_inf() : r2, nan ? j + N : j);
+}
+// the column of a ranked slot: j, j + N (a NaN r2) or unfilled (the row itself)
+__device__ __forceinline__ int knn_slot_col(int kj, int N, int row) {
+  return kj < N ? kj : (kj < 2 * N ? kj - N : row);
 }
 
 // Row `i` of lane l, ranked by the whole wave: lanes scan columns lane, lane + 64, ...
@@ -293,7 +303,7 @@ __device__ __forceinline__ void knn_wave_scan(const Pos& pos, int N, int l, int 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = j0 + u * 64;
-      if (j < N && j != row) knn_consider<K>(lr, lj, px, py, p[u], j);
+      if (j < N && j != row) knn_consider<K>(lr, lj, px, py, p[u], j, N);
     }
   }
 #pragma unroll
@@ -354,7 +364,7 @@ __device__ __forceinline__ void step_inline_rim(const StepArgs& a, size_t env0, 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = j0 + u * 64;
-        if (j < N && j != row) knn_consider<KN>(lr, lj, px, py, make_double2(p[u].px, p[u].py), j);
+        if (j < N && j != row) knn_consider<KN>(lr, lj, px, py, make_double2(p[u].px, p[u].py), j, N);
       }
     }
     double rr = __builtin_inf();
@@ -400,7 +410,7 @@ __device__ __forceinline__ void step_inline_rim(const StepArgs& a, size_t env0, 
     if (lane < KN) {
       const size_t g = env0 + row;
       if (lane == KN - 1 && a.knn_r2) a.knn_r2[g] = static_cast<float>(rr);
-      const int j = rj < N ? rj : row;  // unfilled slots (non-finite r2 only): self
+      const int j = knn_slot_col(rj, N, row);  // unfilled slots (non-finite r2 only): self
       a.knn_idx[g * KN + lane] = j;
       const St o = load_state<DYN, UF64>(a, env0 + j);
       float4 ob;
@@ -1589,7 +1599,7 @@ __device__ __forceinline__ void knn_write_row(const KnnArgs& a, const double* xb
   const double2 pi = xi[0], vv = xi[1];
 #pragma unroll
   for (int m = 0; m < K; ++m) {
-    const int j = kj[m] < N ? kj[m] : i;  // unfilled slots (non-finite r2 only): self
+    const int j = knn_slot_col(kj[m], N, i);  // unfilled slots (non-finite r2 only): self
     a.idx[g * K + m] = j;
     const double2* xj = reinterpret_cast<const double2*>(xb) + 2 * (size_t)j;
     const double2 pj = xj[0], vj = xj[1];
@@ -1793,7 +1803,7 @@ __device__ __forceinline__ void knn_block(const KnnArgs& a, const int L, unsigne
           const int s0 = cell_end[y * G.nx + xa], s1 = cell_end[y * G.nx + xb2 + 1];
           for (int s = s0; s < s1; ++s) {
             const int j = sorted[s];
-            if (j != i) knn_consider<K>(kr, kj, pxi, pyi, lpos[j], j);
+            if (j != i) knn_consider<K>(kr, kj, pxi, pyi, lpos[j], j, N);
           }
         };
         for (int d = 0; d <= dmax; ++d) {
@@ -1813,7 +1823,7 @@ __device__ __forceinline__ void knn_block(const KnnArgs& a, const int L, unsigne
       }
     } else if (need && !GF_ABLATE(a, 0x2000)) {
       for (int j = 0; j < N; ++j)
-        if (j != i) knn_consider<K>(kr, kj, pxi, pyi, pos(j), j);
+        if (j != i) knn_consider<K>(kr, kj, pxi, pyi, pos(j), j, N);
     }
     // self last (its r2 is inf in the reference), for k >= the agents with finite r2
     if (need) knn_insert<K>(kr, kj, __builtin_inf(), i);

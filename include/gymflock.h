@@ -120,7 +120,9 @@ int fe_get_config(const fe_handle* h, fe_config* out);
 /* Change comm_radius, dt, action_scalar, mean_pooling and centralized for the following
  * launches, keeping the state (the reference reads these attributes at call time, e.g.
  * self.centralized in controller() :200-201). n_agents, n_envs, n_neighbors and device
- * must equal the handle's (GF_EINVAL otherwise). */
+ * must equal the handle's (GF_EINVAL otherwise). A change of comm_radius, centralized or
+ * action_scalar drops the last controller output (it was computed under the old values):
+ * FE_U_EXPERT and fe_get_controls then need a new fe_controller / FE_WITH_CONTROLLER. */
 int fe_set_params(fe_handle* h, const fe_config* cfg);
 
 /* State ---------------------------------------------------------------------- */

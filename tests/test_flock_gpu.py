@@ -594,6 +594,51 @@ def test_knn_small_env_cases_vs_oracle(n):
     env.close()
 
 
+@pytest.mark.parametrize("n", [192, 193])
+def test_knn_one_env_window_edges_vs_oracle(n):
+    """The one-env exact kNN window at its upper edge (kStepExactKnnMaxOneEnv = 192,
+    csrc/flock_internal.h): a handle of one env with N = 192 takes the exact in-step
+    ranking (the largest KX tile of one env), N = 193 the fused-key ranking with the rim
+    kernel. The nine kNN shapes in both agent orders through FlockingEnv.step in direct
+    mode (one fe_step_host_knn call), then `u = env.controller(); env.step(u)` with the
+    next expert action fused into the step (fe_step_host_knn_ctrl), and through a
+    one-env batched handle (FE_WITH_KNN). Indices bit-exact, observations exact, states
+    bit-exact, controls rtol 1e-9, against the oracle (flocking.py:20-25)."""
+    from gym_flock.envs.flocking.flocking import FlockingEnv
+    cases = _small_knn_cases(n, np.random.RandomState(3300 + n))
+    env = FlockingEnv()
+    env.n_agents = n
+    env._make_spaces()
+    h = nat.FlockHandle(n, 1, n_neighbors=7)
+    for case in KNN_CASES:
+        for x0 in (cases[case], cases[case][::-1].copy()):
+            u0 = np.zeros((n, 2), np.float32)
+            x1 = orc.integrate(x0, u0)
+            ridx, robs = orc.knn_observation(x1, 7)
+            h.set_state(x0[None])
+            h.step(u0[None], nat.FE_WITH_KNN)
+            idx, obs = h.knn(0)
+            np.testing.assert_array_equal(idx, ridx, err_msg=case + " (handle)")
+            np.testing.assert_array_equal(obs, robs.astype(np.float32), err_msg=case + " (handle)")
+            env.x = x0
+            (eobs, _), _, _, _ = env.step(u0)
+            np.testing.assert_array_equal(env.x, x1, err_msg=case)
+            np.testing.assert_array_equal(env.nearest, ridx, err_msg=case + " (env)")
+            np.testing.assert_array_equal(eobs, robs.astype(np.float32), err_msg=case + " (env)")
+            u = env.controller()
+            np.testing.assert_allclose(u, orc.controller(x1), rtol=1e-9, atol=1e-12, err_msg=case)
+            (eobs, _), _, _, _ = env.step(u)
+            ref = orc.step(x1, u, with_controller=True)
+            ridx2, robs2 = orc.knn_observation(ref["x"], 7)
+            np.testing.assert_array_equal(env.x, ref["x"], err_msg=case + " (fused)")
+            np.testing.assert_array_equal(env.nearest, ridx2, err_msg=case + " (fused)")
+            np.testing.assert_array_equal(eobs, robs2.astype(np.float32), err_msg=case + " (fused)")
+            assert env._ctrl_cache is not None  # made by the step's own launch
+            np.testing.assert_allclose(env.controller(), ref["ctrl"], rtol=1e-9, atol=1e-12, err_msg=case)
+    h.close()
+    env.close()
+
+
 @pytest.mark.parametrize("n", [100, 128, 129])
 def test_knn_small_env_continuous(n):
     """30 continuous Flocking-v0 steps of 4 envs at N around the exact-ranking limit
