@@ -135,6 +135,16 @@ struct fe_handle {
   hipEvent_t step_ev = nullptr;
   hipEvent_t step_ev2 = nullptr;        // the gather's wait on stream2 (split steps)
   hipEvent_t h2d_ev = nullptr;          // completion of the borrowed host-action copy
+  // Host actions of split steps (fe_step without FE_U_*): copied on a stream of their own
+  // into one of two device buffers, so the copy for step t+1 runs while step t computes;
+  // buffer k is rewritten only after both halves of the step that read it (two calls
+  // back) have finished (ev_uread), and both halves of its step wait for its copy.
+  hipStream_t ustream = nullptr;
+  void* ubuf[2] = {nullptr, nullptr};   // (B,N,2) up to float64 each
+  hipEvent_t ev_ucopy[2] = {nullptr, nullptr};
+  hipEvent_t ev_uread[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  bool uread_live[2] = {false, false};
+  int ucur = 0;
   // ring slots a reward gather's staging copy still reads: steps [first, ...) until the
   // copy kernel (on the side stream) has stored `seq` into completion word kWordRing
   struct RingRead {
@@ -441,6 +451,7 @@ void release(fe_handle* h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->kstream) hipStreamSynchronize(h->kstream);
+  if (h->ustream) hipStreamSynchronize(h->ustream);
   comm_release(h, false);
   void* bufs[] = {h->x[0], h->x[1], h->u, h->ctrl[0], h->ctrl[1], h->sv, h->net, h->reward_ring,
                   h->knn_idx[0], h->knn_idx[1], h->knn_obs[0], h->knn_obs[1], h->knn_r2[0], h->knn_r2[1], h->knn_rimflag[0], h->knn_rimflag[1], h->vel_diffs, h->min_dists, h->degree, h->stats_sum, h->dt_env,
@@ -453,8 +464,12 @@ void release(fe_handle* h) {
   for (hipEvent_t e : h->ev) hipEventDestroy(e);
   if (h->h2d_ev) hipEventDestroy(h->h2d_ev);
   for (hipEvent_t e : {h->ev_s2, h->ev_main, h->tw[0], h->tw[1], h->ev_kin[0], h->ev_kin[1], h->ev_kjoin,
-                       h->kread[0].ev, h->kread[1].ev})
+                       h->kread[0].ev, h->kread[1].ev, h->ev_ucopy[0], h->ev_ucopy[1], h->ev_uread[0][0],
+                       h->ev_uread[0][1], h->ev_uread[1][0], h->ev_uread[1][1]})
     if (e) hipEventDestroy(e);
+  for (void* p : h->ubuf)
+    if (p) hipFree(p);
+  if (h->ustream) hipStreamDestroy(h->ustream);
   if (h->kstream) hipStreamDestroy(h->kstream);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
@@ -1030,6 +1045,25 @@ int fe_compute_helpers(fe_handle* h, int flags) {
   return GF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// The host-action copy stream and its two device buffers (fe_handle::ustream), on first use.
+int ensure_ucopy(fe_handle* h) {
+  if (h->ustream) return GF_OK;
+  for (int k = 0; k < 2; ++k) {
+    if (int rc = dalloc(reinterpret_cast<double**>(&h->ubuf[k]), h->BN * 2)) return rc;
+    GF_HIP(hipEventCreateWithFlags(&h->ev_ucopy[k], hipEventDisableTiming));
+    GF_HIP(hipEventCreateWithFlags(&h->ev_uread[k][0], hipEventDisableTiming));
+    GF_HIP(hipEventCreateWithFlags(&h->ev_uread[k][1], hipEventDisableTiming));
+  }
+  GF_HIP(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
+  return GF_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int fe_step(fe_handle* h, const void* u, int flags) {
   if (!h) return fail(GF_EINVAL, "null handle");
   if (!h->has_state) return fail(GF_ESTATE, "state not set (call fe_set_state first)");
@@ -1037,6 +1071,7 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   const bool ctrl = flags & FE_WITH_CONTROLLER;
   bool uf64 = flags & FE_U_F64;
   const void* up = nullptr;
+  int uk = -1;  // the action buffer of a split step's host actions (ubuf), or none
   if (flags & FE_U_EXPERT) {
     if (!h->has_ctrl) return fail(GF_ESTATE, "FE_U_EXPERT needs a previous controller output");
     up = h->ctrl[h->ccur];
@@ -1053,6 +1088,20 @@ int fe_step(fe_handle* h, const void* u, int flags) {
     // their phase (no de-phasing: that is for the first split step after other work)
     up = u;
     h->main_dirty = true;
+  } else if (split_next(h, h->cfg.n_envs)) {
+    // a split step: the copy on the action stream, overlapping the step before
+    if (int rc = ensure_ucopy(h)) return rc;
+    uk = h->ucur;
+    h->ucur ^= 1;
+    if (h->uread_live[uk]) {  // both halves of the step that read this buffer
+      GF_HIP(hipStreamWaitEvent(h->ustream, h->ev_uread[uk][0], 0));
+      GF_HIP(hipStreamWaitEvent(h->ustream, h->ev_uread[uk][1], 0));
+    }
+    GF_HIP(hipMemcpyAsync(h->ubuf[uk], u, h->BN * 2 * (uf64 ? 8 : 4), hipMemcpyHostToDevice, h->ustream));
+    GF_HIP(hipEventRecord(h->ev_ucopy[uk], h->ustream));
+    GF_HIP(hipStreamWaitEvent(h->stream, h->ev_ucopy[uk], 0));
+    GF_HIP(hipStreamWaitEvent(h->stream2, h->ev_ucopy[uk], 0));
+    up = h->ubuf[uk];
   } else {
     // the previous step's second half may still read h->u: copy after it
     if (int rc = join_s2(h)) return rc;
@@ -1074,6 +1123,11 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   const int km = knn_mode(h, flags, true);
   if (int rc = prepare_outputs(h, flags, a, h->cur ^ 1)) return rc;
   if (int rc = timed_launch(h, a, true, uf64, ctrl)) return rc;
+  if (uk >= 0) {  // the halves that read the buffer: the copy two calls on waits for them
+    GF_HIP(hipEventRecord(h->ev_uread[uk][0], h->stream));
+    GF_HIP(hipEventRecord(h->ev_uread[uk][1], h->last_b0 ? h->stream2 : h->stream));
+    h->uread_live[uk] = true;
+  }
   h->cur ^= 1;
   if (ctrl) h->ccur ^= 1;
   h->has_ctrl = ctrl;
@@ -1083,7 +1137,8 @@ int fe_step(fe_handle* h, const void* u, int flags) {
   if (km)
     if (int rc = launch_knn_cur(h, km)) return rc;
   // the host action buffer is borrowed only for this call: wait for its copy, not the step
-  if (!(flags & (FE_U_DEVICE | FE_U_EXPERT | FE_U_RESIDENT))) GF_HIP(hipEventSynchronize(h->h2d_ev));
+  if (uk >= 0) GF_HIP(hipEventSynchronize(h->ev_ucopy[uk]));
+  else if (!(flags & (FE_U_DEVICE | FE_U_EXPERT | FE_U_RESIDENT))) GF_HIP(hipEventSynchronize(h->h2d_ev));
   return GF_OK;
 }
 

@@ -105,3 +105,48 @@ def test_device_actions_split_match_single_stream():
         h.step(us[t])
     np.testing.assert_array_equal(h.get_state(), outs[0][-3])
     h.close()
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_host_actions_pipelined_split_steps(f64):
+    """Host actions of split steps go through the action stream into two device buffers,
+    so each copy overlaps the step before. 16 back-to-back steps, each call given the same
+    numpy array overwritten right after it returns (the call must have copied it by then),
+    with resident-action steps and a getter mixed in: every state and reward bit-exact
+    against one-launch steps on a second handle with the actions set per step, and
+    against the oracle for two envs."""
+    from oracle import flocking as orc
+    B, N, T = 6, 256, 16
+    x0 = synthetic_batch(B, N, seed0=77)
+    us = np.random.RandomState(5).uniform(-1, 1, size=(T, B, N, 2)).astype(np.float64 if f64 else np.float32)
+    flags = nat.FE_U_F64 if f64 else 0
+    h = nat.FlockHandle(N, B)
+    g = nat.FlockHandle(N, B)
+    g.set_streams(1)
+    h.set_state(x0)
+    g.set_state(x0)
+    buf = np.empty_like(us[0])
+    rew_h, rew_g = [], []
+    for t in range(T):
+        if t == 9:
+            h.set_actions(us[t])
+            h.step(None, nat.FE_U_RESIDENT | flags)
+        else:
+            buf[...] = us[t]
+            h.step(buf, flags)
+            buf[...] = np.nan  # the borrowed array is free again once the call returned
+        g.set_actions(us[t])
+        g.step(None, nat.FE_U_RESIDENT | flags)
+        if t % 5 == 4:  # (a getter: the step after it is one launch, the others split)
+            np.testing.assert_array_equal(h.get_state(), g.get_state())
+            rew_h.append(h.rewards())
+            rew_g.append(g.rewards())
+    np.testing.assert_array_equal(h.get_state(), g.get_state())
+    np.testing.assert_array_equal(np.array(rew_h), np.array(rew_g))
+    for b in (0, B - 1):
+        x = x0[b]
+        for t in range(T):
+            x = orc.integrate(x, us[t, b])
+        np.testing.assert_array_equal(h.get_state(b), x)
+    h.close()
+    g.close()
