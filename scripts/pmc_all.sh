@@ -1,5 +1,5 @@
 #!/bin/bash
-# Summarise a profile session's PMC passes (scripts/r05_profile.sh) into
+# Summarise a profile session's PMC passes (scripts/session_recipes.sh r05_profile) into
 # profiles/pmc_traffic.json: per-launch HBM bytes of each bench sub-line's kernel beside its
 # algorithmic bytes per launch.   bash scripts/pmc_all.sh gpurun_out/r05_v2
 D=$1

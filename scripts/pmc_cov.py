@@ -7,7 +7,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-flock_amd")]
-from gym_flock.envs.spatial.maps import generate_targets  # noqa: E402
+from oracle.maps_host import generate_targets  # noqa: E402
 from gym_flock.vec import VecCoverage  # noqa: E402
 
 R, B, M = 200, 512, 1000

@@ -1,5 +1,5 @@
 """Per-launch instruction counters of the step kernels from rocprofv3 --pmc csv dirs
-(scripts/r03_s15.sh): one line per configuration, per-wave VALU/SALU/LDS and the VALU
+(scripts/session_recipes.sh r03_s15): one line per configuration, per-wave VALU/SALU/LDS and the VALU
 issue time they imply (wave64 VALU = 4 cycles of a 16-lane SIMD, 1024 SIMDs, 2.4 GHz).
   python scripts/pmc_mix.py gpurun_out/s15"""
 import collections

@@ -9,7 +9,7 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-flock_amd"))
-from gym_flock.envs.spatial.maps import generate_targets  # noqa: E402
+from oracle.maps_host import generate_targets  # noqa: E402
 from gym_flock.vec import VecCoverage  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "run"
