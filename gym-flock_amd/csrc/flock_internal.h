@@ -10,7 +10,11 @@ namespace gf {
 // Ablation switches (StepArgs / KnnArgs .diag, timing experiments that give wrong
 // outputs) exist only in the diagnostic build (make diag: -DGF_DIAG); the product build
 // compiles every such branch out.
-#ifdef GF_DIAG
+// -DGF_CT_ABLATE=<mask>: the same switches as compile-time constants, for register
+// studies (scripts/vgpr_phases.sh: each phase compiled out, -Rpass-analysis per build).
+#if defined(GF_CT_ABLATE)
+#define GF_ABLATE(args, bits) ((static_cast<unsigned long long>(GF_CT_ABLATE) & (bits)) != 0)
+#elif defined(GF_DIAG)
 #define GF_ABLATE(args, bits) (((args).diag & (bits)) != 0)
 #else
 #define GF_ABLATE(args, bits) false

@@ -799,7 +799,10 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, const St* tile,
 // no spills; its LDS is floored to hold it at 6 workgroups per CU, see
 // kStepLdsPlainFloor), 6 with the controller (79 VGPRs, 23.2 KiB of LDS: 6 per CU);
 // variants are not capped (their extra state would spill).
-constexpr int kWavesPlain = 6, kWavesPf = 4, kWavesCtrl = 6, kWavesKnn = 5, kWavesKnnCtrl = 4;
+#ifndef GF_WAVES_KNN  // register studies (scripts/vgpr_phases.sh) may raise it
+#define GF_WAVES_KNN 5
+#endif
+constexpr int kWavesPlain = 6, kWavesPf = 4, kWavesCtrl = 6, kWavesKnn = GF_WAVES_KNN, kWavesKnnCtrl = 4;
 // Phase timeline instrumentation (diagnostic builds only, -DGF_STAMPS): lane 0 of
 // wave 0 records s_memrealtime (100 MHz) at phase boundaries of each workgroup, plus
 // its HW_ID / XCC_ID, for scripts/phase_timeline.py. Product builds compile it out.
