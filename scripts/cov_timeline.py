@@ -21,7 +21,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "gym-flock_amd"))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-flock_amd")]
 from gym_flock import _native as nat  # noqa: E402
 from oracle.maps_host import generate_targets  # noqa: E402
 from gym_flock.vec import VecCoverage  # noqa: E402

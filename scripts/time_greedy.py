@@ -8,7 +8,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-flock_amd"))
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."), os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-flock_amd")]
 from oracle.maps_host import generate_targets  # noqa: E402
 from gym_flock.vec import VecCoverage  # noqa: E402
 
