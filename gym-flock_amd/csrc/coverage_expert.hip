@@ -662,9 +662,12 @@ namespace {
 // ballots on its bits. (Round 5 visited the distinct counts one by one, a pass over the
 // row per count: ~100 passes on a map's longer rows, 5.7 ms for 512 maps.)
 constexpr int kListBins = 1024;  // hop counts 0 .. MAX_COST - 1
+// bin v's LDS word: one pad word per 16 bins, so the scan's lane-contiguous runs of 16
+// bins sit in distinct banks (lane l's run starts at word 17 l)
+__device__ __forceinline__ uint32_t list_bin(uint32_t v) { return v + (v >> 4); }
 
 __global__ __launch_bounds__(256) void cov_greedy_list_kernel(CovTmArgs a) {
-  __shared__ uint32_t bins_s[4][kListBins];
+  __shared__ uint32_t bins_s[4][kListBins + kListBins / 16];
   __shared__ uint16_t vv_s[4][kGreedyListMaxT], ee_s[4][kGreedyListMaxT];
   const int b = a.envs[blockIdx.x];
   const int c = blockIdx.y * 4 + (int)(threadIdx.x >> 6);
@@ -680,7 +683,7 @@ __global__ __launch_bounds__(256) void cov_greedy_list_kernel(CovTmArgs a) {
   const int32_t* nb = a.nbr + row * 4;
   const int n = a.cnt[row];
   const int nb0 = nb[0], nb1 = nb[1], nb2 = nb[2], nb3 = nb[3];
-  for (int q = lane; q < kListBins; q += 64) bins[q] = 0u;
+  for (int q = lane; q < kListBins + kListBins / 16; q += 64) bins[q] = 0u;
   for (int t = lane; t < T; t += 64) {
     const uint32_t v = cost[t];
     const bool listed = v != kInf && v < (uint32_t)kMaxCost;  // inf -> MAX_COST: never argmin-chosen
@@ -700,11 +703,11 @@ __global__ __launch_bounds__(256) void cov_greedy_list_kernel(CovTmArgs a) {
     }
     vv[t] = listed ? (uint16_t)v : (uint16_t)0xFFFFu;
     ee[t] = (uint16_t)((uint32_t)t | act << 10 | flag << 12);
-    if (listed) atomicAdd(&bins[v], 1u);
+    if (listed) atomicAdd(&bins[list_bin(v)], 1u);
   }
   constexpr int BPL = kListBins / 64;  // bins per lane
   uint32_t run = 0;
-  for (int q = 0; q < BPL; ++q) run += bins[lane * BPL + q];
+  for (int q = 0; q < BPL; ++q) run += bins[lane * (BPL + 1) + q];
   uint32_t incl = run;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -714,8 +717,8 @@ __global__ __launch_bounds__(256) void cov_greedy_list_kernel(CovTmArgs a) {
   const uint32_t len = (uint32_t)__shfl((int)incl, 63, 64);
   uint32_t off = incl - run;
   for (int q = 0; q < BPL; ++q) {
-    const uint32_t k = bins[lane * BPL + q];
-    bins[lane * BPL + q] = off;
+    const uint32_t k = bins[lane * (BPL + 1) + q];
+    bins[lane * (BPL + 1) + q] = off;
     off += k;
   }
   uint16_t* out = a.glist + row * a.gstride;
@@ -733,11 +736,11 @@ __global__ __launch_bounds__(256) void cov_greedy_list_kernel(CovTmArgs a) {
     }
     uint32_t base = 0;
     if (listed) {
-      base = bins[v];
+      base = bins[list_bin(v)];
       out[base + (uint32_t)__popcll(eq & below_me)] = ee[t];
     }
     // the class's lowest lane advances its offset after every lane of the class read it
-    if (listed && (eq & below_me) == 0ull) bins[v] = base + (uint32_t)__popcll(eq);
+    if (listed && (eq & below_me) == 0ull) bins[list_bin(v)] = base + (uint32_t)__popcll(eq);
   }
   if (lane == 0) a.glen[row] = (uint16_t)len;
 }
