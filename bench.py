@@ -1171,8 +1171,8 @@ def main():
         from gym_flock import _native as nat
         line["runtime"] = nat.runtime_info()  # the HIP runtime and RCCL this process measured on
         if world == 1 and not args.no_other_configs:
-            log("config 4 (Coverage R=200 x 512)...")
-            line["coverage_config4"] = bench_config4(args)
+            log("config 4 (Coverage R=200 x 512, with the greedy expert and per-episode maps)...")
+            line["coverage_config4"] = bench_config4(args, with_greedy=True)
             log("config 5 (N=8192 x 32)...")
             line["n8192_config5"] = bench_config5(args)
             log("drop-in single-env path (N=100, 1024)...")

@@ -1571,8 +1571,75 @@ GYMFLOCK_LIB=$PWD/gym-flock_amd/lib/libgymflock.so R=200 timeout -k 10 120 pytho
 echo "tree R=200 first steps: $(grep 'step 0' $O/probe_r200.txt | awk '{print $5}' | tr '\n' ' ')"
 }
 
+r06_profile_a() {
+# Round-6 measurement set, part A: the GPU suite, smoke, the default bench line (driver
+# window, with the CPU baseline, the greedy expert and the new-map episode of config 4) and at
+# 200 steps, the Coverage workload, the multi-rank path at one rank (--force-dist), and the
+# time-matrix + greedy-list build of 512 distinct device maps (scripts/time_tm.py).
+#   bash scripts/session_recipes.sh r06_profile_a v1   -> gpurun_out/r06_<tag>/
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-v1}
+R=$PWD
+O=$R/gpurun_out/r06_$TAG
+mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|ERROR" $O/pytest_gpu.log | head; tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
+tail -1 $O/smoke.txt
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err || { tail $O/bench20.err; exit 1; }
+echo "bench20 ok"
+timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench200.json 2> $O/bench200.err || { tail $O/bench200.err; exit 1; }
+echo "bench200 ok"
+timeout -k 10 300 python bench.py --workload coverage --steps 200 --warmup 20 --no-cpu-baseline > $O/bench_cov.json 2> $O/bench_cov.err || { tail $O/bench_cov.err; exit 1; }
+echo "bench_cov ok"
+timeout -k 10 400 python bench.py --force-dist --steps 20 --warmup 5 --no-cpu-baseline --no-other-configs > $O/bench_forcedist.json 2> $O/bench_forcedist.err || { tail $O/bench_forcedist.err; exit 1; }
+echo "bench_forcedist ok"
+ROUNDS=8 timeout -k 10 300 python scripts/time_tm.py r06 > $O/time_tm.json 2> $O/time_tm.err || { tail $O/time_tm.err; exit 1; }
+cat $O/time_tm.json
+}
+
+r06_profile_b() {
+# Round-6 measurement set, part B: a rocprofv3 kernel trace + stats of a 100-step bench with
+# its per-grid kernel stats (scripts/trace_by_grid.py), PMC HBM traffic (FETCH_SIZE and
+# WRITE_SIZE passes) of every bench sub-line's kernel (summarised by scripts/pmc_all.sh), and
+# three more driver-window lines for the run-to-run spread.
+#   bash scripts/session_recipes.sh r06_profile_b v1   -> gpurun_out/r06_<tag>/
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-v1}
+R=$PWD
+O=$R/gpurun_out/r06_$TAG
+mkdir -p $O; export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o trace -- python3 $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $O/rocprof_trace.log 2>&1 || { tail $O/rocprof_trace.log; exit 1; }
+cd $R
+python scripts/trace_by_grid.py $O/trace/trace_kernel_trace.csv $O/trace_by_grid --steps 100 > $O/trace_by_grid.txt && cat $O/trace_by_grid.txt
+cd /tmp
+pmc() {  # pmc <name> <script> [env...]
+  local name=$1 script=$2; shift 2
+  for c in FETCH_SIZE WRITE_SIZE; do
+    env "$@" timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${name}_$c -o pmc -- python3 $R/scripts/$script > $O/pmc_${name}_$c.log 2>&1 || return 1
+  done
+}
+pmc plain pmc_step.py &&
+pmc ctrl pmc_step.py MODE=ctrl &&
+pmc packed pmc_step.py MODE=packed &&
+pmc knn pmc_step.py KNN=1 &&
+pmc n8192 pmc_step.py N=8192 B=32 &&
+pmc cov pmc_cov.py || { echo "pmc failed"; exit 1; }
+cd $R
+bash scripts/pmc_all.sh $O > $O/pmc_all.txt 2>&1; echo "pmc_all rc=$?"; cat $O/pmc_all.txt
+for r in 1 2 3; do timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-other-configs > $O/bench20_rep$r.json 2>/dev/null || exit 1; done
+python - $O <<'PY'
+import json, sys
+for r in (1, 2, 3):
+    d = json.loads(open("%s/bench20_rep%d.json" % (sys.argv[1], r)).read().strip().splitlines()[-1])
+    print("rep", r, round(d["ms_per_step"] * 1e3, 2), "us", round(d["roofline"]["frac"], 3),
+          "knn", round(d["flocking_v0_knn7"]["ms_per_step"] * 1e3, 2), round(d["flocking_v0_knn7"]["ratio_to_plain_step"], 3))
+PY
+}
+
 if [ $# -lt 1 ]; then
-  echo "usage: $0 <session> [args]   sessions: r03_ab1 r03_ab2 r03_profile r03_session r03_s3 r03_s4 r03_s5 r03_s6 r03_s7 r03_s8 r03_s9 r03_s10 r03_s11 r03_s12 r03_s13 r03_s14 r03_s15 r03_s16 r03_s17 r03_s18 r03_s19 r03_s20 r03_s21 r03_s22 r03_s25 r03_s26 r03_s27 r03_s28 r03_s29 r03_s30 r03_s31 r03_s32 r03_s33 r03_s34 r03_s35 r03_s36 r03_s37 r03_s38 r03_s39 r04_final r04_profile r04_session r04_s3 r04_s4 r04_s5 r04_s7 r04_s8 r04_s9 r04_s10 r04_s11 r04_s12 r04_s13 r04_s14 r04_s15 r04_s16 r04_s17 r04_s18 r04_s19 r04_s20 r04_s21 r04_s22 r04_s23 r04_s24 r04_s25 r04_s26 r04_s27 r04_s28 r04_s29 r04_s30 r04_s31 r04_s32 r04_s33 r04_s34 r05_profile r05_s1 r05_s2 r05_s3 r05_s4 r05_s5 r05_s6 r05_s7 r05_s8 r05_s9 r05_s10 r05_s11 r05_s12 r05_s13 r05_s14 r05_s15 r05_s16 r05_s17 r05_s18 r05_s19 r05_s20 r05_s21 r05_s22 r05_s23 r05_s24 r05_s25 r05_s26 r05_s27"
+  echo "usage: $0 <session> [args]   sessions: r03_ab1 r03_ab2 r03_profile r03_session r03_s3 r03_s4 r03_s5 r03_s6 r03_s7 r03_s8 r03_s9 r03_s10 r03_s11 r03_s12 r03_s13 r03_s14 r03_s15 r03_s16 r03_s17 r03_s18 r03_s19 r03_s20 r03_s21 r03_s22 r03_s25 r03_s26 r03_s27 r03_s28 r03_s29 r03_s30 r03_s31 r03_s32 r03_s33 r03_s34 r03_s35 r03_s36 r03_s37 r03_s38 r03_s39 r04_final r04_profile r04_session r04_s3 r04_s4 r04_s5 r04_s7 r04_s8 r04_s9 r04_s10 r04_s11 r04_s12 r04_s13 r04_s14 r04_s15 r04_s16 r04_s17 r04_s18 r04_s19 r04_s20 r04_s21 r04_s22 r04_s23 r04_s24 r04_s25 r04_s26 r04_s27 r04_s28 r04_s29 r04_s30 r04_s31 r04_s32 r04_s33 r04_s34 r05_profile r05_s1 r05_s2 r05_s3 r05_s4 r05_s5 r05_s6 r05_s7 r05_s8 r05_s9 r05_s10 r05_s11 r05_s12 r05_s13 r05_s14 r05_s15 r05_s16 r05_s17 r05_s18 r05_s19 r05_s20 r05_s21 r05_s22 r05_s23 r05_s24 r05_s25 r05_s26 r05_s27 r06_profile_a r06_profile_b"
   exit 2
 fi
 "$@"
