@@ -89,6 +89,23 @@ static void validation_paths() {
   char hp[512], rp[512];
   CHECK(fe_runtime_info(nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0) == 0);
   CHECK(fe_runtime_info(&rt, &drv, &nccl, hp, sizeof hp, rp, sizeof rp) == 0 && rt > 0 && nccl > 0);
+  // round-6 map entry points: the host-only lattice query, null handles and configs
+  cov_map_config mc{};
+  int32_t nl = 0;
+  CHECK(cov_map_lattice(nullptr, nullptr, &nl) != 0);
+  CHECK(cov_map_lattice(&mc, nullptr, &nl) != 0);  // zero spacing
+  mc.x_min = mc.y_min = -20.0;
+  mc.x_max = mc.y_max = 20.0;
+  mc.lattice_spacing = 5.5;
+  mc.world_radius = 20.0;
+  mc.road_radius = mc.link_radius = 6.6;
+  mc.near_radius = 6.6 / 1.4;
+  mc.n_cities = 12;
+  CHECK(cov_map_lattice(&mc, nullptr, &nl) == 0 && nl > 0);
+  std::vector<double> lat((size_t)nl * 2);
+  CHECK(cov_map_lattice(&mc, lat.data(), &nl) == 0);
+  CHECK(cov_generate_maps(nullptr, &mc, -1, 0, nullptr, COV_MAP_SEED, nullptr, nullptr, nullptr) != 0);
+  CHECK(cov_get_targets(nullptr, 0, lat.data()) != 0);
 }
 
 static bool have_device() {
@@ -286,6 +303,59 @@ static void coverage_session() {
   CHECK(cov_destroy(h) == 0);
 }
 
+// Per-episode maps: the lattice query, seeded and continued device streams, given cities,
+// the targets read back, a map too big for its handle, then a step on the new maps.
+static void map_session() {
+  cov_map_config mc{};
+  mc.x_min = mc.y_min = -120.0;
+  mc.x_max = mc.y_max = 120.0;
+  mc.lattice_spacing = 5.5;
+  mc.world_radius = 120.0;
+  mc.road_radius = mc.link_radius = 6.6;
+  mc.near_radius = 6.6 / 1.4;
+  mc.n_cities = 12;
+  int32_t nl = 0;
+  CHECK(cov_map_lattice(&mc, nullptr, &nl) == 0 && nl > 0);
+  std::vector<double> lat((size_t)nl * 2);
+  int32_t short_n = 3;
+  CHECK(cov_map_lattice(&mc, lat.data(), &short_n) != 0 && short_n == nl);  // capacity short
+  CHECK(cov_map_lattice(&mc, lat.data(), &nl) == 0);
+  const int R = 6, B = 2;
+  cov_config cc{};
+  cc.n_robots = R;
+  cc.n_envs = B;
+  cc.max_nodes = 1000;
+  cc.episode_length = 75;
+  cc.res = 5.5;
+  cc.motion_radius = 6.6;
+  cc.device = 0;
+  cc.horizon = -1;
+  cov_handle* h = nullptr;
+  CHECK(cov_create(&cc, &h) == 0);
+  if (!h) return;
+  std::vector<int32_t> nt(B), st(B);
+  std::vector<double> cities((size_t)B * 12 * 2);
+  CHECK(cov_generate_maps(h, &mc, -1, 8, nullptr, COV_MAP_SEED, nt.data(), st.data(), cities.data()) == 0);
+  for (int b = 0; b < B; ++b) CHECK(nt[b] > R && nt[b] <= 1000 - R);
+  CHECK(cov_generate_maps(h, &mc, 1, 0, nullptr, 0, nt.data(), st.data(), nullptr) == 0);  // stream continues
+  CHECK(cov_generate_maps(h, &mc, 0, 0, cities.data(), COV_MAP_CITIES, nt.data(), st.data(), nullptr) == 0);
+  std::vector<double> tg((size_t)nt[0] * 2);
+  CHECK(cov_get_targets(h, 0, tg.data()) == 0);
+  CHECK(cov_get_targets(h, B, tg.data()) != 0);
+  mc.n_cities = 33;  // more than the kernel holds
+  CHECK(cov_generate_maps(h, &mc, -1, 8, nullptr, COV_MAP_SEED, nt.data(), st.data(), nullptr) != 0);
+  CHECK(cov_destroy(h) == 0);
+  // the same maps cannot fit a handle of 200 nodes: GF_EINVAL with the sizes reported
+  cc.max_nodes = 200;
+  mc.n_cities = 12;
+  CHECK(cov_create(&cc, &h) == 0);
+  if (!h) return;
+  CHECK(cov_generate_maps(h, &mc, -1, 8, nullptr, COV_MAP_SEED, nt.data(), st.data(), nullptr) != 0);
+  CHECK((st[0] & COV_MAP_TOO_MANY) != 0);
+  CHECK(std::strlen(fe_last_error()) > 0);
+  CHECK(cov_destroy(h) == 0);
+}
+
 static void graph_session() {
   gu_graph* g = nullptr;
   CHECK(gu_create(0, &g) == 0);
@@ -311,6 +381,7 @@ int main() {
     std::printf("device present: running the GPU sessions\n");
     flocking_session();
     coverage_session();
+    map_session();
     graph_session();
   } else {
     std::printf("no device: validation and no-device paths only\n");
