@@ -1636,6 +1636,16 @@ for r in (1, 2, 3):
     print("rep", r, round(d["ms_per_step"] * 1e3, 2), "us", round(d["roofline"]["frac"], 3),
           "knn", round(d["flocking_v0_knn7"]["ms_per_step"] * 1e3, 2), round(d["flocking_v0_knn7"]["ratio_to_plain_step"], 3))
 PY
+# the Coverage step's launch floor: wall, kernel and host enqueue time per step with one and
+# two launches per step, with the runtime's kernel arguments in device memory (its default)
+# and in host memory (HIP_FORCE_DEV_KERNARG=0)
+for st in 2 1; do for ka in dflt 0; do
+  if [ $ka = dflt ]; then e=""; else e="HIP_FORCE_DEV_KERNARG=0"; fi
+  env $e STREAMS=$st ROUNDS=5 timeout -k 10 120 python scripts/time_cov.py s${st}_ka$ka >> $O/cov_launch_floor.txt 2>&1 || exit 1
+done; done
+cat $O/cov_launch_floor.txt
+HIP_FORCE_DEV_KERNARG=0 timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench20_ka0.json 2> $O/bench20_ka0.err || { tail $O/bench20_ka0.err; exit 1; }
+echo "bench20 (host kernargs) ok"
 }
 
 if [ $# -lt 1 ]; then
