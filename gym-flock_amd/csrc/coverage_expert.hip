@@ -181,6 +181,9 @@ __global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, 
   V* col = reinterpret_cast<V*>(smem);  // [T + 1][64], column T = dummy inf
   for (int t = 0; t <= T; ++t) col[t * kTmLanes + lane] = (t == src) ? 0 : (V)inf;
   int16_t* prevT = a.prevT + (size_t)b * Tm * Tm;  // [q][src]
+  // raw buffer over the env's [Tm][Tm] predecessors (stride 0: offsets range-checked
+  // against Tm * Tm * 2 bytes; dword 3 = gfx9's data format)
+  const __amdgpu_buffer_rsrc_t prv = __builtin_amdgcn_make_buffer_rsrc(prevT, 0, Tm * Tm * 2, 0x00020000);
   if (valid)
     for (int q = 0; q < T; ++q) prevT[(size_t)q * Tm + src] = -1;
   const uint32_t* sched = sched_all + (size_t)b * a.sched_stride;
@@ -215,7 +218,12 @@ __global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, 
         const bool better = via < vq[k];
         col[(w[k] >> 16) * kTmLanes + lane] = (V)(via < vq[k] ? via : vq[k]);
         changed |= better ? 1 : 0;
-        if (better) prevT[(size_t)(w[k] >> 16) * Tm + src] = (int16_t)(w[k] & 0xFFFF);
+        // the predecessor, branch-free: a lane that did not improve stores past the end
+        // of the buffer's range, which the hardware drops (no exec-mask branch per edge:
+        // 8.63 -> 8.05-8.11 ms for 512 maps, profiles/r06/ab_tm_branchfree.txt)
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w[k] & 0xFFFF), prv,
+                                              better ? (int)(((w[k] >> 16) * (uint32_t)Tm + src) * 2) : (int)0x7FFFFFF0,
+                                              0, 0);
       }
     }
     if (!PASS_B || sizeof(V) == 1) {
