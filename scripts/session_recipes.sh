@@ -1693,8 +1693,27 @@ print("step", d["ms_per_step"], "tm", g["time_matrix_ms_all_envs"], "new-map epi
 PY
 }
 
+r06_s3() {
+# Round 6, session 3: the time matrix's edge schedule read in 64-slot windows by vector
+# loads (build/lib_tm_vwin, -DGF_TM_VWIN=1) and, on top, batches software-pipelined within a
+# conflict level (build/lib_tm_pipe, -DGF_TM_PIPE=1), against the product's per-batch scalar
+# loads, three interleaved rounds; the Coverage greedy, maps and step tests on the variants.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r06_s3; mkdir -p $O
+for r in 1 2 3; do for v in prod tm_vwin tm_pipe; do
+  L=$PWD/build/lib_$v/libgymflock.so; [ $v = prod ] && L=$PWD/gym-flock_amd/lib/libgymflock.so
+  GYMFLOCK_LIB=$L timeout -k 10 120 python scripts/time_tm.py $v >> $O/ab_tm_vwin.txt 2>&1 || exit 1
+done; done
+cut -c1-110 $O/ab_tm_vwin.txt
+for v in tm_vwin tm_pipe prod; do
+  L=$PWD/build/lib_$v/libgymflock.so; [ $v = prod ] && L=$PWD/gym-flock_amd/lib/libgymflock.so
+  GYMFLOCK_LIB=$L timeout -k 10 400 python -u -m pytest tests/test_coverage_greedy_gpu.py tests/test_coverage_maps_gpu.py tests/test_coverage_gpu.py -q --timeout 120 --timeout-method thread > $O/tests_$v.log 2>&1; rc=$?; echo "$v: $(tail -1 $O/tests_$v.log)"; [ $rc -ne 0 ] && exit $rc
+done
+exit 0
+}
+
 if [ $# -lt 1 ]; then
-  echo "usage: $0 <session> [args]   sessions: r03_ab1 r03_ab2 r03_profile r03_session r03_s3 r03_s4 r03_s5 r03_s6 r03_s7 r03_s8 r03_s9 r03_s10 r03_s11 r03_s12 r03_s13 r03_s14 r03_s15 r03_s16 r03_s17 r03_s18 r03_s19 r03_s20 r03_s21 r03_s22 r03_s25 r03_s26 r03_s27 r03_s28 r03_s29 r03_s30 r03_s31 r03_s32 r03_s33 r03_s34 r03_s35 r03_s36 r03_s37 r03_s38 r03_s39 r04_final r04_profile r04_session r04_s3 r04_s4 r04_s5 r04_s7 r04_s8 r04_s9 r04_s10 r04_s11 r04_s12 r04_s13 r04_s14 r04_s15 r04_s16 r04_s17 r04_s18 r04_s19 r04_s20 r04_s21 r04_s22 r04_s23 r04_s24 r04_s25 r04_s26 r04_s27 r04_s28 r04_s29 r04_s30 r04_s31 r04_s32 r04_s33 r04_s34 r05_profile r05_s1 r05_s2 r05_s3 r05_s4 r05_s5 r05_s6 r05_s7 r05_s8 r05_s9 r05_s10 r05_s11 r05_s12 r05_s13 r05_s14 r05_s15 r05_s16 r05_s17 r05_s18 r05_s19 r05_s20 r05_s21 r05_s22 r05_s23 r05_s24 r05_s25 r05_s26 r05_s27 r06_profile_a r06_profile_b r06_s1 r06_s2"
+  echo "usage: $0 <session> [args]   sessions: r03_ab1 r03_ab2 r03_profile r03_session r03_s3 r03_s4 r03_s5 r03_s6 r03_s7 r03_s8 r03_s9 r03_s10 r03_s11 r03_s12 r03_s13 r03_s14 r03_s15 r03_s16 r03_s17 r03_s18 r03_s19 r03_s20 r03_s21 r03_s22 r03_s25 r03_s26 r03_s27 r03_s28 r03_s29 r03_s30 r03_s31 r03_s32 r03_s33 r03_s34 r03_s35 r03_s36 r03_s37 r03_s38 r03_s39 r04_final r04_profile r04_session r04_s3 r04_s4 r04_s5 r04_s7 r04_s8 r04_s9 r04_s10 r04_s11 r04_s12 r04_s13 r04_s14 r04_s15 r04_s16 r04_s17 r04_s18 r04_s19 r04_s20 r04_s21 r04_s22 r04_s23 r04_s24 r04_s25 r04_s26 r04_s27 r04_s28 r04_s29 r04_s30 r04_s31 r04_s32 r04_s33 r04_s34 r05_profile r05_s1 r05_s2 r05_s3 r05_s4 r05_s5 r05_s6 r05_s7 r05_s8 r05_s9 r05_s10 r05_s11 r05_s12 r05_s13 r05_s14 r05_s15 r05_s16 r05_s17 r05_s18 r05_s19 r05_s20 r05_s21 r05_s22 r05_s23 r05_s24 r05_s25 r05_s26 r05_s27 r06_profile_a r06_profile_b r06_s1 r06_s2 r06_s3"
   exit 2
 fi
 "$@"
