@@ -169,6 +169,10 @@ class VecCoverage:
         self.n_targets[:] = n
         return n, st
 
+    def targets(self, env):
+        """Env `env`'s current map, (n_targets, 2) float64 (cov_get_targets)."""
+        return self.h.targets(env, int(self.n_targets[env]))
+
     def reset(self, seed=0, draws="device", new_maps=False, map_seed=None):
         """Env b is a reference env whose np_random was seeded seed + env_offset + b: its
         reset draws (coverage.py:405-424), then its stream continues on the device for the

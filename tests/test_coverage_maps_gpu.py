@@ -160,7 +160,7 @@ def test_vec_reset_new_maps_then_expert_episode_vs_oracle():
                 np.testing.assert_array_equal(got[key].reshape(ref[key].shape), ref[key], err_msg="t=%d b=%d" % (t, b))
     v.reset(seed=12, new_maps=True)
     for b in range(B):
-        np.testing.assert_array_equal(v.h.targets(b, v.n_targets[b]), nxt[b])
+        np.testing.assert_array_equal(v.targets(b), nxt[b])
     v.close()
 
 
