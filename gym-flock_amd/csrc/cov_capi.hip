@@ -1,5 +1,6 @@
 // C-ABI of the Coverage-v0 engine (include/gymflock.h, cov_* functions).
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -543,9 +544,19 @@ int cov_generate_maps(cov_handle* h, const cov_map_config* mc, int env, uint64_t
   // 3 NC - 6 of them, none longer than the cities' square's diagonal), within the LDS left
   const double diag = 2.0 * std::sqrt(2.0) * mc->world_radius;
   const double wbound = NC + (3.0 * NC - 6.0) * (std::floor(diag / mc->road_radius) + 1.0);
-  const size_t lds_free = 150 * 1024 - (size_t)h->lat_L * 12;
-  if ((size_t)h->lat_L * 12 + 64 * 16 > 150 * 1024) return cfail(GF_EINVAL, "map: lattice too large for the LDS");
-  const int wcap = static_cast<int>(std::min<double>(wbound, (double)(lds_free / 16)));
+  const size_t lds_max = 150 * 1024, lds_lat = (size_t)h->lat_L * 12;
+  if (lds_lat + 64 * 16 > lds_max) return cfail(GF_EINVAL, "map: lattice too large for the LDS");
+  // the waypoint grid of the near-road test: cells of side near_radius (1 + 2^-20) over the
+  // cities' square and the arena, one cell of margin; without room for it (or for an odd
+  // configuration), every lattice point scans every waypoint
+  const double gh = mc->near_radius * (1.0 + 0x1p-20);
+  const double gx0 = std::min(mc->x_min, -mc->world_radius) - gh, gy0 = std::min(mc->y_min, -mc->world_radius) - gh;
+  const double gspan = std::max(std::max(mc->x_max, mc->world_radius) + gh - gx0, std::max(mc->y_max, mc->world_radius) + gh - gy0);
+  int G = (gh > 0.0 && std::isfinite(gspan / gh) && gspan / gh < 256.0) ? static_cast<int>(std::ceil(gspan / gh)) : 0;
+  const double wcap_scan = std::min<double>(wbound, (double)((lds_max - lds_lat) / 16));
+  const double wfit_g = G > 0 ? ((double)lds_max - (double)lds_lat - 4.0 * G * G) / 20.0 : 0.0;
+  if (wfit_g < wcap_scan) G = 0;  // the grid would cost waypoint capacity
+  const int wcap = static_cast<int>(wcap_scan);
   const int b0 = env < 0 ? 0 : env, b1 = env < 0 ? B : env + 1, nsel = b1 - b0;
   std::vector<int32_t> sel;
   for (int b = b0; b < b1; ++b) sel.push_back(b);
@@ -569,6 +580,10 @@ int cov_generate_maps(cov_handle* h, const cov_map_config* mc, int env, uint64_t
   m.NJ = h->lat_NJ;
   m.K = static_cast<int>(std::floor(mc->link_radius / mc->lattice_spacing)) + 1;
   m.wcap = wcap;
+  m.G = G;
+  m.gx0 = gx0;
+  m.gy0 = gy0;
+  m.gh = gh;
   m.cities = h->map_cities;
   m.mt_key = h->map_key;
   m.mt_pos = h->map_pos;

@@ -305,6 +305,8 @@ struct CovMapArgs {
   const int32_t* cell;       // (NI * NJ) the lattice point of each cell, or -1
   int NI, NJ, K;             // cell grid, cells searched either side for a link
   int wcap;                  // waypoints the LDS holds
+  int G;                     // waypoint grid (G x G cells of side gh from (gx0, gy0)) for the
+  double gx0, gy0, gh;       //   near-road test; G = 0: every lattice point scans every waypoint
   double* cities;            // (B, kMapMaxCities, 2): drawn by cov_map_cities_kernel or uploaded
   uint32_t* mt_key;          // (B, 624) each env's map stream (the reference's global np.random)
   int32_t* mt_pos;           // (B)
@@ -317,7 +319,7 @@ struct CovMapArgs {
 };
 constexpr int kMapMaxCities = 32;
 constexpr int32_t kMapNearDegenerate = 1, kMapTooMany = 2, kMapTooFew = 4, kMapOverflow = 8;
-size_t cov_map_lds_bytes(int L, int wcap);
+size_t cov_map_lds_bytes(int L, int wcap, int G);
 hipError_t launch_cov_map_cities(const CovMapArgs& a, hipStream_t s);
 hipError_t launch_cov_map(const CovMapArgs& a, hipStream_t s);
 

@@ -45,9 +45,32 @@ __device__ __forceinline__ double dist2d(double ax, double ay, double bx, double
 // Motion graph of one env (utils.py:8-24 with self_loops=True, coverage.py:572-594):
 // every ordered target pair with 0 < |p_i - p_j| <= radius, in row-major order, which
 // per sender is ascending receiver order (what np.where returns in get_action_edges).
+// The radius test of the motion graph, `0 < sqrt(dx*dx + dy*dy) <= r` exactly as dist2d
+// rounds it, from the squared distance s: sqrt is correctly rounded and monotonic, so s at
+// or below r2lo = r*r*(1 - 2^-50) always passes and s above r2hi = r*r*(1 + 2^-50) never
+// does (the margins exceed the roundings of r*r and of the square root by far); only s
+// between them takes the square root. 0 < sqrt(s) iff 0 < s; a NaN s fails both ways.
+__device__ __forceinline__ bool within_radius(double s, double r, double r2lo, double r2hi) {
+  return s > 0.0 && (s <= r2lo || (s <= r2hi && sqrt(s) <= r));
+}
+
+// Targets staged in LDS with a cell grid (GRID, when Tmax <= kGraphLdsTargets): cells of
+// side h = radius (1 + 2^-20) over the targets' bounding box, so every target within the
+// radius of a node lies in the 3 x 3 cells around it (the margin dwarfs the rounding of the
+// cell coordinates); a node's in-radius targets are kept as its 4 smallest indices, the
+// row-major scan order of the reference. Without the grid (too many cells, a non-finite
+// coordinate, or GRID off) every node scans every target.
+constexpr int kGraphLdsTargets = 4096;
+constexpr int kGraphCells = 4096;
+
+template <bool GRID>
 __global__ __launch_bounds__(kCovThreads) void cov_graph_kernel(CovArgs a, const int32_t* envs, int n_envs_sel) {
   __shared__ int scan[kCovThreads];
   __shared__ int total_s;
+  __shared__ double bb_s[kCovThreads / 64][4];
+  __shared__ int grid_s[3];  // Gx, Gy (0: scan), cell count
+  __shared__ double org_s[2];
+  extern __shared__ __attribute__((aligned(16))) double2 tgs[];  // GRID: (Tm) targets, (cells + 1) runs, (Tm) by cell
   const int e = blockIdx.x;
   if (e >= n_envs_sel) return;
   const int b = envs ? envs[e] : e;
@@ -57,15 +80,111 @@ __global__ __launch_bounds__(kCovThreads) void cov_graph_kernel(CovArgs a, const
   int32_t* nbr = a.nbr + (size_t)b * Tm * 4;
   int32_t* cnt = a.cnt + (size_t)b * Tm;
   const int tid = threadIdx.x;
+  const double r = a.motion_radius, rr = r * r;
+  const double r2lo = rr * (1.0 - 0x1p-50), r2hi = rr * (1.0 + 0x1p-50);
+  const double2* tg2 = reinterpret_cast<const double2*>(tg);
+  auto test = [&](double px, double py, double2 q) {
+    const double dx = px - q.x, dy = py - q.y;
+    return within_radius(dx * dx + dy * dy, r, r2lo, r2hi);
+  };
   // 1. neighbour lists (<= 4 per node; more is the reference's "Increase MAX_EDGES")
+  int Gx = 0, Gy = 0;
+  int* cend = reinterpret_cast<int*>(tgs + Tm);  // (cells) end of each cell's run
+  int* sidx = cend + kGraphCells;                 // (T) target indices in cell order
+  double ox = 0.0, oy = 0.0;
+  const double h = r * (1.0 + 0x1p-20);
+  if (GRID) {
+    double lo_x = __builtin_inf(), lo_y = __builtin_inf(), hi_x = -__builtin_inf(), hi_y = -__builtin_inf();
+    bool finite = true;
+    for (int j = tid; j < T; j += kCovThreads) {
+      const double2 q = tg2[j];
+      tgs[j] = q;
+      finite = finite && isfinite(q.x) && isfinite(q.y);
+      lo_x = fmin(lo_x, q.x), lo_y = fmin(lo_y, q.y), hi_x = fmax(hi_x, q.x), hi_y = fmax(hi_y, q.y);
+    }
+    if (!finite) lo_x = __builtin_nan("");  // poisons the box: scan
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const double o0 = __shfl_xor(lo_x, d, 64), o1 = __shfl_xor(lo_y, d, 64);
+      const double o2 = __shfl_xor(hi_x, d, 64), o3 = __shfl_xor(hi_y, d, 64);
+      lo_x = (isnan(o0) || isnan(lo_x)) ? __builtin_nan("") : fmin(lo_x, o0);
+      lo_y = fmin(lo_y, o1), hi_x = fmax(hi_x, o2), hi_y = fmax(hi_y, o3);
+    }
+    if ((tid & 63) == 0) {
+      bb_s[tid >> 6][0] = lo_x, bb_s[tid >> 6][1] = lo_y, bb_s[tid >> 6][2] = hi_x, bb_s[tid >> 6][3] = hi_y;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double x0 = bb_s[0][0], y0 = bb_s[0][1], x1 = bb_s[0][2], y1 = bb_s[0][3];
+      bool nan = isnan(x0);
+      for (int w = 1; w < kCovThreads / 64; ++w) {
+        nan = nan || isnan(bb_s[w][0]);
+        x0 = fmin(x0, bb_s[w][0]), y0 = fmin(y0, bb_s[w][1]), x1 = fmax(x1, bb_s[w][2]), y1 = fmax(y1, bb_s[w][3]);
+      }
+      const double fx = (x1 - x0) / h + 1.0, fy = (y1 - y0) / h + 1.0;
+      int gx = 0, gy = 0;
+      if (!nan && T > 0 && fx < (double)kGraphCells && fy < (double)kGraphCells && fx * fy < (double)kGraphCells) {
+        gx = (int)fx, gy = (int)fy;
+      }
+      grid_s[0] = gx, grid_s[1] = gy;
+      org_s[0] = x0, org_s[1] = y0;
+    }
+    __syncthreads();
+    Gx = grid_s[0], Gy = grid_s[1];
+    ox = org_s[0], oy = org_s[1];
+  }
+  // a target's cell: (x - ox) / h >= 0 for every target of the box
+  auto cellx = [&](double v) { return min((int)((v - ox) / h), Gx - 1); };
+  auto celly = [&](double v) { return min((int)((v - oy) / h), Gy - 1); };
+  if (GRID && Gx > 0) {
+    const int nc = Gx * Gy;
+    for (int c = tid; c < nc; c += kCovThreads) cend[c] = 0;
+    __syncthreads();
+    for (int j = tid; j < T; j += kCovThreads) atomicAdd(&cend[cellx(tgs[j].x) * Gy + celly(tgs[j].y)], 1);
+    __syncthreads();
+    if (tid == 0) {  // cell starts (a few thousand cells at most)
+      int run = 0;
+      for (int c = 0; c < nc; ++c) {
+        const int n = cend[c];
+        cend[c] = run;
+        run += n;
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < T; j += kCovThreads) sidx[atomicAdd(&cend[cellx(tgs[j].x) * Gy + celly(tgs[j].y)], 1)] = j;
+    __syncthreads();  // cend[c] is now the end of cell c's run (the start of c + 1)
+  }
   for (int i = tid; i < T; i += kCovThreads) {
     const double px = tg[2 * i], py = tg[2 * i + 1];
     int c = 0;
-    for (int j = 0; j < T; ++j) {
-      const double d = dist2d(px, py, tg[2 * j], tg[2 * j + 1]);
-      if (d > 0.0 && d <= a.motion_radius) {
-        if (c < 4) nbr[4 * i + c] = j;
-        ++c;
+    if (GRID && Gx > 0) {
+      // the in-radius targets of the 3 x 3 cells, the 4 smallest indices kept in order
+      int n0 = INT_MAX, n1 = INT_MAX, n2 = INT_MAX, n3 = INT_MAX;
+      const int ci = cellx(px), cj = celly(py);
+      for (int gi = max(ci - 1, 0); gi <= min(ci + 1, Gx - 1); ++gi)
+        for (int gj = max(cj - 1, 0); gj <= min(cj + 1, Gy - 1); ++gj) {
+          const int cc = gi * Gy + gj, k1 = cend[cc];
+          for (int k = cc > 0 ? cend[cc - 1] : 0; k < k1; ++k) {
+            const int j = sidx[k];
+            if (!test(px, py, tgs[j])) continue;
+            ++c;
+            int x = j, t;
+            t = min(n0, x), x = max(n0, x), n0 = t;
+            t = min(n1, x), x = max(n1, x), n1 = t;
+            t = min(n2, x), x = max(n2, x), n2 = t;
+            n3 = min(n3, x);
+          }
+        }
+      nbr[4 * i] = n0;
+      nbr[4 * i + 1] = n1;
+      nbr[4 * i + 2] = n2;
+      nbr[4 * i + 3] = n3;
+    } else {
+      for (int j = 0; j < T; ++j) {
+        if (test(px, py, GRID ? tgs[j] : tg2[j])) {
+          if (c < 4) nbr[4 * i + c] = j;
+          ++c;
+        }
       }
     }
     if (c > 4) atomicOr(a.err, 1);
@@ -869,7 +988,15 @@ size_t cov_step_lds_bytes(int R, int M) {
 }
 
 hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStream_t s) {
-  hipLaunchKernelGGL(cov_graph_kernel, dim3(n), dim3(kCovThreads), 0, s, a, envs, n);
+  if (a.Tmax <= kGraphLdsTargets) {
+    const size_t lds = (size_t)a.Tmax * 16 + (size_t)kGraphCells * 4 + (size_t)a.Tmax * 4;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cov_graph_kernel<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cov_graph_kernel<true>, dim3(n), dim3(kCovThreads), lds, s, a, envs, n);
+  } else {
+    hipLaunchKernelGGL(cov_graph_kernel<false>, dim3(n), dim3(kCovThreads), 0, s, a, envs, n);
+  }
   return hipGetLastError();
 }
 

@@ -149,6 +149,8 @@ __global__ __launch_bounds__(kMapThreads) void cov_map_kernel(CovMapArgs a) {
   int32_t* parent = reinterpret_cast<int32_t*>(wp + a.wcap);  // (L) union-find forest
   int32_t* cnt = parent + L;                           // (L) component sizes by root
   int32_t* cidx = cnt + L;                             // (L) lattice point -> target node or -1
+  int32_t* cend = cidx + L;                            // (G * G) waypoint grid: end of each cell's run
+  int32_t* widx = cend + a.G * a.G;                    // (wcap) waypoints in cell order
   // 1. cities, no edges yet
   if (tid < NC) {
     const double* c = a.cities + ((size_t)b * kMapMaxCities + tid) * 2;
@@ -250,16 +252,59 @@ __global__ __launch_bounds__(kMapThreads) void cov_map_kernel(CovMapArgs a) {
     }
   }
   __syncthreads();
-  // 4. lattice points near a road (waypoints are LDS broadcasts)
-  for (int l = tid; l < L; l += kMapThreads) {
-    const double2 p = a.lat[l];
-    double m = __builtin_inf();
-    for (int w = 0; w < W; ++w) {
-      const double2 q = wp[w];
-      const double dx = p.x - q.x, dy = p.y - q.y;
-      m = fmin(m, dx * dx + dy * dy);
+  // 4. lattice points near a road: sqrt(min_w |p - w|^2) <= near_radius, i.e. (sqrt and
+  // its rounding being monotone) some waypoint w with sqrt(|p - w|^2) <= near_radius
+  const double nr = a.near_radius, n2lo = nr * nr * (1.0 - 0x1p-50), n2hi = nr * nr * (1.0 + 0x1p-50);
+  auto near = [&](double2 p, double2 q) {  // the squared distance decides unless at the edge
+    const double dx = p.x - q.x, dy = p.y - q.y, s = dx * dx + dy * dy;
+    return s <= n2lo || (s <= n2hi && sqrt(s) <= nr);
+  };
+  if (a.G > 0) {
+    // waypoints counting-sorted into cells of side gh > near_radius, so every waypoint
+    // near p lies in the 3 x 3 cells around p's cell (the margin, gh - near_radius =
+    // near_radius * 2^-20, dwarfs the rounding of the cell coordinates)
+    const int G = a.G;
+    auto gcell = [&](double v, double o) {
+      const double f = (v - o) / a.gh;
+      return f >= 0.0 ? (f < (double)G ? (int)f : G - 1) : 0;  // NaN: 0 (never near anything)
+    };
+    for (int c = tid; c < G * G; c += kMapThreads) cend[c] = 0;
+    __syncthreads();
+    for (int w = tid; w < W; w += kMapThreads) atomicAdd(&cend[gcell(wp[w].x, a.gx0) * G + gcell(wp[w].y, a.gy0)], 1);
+    __syncthreads();
+    const int per = (G * G + kMapThreads - 1) / kMapThreads;
+    const int c0 = min(G * G, tid * per), c1 = min(G * G, c0 + per);
+    int run = 0;
+    for (int c = c0; c < c1; ++c) run += cend[c];
+    int wtot;
+    run = block_exscan(run, wsum, &wtot);
+    for (int c = c0; c < c1; ++c) {  // each cell's start; the scatter below leaves its end
+      const int n = cend[c];
+      cend[c] = run;
+      run += n;
     }
-    cidx[l] = sqrt(m) <= a.near_radius ? 1 : 0;
+    __syncthreads();
+    for (int w = tid; w < W; w += kMapThreads)
+      widx[atomicAdd(&cend[gcell(wp[w].x, a.gx0) * G + gcell(wp[w].y, a.gy0)], 1)] = w;
+    __syncthreads();
+    for (int l = tid; l < L; l += kMapThreads) {
+      const double2 p = a.lat[l];
+      const int ci = gcell(p.x, a.gx0), cj = gcell(p.y, a.gy0);
+      bool found = false;
+      for (int i = max(ci - 1, 0); i <= min(ci + 1, G - 1) && !found; ++i)
+        for (int j = max(cj - 1, 0); j <= min(cj + 1, G - 1) && !found; ++j) {
+          const int c = i * G + j, k1 = cend[c];
+          for (int k = c > 0 ? cend[c - 1] : 0; k < k1 && !found; ++k) found = near(p, wp[widx[k]]);
+        }
+      cidx[l] = found ? 1 : 0;
+    }
+  } else {
+    for (int l = tid; l < L; l += kMapThreads) {  // every waypoint (LDS broadcasts)
+      const double2 p = a.lat[l];
+      bool found = false;
+      for (int w = 0; w < W && !found; ++w) found = near(p, wp[w]);
+      cidx[l] = found ? 1 : 0;
+    }
   }
   __syncthreads();
   // 5a. number the near points in lattice order (contiguous chunks per thread)
@@ -356,7 +401,9 @@ __global__ __launch_bounds__(kMapThreads) void cov_map_kernel(CovMapArgs a) {
 
 }  // namespace
 
-size_t cov_map_lds_bytes(int L, int wcap) { return (size_t)wcap * 16 + (size_t)L * 12; }
+size_t cov_map_lds_bytes(int L, int wcap, int G) {
+  return (size_t)wcap * 16 + (size_t)L * 12 + (G > 0 ? (size_t)G * G * 4 + (size_t)wcap * 4 : 0);
+}
 
 hipError_t launch_cov_map_cities(const CovMapArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(cov_map_cities_kernel, dim3(a.n_sel), dim3(64), 0, s, a);
@@ -364,7 +411,11 @@ hipError_t launch_cov_map_cities(const CovMapArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_cov_map(const CovMapArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(cov_map_kernel, dim3(a.n_sel), dim3(kMapThreads), cov_map_lds_bytes(a.L, a.wcap), s, a);
+  const size_t lds = cov_map_lds_bytes(a.L, a.wcap, a.G);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cov_map_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cov_map_kernel, dim3(a.n_sel), dim3(kMapThreads), lds, s, a);
   return hipGetLastError();
 }
 

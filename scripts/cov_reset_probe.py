@@ -1,0 +1,55 @@
+"""Drop-in CoverageEnv.reset() cost (run on the GPU box, optionally under rocprofv3
+--kernel-trace --stats): R robots, max_nodes 1000, np.random.seed(8), one warm-up reset,
+then RESETS timed resets, each followed by one random step (as an episode would). Prints
+the median / min host ms per reset, and the same split into its parts: the map
+(_generate_targets: the cities from np.random, cov_generate_maps, the targets read back),
+the graph bookkeeping (_initialize_graph) and the rest (start draws, cov_reset)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-flock_amd")]
+from gym_flock.envs.spatial import CoverageEnv  # noqa: E402
+
+R = int(os.environ.get("R", "6"))
+n = int(os.environ.get("RESETS", "30"))
+np.random.seed(8)
+env = CoverageEnv(n_robots=R, nearby_starts=False, max_nodes=1000)
+env.seed(9)
+parts = {"map": [], "graph": [], "total": []}
+gen, init = env._generate_targets, env._initialize_graph
+
+
+def timed_gen():
+    t0 = time.perf_counter()
+    out = gen()
+    parts["map"].append(1e3 * (time.perf_counter() - t0))
+    return out
+
+
+def timed_init(*a, **k):
+    t0 = time.perf_counter()
+    out = init(*a, **k)
+    parts["graph"].append(1e3 * (time.perf_counter() - t0))
+    return out
+
+
+env._generate_targets, env._initialize_graph = timed_gen, timed_init
+env.reset()
+env.step(env.controller(random=True))
+for k in parts:
+    parts[k].clear()
+for _ in range(n):
+    t0 = time.perf_counter()
+    env.reset()
+    parts["total"].append(1e3 * (time.perf_counter() - t0))
+    env.step(env.controller(random=True))
+tot = np.array(parts["total"])
+rest = tot - np.array(parts["map"]) - np.array(parts["graph"])
+print("R=%d resets=%d  total median %.3f ms (min %.3f)  map %.3f  graph %.3f  rest %.3f  n_targets %d" %
+      (R, n, np.median(tot), tot.min(), np.median(parts["map"]), np.median(parts["graph"]), np.median(rest),
+       env.n_targets))
+env.close()

@@ -358,3 +358,47 @@ def test_default_env_nearby_starts():
         np.testing.assert_array_equal(obs[k].reshape(ref[k].shape), ref[k], err_msg=k)
     assert r == rr and d == dd
     env.close()
+
+
+def _jittered_grid(nx, ny, seed, spacing=5.5, jitter=0.3):
+    rs = np.random.RandomState(seed)
+    xs, ys = np.meshgrid(np.arange(nx) * spacing, np.arange(ny) * spacing)
+    p = np.stack([xs.ravel(), ys.ravel()], axis=1)
+    return p + rs.uniform(-jitter, jitter, size=p.shape)
+
+
+def test_motion_graph_edge_cases_vs_oracle():
+    """The motion-graph kernel (cell grid over the targets' box, the radius test from
+    squared distances except at the edge) against the oracle's radius graph: a jittered
+    grid with pairs at exactly the radius and one ulp either side, coincident targets
+    (distance 0: no edge), and a map spread so wide that the grid gives way to the scan
+    of every target; a target with more than 4 neighbours is refused."""
+    r = 5.5 * 1.2
+    g = _jittered_grid(8, 7, 1)
+    edge = np.array([[200.0, 0.0], [200.0 + r, 0.0], [300.0, 0.0], [np.nextafter(300.0 + r, np.inf), 0.0],
+                     [400.0, 0.0], [np.nextafter(400.0 + r, 0.0), 0.0], [500.0, 500.0], [500.0, 500.0],
+                     [500.0, 500.0 + r]])
+    wide = np.concatenate([_jittered_grid(6, 1, 2), [[1.0e5, 3.0], [1.0e5 + r, 3.0], [-2.0e5, -7.0]]])
+    maps = [np.concatenate([g, edge]), wide, g[::-1].copy()]
+    B, R, M = len(maps), 3, 200
+    v = VecCoverage(B, R, max_nodes=M)
+    for b in range(B):
+        v.set_targets(maps[b], env=b)
+    start, visited = v.reset(seed=5)
+    for b in range(B):
+        o = oc.CoverageOracle(maps[b], R, M)
+        T = len(maps[b])
+        assert v.h.n_motion()[b] == o.n_motion
+        obs0 = o.reset(start[b], np.nonzero(visited[b, :T] == 0)[0] + R)
+        assert_obs(v.obs(b), {k + "0": val for k, val in obs0.items()})
+    s, q, _ = oc.radius_graph(maps[0], r)
+    pairs = set(zip(s.tolist(), q.tolist()))
+    T0 = len(g)
+    assert (T0, T0 + 1) in pairs and (T0 + 2, T0 + 3) not in pairs and (T0 + 4, T0 + 5) in pairs
+    assert (T0 + 6, T0 + 7) not in pairs  # coincident
+    v.close()
+    crowded = np.array([[0.0, 0.0], [1.0, 0.0], [0.0, 1.0], [-1.0, 0.0], [0.0, -1.0], [1.0, 1.0]])
+    h = nat.CoverageHandle(2, 1, 50)
+    with pytest.raises(nat.GymFlockError):
+        h.set_targets(crowded, env=0)
+    h.close()
