@@ -199,3 +199,22 @@ def test_dropin_reset_draws_reference_maps():
         rs.random_sample(24)
         assert after == rs.random_sample()
     env.close()
+
+
+@pytest.mark.parametrize("world_radius", [260.0, 3000.0], ids=["grid", "scan"])
+def test_device_map_far_cities_grid_and_scan(world_radius):
+    """A small arena (30 x 30 half-widths) with 4 of the 12 given cities ~250 away: the
+    near-road test through the waypoint grid (world_radius 260: a 113-cell grid, most of
+    it far from the arena) and through the scan of every waypoint (world_radius 3000: the
+    grid would need more than 256 cells a side) give the restated algorithm's map."""
+    rs = np.random.RandomState(3)
+    c = np.concatenate([rs.uniform(-28, 28, size=(8, 2)), [[-250, -240], [255, -235], [-245, 258], [252, 248]]])
+    mc = nat.map_config_default(xmax=30, ymax=30)
+    mc.world_radius = world_radius
+    ref, amb = cmo.generate_targets(c, 30, 30)
+    assert 2 <= len(ref) < 500 and not amb
+    h = nat.CoverageHandle(2, 1, 500)
+    n, st, _ = h.generate_maps(cities=c[None], env=0, map_config=mc)
+    assert n[0] == len(ref) and st[0] == 0
+    np.testing.assert_array_equal(h.targets(0, n[0]), ref)
+    h.close()
