@@ -275,7 +275,10 @@ __global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, 
 // the workgroup. The predecessors are kept in LDS too (the waves' global stores to one
 // entry would not be ordered by the barriers) and written out at the end. Same results
 // as cov_time_matrix_kernel.
-constexpr int kTmWaves = 4;
+#ifndef GF_TM_WAVES
+#define GF_TM_WAVES 8  // 8 per chunk: the drop-in first step 5-7 % below 4 waves (profiles/r06/ab_tm_waves_per_chunk.txt)
+#endif
+constexpr int kTmWaves = GF_TM_WAVES;
 constexpr size_t kTmFewChunks = 256;  // launches of at most this many chunks (one per CU) take it
 
 template <typename V, bool PASS_B>

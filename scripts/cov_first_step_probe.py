@@ -15,7 +15,7 @@ R = int(os.environ.get("R", 6))
 np.random.seed(8)
 env = CoverageEnv(n_robots=R, nearby_starts=R <= 6, max_nodes=1000)
 env.seed(3)
-for ep in range(4):
+for ep in range(int(os.environ.get("EPISODES", 4))):
     env.reset()
     done, k = False, 0
     while not done:
