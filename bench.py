@@ -1104,10 +1104,18 @@ def main():
         env.reset(x=x_init)
         for _ in range(max(1, min(W, 5))):  # untimed, as the other lines' warmup steps
             env.step(u)
-        eh, _ = timed(env, ranks, K, lambda s: env.step(u))
+        calls = []
+
+        def host_step(s):
+            c0 = time.perf_counter()
+            env.step(u)
+            calls.append(1e6 * (time.perf_counter() - c0))
+
+        eh, _ = timed(env, ranks, K, host_step)
         extra["host_actions"] = {
             "value": world * B * N * K / eh, "unit": "agent-steps/s", "ms_per_step": 1e3 * eh / K,
             "ratio_to_plain_step": eh / elapsed, "action_bytes_per_step": int(u.nbytes),
+            "call_us_first": [round(c, 1) for c in calls[:6]], "call_us_median": float(np.median(calls)),
             "note": "PCIe-inclusive: env.step(u) with a host (B,N,2) float32 action array each step, uploaded "
                     "on the handle's action stream into one of two device buffers while the previous step "
                     "runs (fe_step returns once its copy is done, not its step); outputs stay in HBM"}

@@ -47,4 +47,19 @@ for warm in (1, 5, 50):
         ms, calls = window(k, lambda: env.step(u))
         print("host u    warm %2d  K=%3d  %.4f ms/step  ratio %.3f  first calls (us) %s  median call %.1f us" %
               (warm, k, ms, ms / res[k], " ".join("%.0f" % c for c in calls[:6]), float(np.median(calls))))
+# the bench's sequence: packed-output steps, a reset, 5 host-action warm-up steps, then
+# the window with and without the HIP-event timing window bench.py's timed() opens
+for timing in (False, True, False, True):
+    for _ in range(50):
+        env.step(resident=True, network="packed")
+    env.reset(x=x0)
+    for _ in range(5):
+        env.step(u)
+    if timing:
+        env.h.timing_start(every=8)
+    ms, calls = window(20, lambda: env.step(u))
+    if timing:
+        env.h.timing_stop()
+    print("bench seq timing %d  K= 20  %.4f ms/step  ratio %.3f  first calls (us) %s  median call %.1f us" %
+          (timing, ms, ms / res[20], " ".join("%.0f" % c for c in calls[:6]), float(np.median(calls))))
 env.close()
