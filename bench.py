@@ -1101,6 +1101,7 @@ def main():
     # memory every step (the PCIe-inclusive rate of a trainer that hands actions over per
     # step; the headline keeps them resident in HBM)
     if not args.no_host_actions_line:
+        clock_warmup(lambda: env.step(u), env.sync, 50.0)  # as the other lines
         env.reset(x=x_init)
         for _ in range(max(1, min(W, 5))):  # untimed, as the other lines' warmup steps
             env.step(u)

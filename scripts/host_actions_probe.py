@@ -62,4 +62,16 @@ for timing in (False, True, False, True):
         env.h.timing_stop()
     print("bench seq timing %d  K= 20  %.4f ms/step  ratio %.3f  first calls (us) %s  median call %.1f us" %
           (timing, ms, ms / res[20], " ".join("%.0f" % c for c in calls[:6]), float(np.median(calls))))
+# after closed-loop controller steps (the bench's controller line runs before the host line)
+for rep in range(2):
+    env.reset(x=x0)
+    env.controller()
+    for _ in range(300):
+        env.step(expert=True, controller=True)
+    env.reset(x=x0)
+    for _ in range(5):
+        env.step(u)
+    ms, calls = window(20, lambda: env.step(u))
+    print("after ctrl       K= 20  %.4f ms/step  ratio %.3f  first calls (us) %s  median call %.1f us" %
+          (ms, ms / res[20], " ".join("%.0f" % c for c in calls[:6]), float(np.median(calls))))
 env.close()
