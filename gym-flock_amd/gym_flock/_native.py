@@ -905,6 +905,16 @@ class CoverageHandle:
         check(self.lib.cov_get_obs(self.h, int(env), ptr(nodes), ptr(edges), ptr(snd), ptr(rcv), ptr(step)))
         return {"nodes": nodes, "edges": edges, "senders": snd, "receivers": rcv, "step": step}
 
+    def motion_edges(self, env=0, n=None):
+        """The first n (default: the env's motion-edge count) senders and receivers of env's
+        observation, i.e. its motion graph (global node indices), without the rest."""
+        m = self.max_nodes
+        snd = np.empty(4 * m, np.int32)
+        rcv = np.empty(4 * m, np.int32)
+        check(self.lib.cov_get_obs(self.h, int(env), None, None, ptr(snd), ptr(rcv), None))
+        n = int(self.n_motion()[env]) if n is None else int(n)
+        return snd[:n], rcv[:n]
+
     def rewards(self):
         r = np.empty(self.n_envs)
         d = np.empty(self.n_envs, np.uint8)

@@ -100,6 +100,7 @@ class CoverageEnv(Env):
         self._closest = None       # robots' nodes after the last step (the next last_loc)
         self._want_greedy = False  # controller(greedy=True) in use: steps fuse the next one
         self._greedy_cache = None  # (actions, needs_random) of the current state, device-made
+        self._motion_cache = None  # the motion graph's (senders, receivers), per graph
         self._abuf = None
         self._layout = None
 
@@ -139,11 +140,13 @@ class CoverageEnv(Env):
         self.max_edges = self.max_nodes * MAX_EDGES
         if not on_device:
             self._h.set_targets(self.targets, env=0)
-        self._closest = self._greedy_cache = None
+        self._closest = self._greedy_cache = self._motion_cache = None
         self.n_motion_edges = int(self._h.n_motion()[0])
         if self.nearby_starts:
             n_nearest = self.get_n_nearest(self.np_random.choice(self.n_targets), self.n_robots * NEARBY_DENSITY)
-            self.start_region = [i in n_nearest for i in range(self.n_targets)]
+            region = np.zeros(self.n_targets, bool)
+            region[list(n_nearest)] = True
+            self.start_region = region.tolist()  # [i in n_nearest for i in range(n_targets)]
         else:
             self.start_region = [True] * self.n_targets
         self.unvisited_region = [True] * self.n_targets
@@ -158,9 +161,13 @@ class CoverageEnv(Env):
 
     @property
     def motion_edges(self):
-        o = self._h.obs(0)
-        n = self.n_motion_edges
-        return o["senders"][:n].astype(np.int64), o["receivers"][:n].astype(np.int64)
+        """(senders, receivers) of the motion graph, global node indices (:572-594): read
+        from the device once per graph (it only changes with the map), then the same arrays,
+        as the reference's attribute."""
+        if self._motion_cache is None:
+            s, q = self._h.motion_edges(0, self.n_motion_edges)
+            self._motion_cache = (s.astype(np.int64), q.astype(np.int64))
+        return self._motion_cache
 
     def get_n_nearest(self, i, n):
         """coverage.py:655-673: grow a node set through the motion graph until it holds n."""

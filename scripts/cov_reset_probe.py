@@ -1,5 +1,5 @@
 """Drop-in CoverageEnv.reset() cost (run on the GPU box, optionally under rocprofv3
---kernel-trace --stats): R robots, max_nodes 1000, np.random.seed(8), one warm-up reset,
+--kernel-trace --stats): R robots, max_nodes 1000 (NEARBY=1: nearby_starts), np.random.seed(8), one warm-up reset,
 then RESETS timed resets, each followed by one random step (as an episode would). Prints
 the median / min host ms per reset, and the same split into its parts: the map
 (_generate_targets: the cities from np.random, cov_generate_maps, the targets read back),
@@ -17,7 +17,7 @@ from gym_flock.envs.spatial import CoverageEnv  # noqa: E402
 R = int(os.environ.get("R", "6"))
 n = int(os.environ.get("RESETS", "30"))
 np.random.seed(8)
-env = CoverageEnv(n_robots=R, nearby_starts=False, max_nodes=1000)
+env = CoverageEnv(n_robots=R, nearby_starts=os.environ.get("NEARBY") == "1", max_nodes=1000)
 env.seed(9)
 parts = {"map": [], "graph": [], "total": []}
 gen, init = env._generate_targets, env._initialize_graph
