@@ -20,6 +20,8 @@ R, B, M = 200, 512, 1000
 np.random.seed(8)
 v = VecCoverage(B, R, max_nodes=M, episode_length=75)
 v.set_targets(generate_targets())
+if os.environ.get("STREAMS"):  # launches per step (cov_set_streams: 1 or 2; default: 2 for greedy steps)
+    v.h.set_streams(int(os.environ["STREAMS"]))
 v.reset(seed=0)
 v.step(greedy=True)  # builds the time matrices and greedy lists
 v.sync()
