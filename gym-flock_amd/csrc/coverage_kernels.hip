@@ -387,6 +387,19 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
       if (tid + j * NT < R) ld[j] = load(tid + j * NT);
   }
   // the env's words, loaded up front so none of them costs a round trip of its own
+  // COV_GREEDY_RNG: the env's MT19937 key, loaded now with the robots' loads (its words
+  // are only written by this workgroup, below) so the fallback draws after the picks do
+  // not wait for a global round trip of their own
+  constexpr int kKeyPer = (kMtN + NT - 1) / NT;
+  uint32_t kpre[kKeyPer];
+  const bool rng_pre = a.glist != nullptr && !a.next_greedy && a.mt_key != nullptr;
+  if (rng_pre) {
+#pragma unroll
+    for (int j = 0; j < kKeyPer; ++j) {
+      const int k = tid + j * NT;
+      kpre[j] = k < kMtN ? a.mt_key[(size_t)b * kMtN + k] : 0u;
+    }
+  }
   const bool dirty = a.dirty[b] != 0;
   const int nv0 = a.nvisited[b], sc0 = a.step_counter[b];
   const bool full = dirty || !has_act;  // recompute every robot's action edges
@@ -402,6 +415,12 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
         gvis[t0 >> 5] = static_cast<uint32_t>(m);
         gvis[(t0 >> 5) + 1] = static_cast<uint32_t>(m >> 32);
       }
+    }
+    if (rng_pre) {  // the prefetched key into its LDS words (read by the draws below)
+      uint32_t* kb = reinterpret_cast<uint32_t*>(ulist + kGreedyDirectMax + 1);
+#pragma unroll
+      for (int j = 0; j < kKeyPer; ++j)
+        if (tid + j * NT < kMtN) kb[tid + j * NT] = kpre[j];
     }
     __syncthreads();
   }
@@ -509,7 +528,6 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     uint32_t* key = a.mt_key + (size_t)b * kMtN;
     const int nfall = counter[1];
     const int pos = a.mt_pos[b];
-    for (int k = tid; k < kMtN; k += NT) kb[k] = key[k];
     {
       const int lane = tid & 63, wv = tid >> 6;
       for (int k0 = wv * 64; k0 < R; k0 += NT) {
