@@ -674,6 +674,15 @@ def bench_greedy(v, targets, R, M, B, K, args):
             v.step(greedy=True)
     v.sync()
     episode = (time.perf_counter() - t0) / 4
+    # the same episodes with their 75 expert steps in one launch (cov_step_expert: each env's
+    # workgroup steps its env 75 times; bit-exact with the launch per step, GPU tests)
+    v.sync()
+    t0 = time.perf_counter()
+    for e in range(4):
+        v.reset(seed=600 + e)
+        v.expert_steps(75, fetch=False)
+    v.sync()
+    episode_one = (time.perf_counter() - t0) / 4
     t0 = time.perf_counter()
     v.reset(seed=500, draws="host")
     reset_host = time.perf_counter() - t0
@@ -700,6 +709,7 @@ def bench_greedy(v, targets, R, M, B, K, args):
     out = {"time_matrix_ms_all_envs": 1e3 * build, "envs": B, "n_targets": len(targets),
            "reset_ms_all_envs": 1e3 * reset_dev, "reset_ms_all_envs_host_draws": 1e3 * reset_host,
            "expert_episode_ms_all_envs": 1e3 * episode, "expert_env_episodes_per_s": B / episode,
+           "expert_episode_ms_all_envs_one_launch": 1e3 * episode_one,
            "expert_episode_ms_all_envs_new_maps": 1e3 * episode_new,
            "expert_env_episodes_per_s_new_maps": B / episode_new,
            "new_maps_reset_and_time_matrices_ms_all_envs": 1e3 * reset_tm_new,

@@ -739,6 +739,50 @@ int cov_get_rng(cov_handle* h, uint32_t* keys, int32_t* pos) {
   return GF_OK;
 }
 
+// n_steps fused greedy expert steps with the device fallback draws in one launch; equal to
+// n_steps calls of cov_step(h, NULL, COV_ACTIONS_GREEDY | COV_GREEDY_RNG).
+int cov_step_expert(cov_handle* h, int n_steps, double* rewards, uint8_t* done) {
+  if (!h) return cfail(GF_EINVAL, "null handle");
+  if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");
+  if (n_steps < 1) return cfail(GF_EINVAL, "n_steps must be at least 1");
+  if (!h->mt_key) return cfail(GF_ESTATE, "set the envs' np_random streams first (cov_set_rng or cov_reset_seeded)");
+  if (h->cfg.n_robots > gf::kMtN) return cfail(GF_EINVAL, "n_robots <= 624 (one key regeneration per step)");
+  if (int rc = use(h)) return rc;
+  if (!h->tm_ready || !h->tm_glist)
+    if (int rc = ensure_time_matrix(h)) return rc;
+  if (!h->tm_glist) return cfail(GF_EINVAL, "the fused expert needs max_nodes - n_robots <= 1024 (the greedy lists)");
+  if (int rc = join_s2(h)) return rc;
+  gf::CovArgsM m{};
+  m.a = h->a;
+  m.a.actions = nullptr;
+  m.a.glist = h->tm_glist;
+  m.a.glen = h->tm_glen;
+  m.a.gstride = h->gstride;
+  m.a.gcost = h->tm_cost;
+  m.a.gprev = h->tm_prevT;
+  m.a.gactions = h->actions;
+  m.a.needs_random = h->needs_random;
+  m.a.mt_key = h->mt_key;
+  m.a.mt_pos = h->mt_pos;
+  m.k_steps = n_steps;
+  const size_t B = h->cfg.n_envs, n = (size_t)n_steps * B;
+  unsigned char* buf = nullptr;
+  if (rewards || done) {
+    if (int rc = scratch(h, n * 9, &buf)) return rc;
+    m.reward_k = reinterpret_cast<double*>(buf);
+    m.done_k = buf + n * 8;
+  }
+  hipError_t e = gf::launch_cov_step_multi(m, h->stream);
+  if (e != hipSuccess) return cfail(GF_EHIP, std::string("cov_step_multi_kernel: ") + hipGetErrorString(e));
+  h->main_dirty = true;
+  h->other_work = true;
+  if (!buf) return GF_OK;
+  if (int rc = copy_out(h, rewards, m.reward_k, n * 8)) return rc;
+  if (int rc = copy_out(h, done, m.done_k, n)) return rc;
+  CV_HIP(hipStreamSynchronize(h->stream));
+  return check_err(h);
+}
+
 int cov_step(cov_handle* h, const int32_t* actions, int flags) {
   if (!h) return cfail(GF_EINVAL, "null handle");
   if (!h->has_state) return cfail(GF_ESTATE, "reset first (cov_reset)");

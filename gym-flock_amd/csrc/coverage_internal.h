@@ -71,6 +71,16 @@ struct CovArgs {
   DoneFlag fin;           // cov_step_host: the grid's completion flag (done_flag.h)
 };
 
+// cov_step_expert: k_steps fused greedy expert steps in one launch, each env's workgroup
+// stepping its env k_steps times; step s's rewards and done flags at [s][b] (a separate
+// argument block, so the one-step kernel's arguments stay as they are)
+struct CovArgsM {
+  CovArgs a;
+  int k_steps;
+  double* reward_k;       // (k_steps,B) or nullptr
+  uint8_t* done_k;        // (k_steps,B) or nullptr
+};
+
 // cov_step_host: one env's actions travel in the kernel arguments up to this many bytes
 constexpr int kCovUInlineBytes = 2048;
 struct CovArgsU {
@@ -336,6 +346,7 @@ hipError_t launch_cov_reset(const CovArgs& a, const int32_t* start, const uint8_
 hipError_t launch_cov_seed_reset(const CovArgs& a, uint32_t seed0, double frac, int32_t* start, uint8_t* visited0,
                                  hipStream_t s);
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s);
+hipError_t launch_cov_step_multi(const CovArgsM& m, hipStream_t s);  // m.k_steps steps, one launch
 // the step with a.actions read from `u` (host memory, copied into the kernel arguments;
 // B * R * 4 <= kCovUInlineBytes)
 hipError_t launch_cov_step_uin(const CovArgs& a, const int32_t* u, hipStream_t s);

@@ -287,17 +287,11 @@ __device__ __forceinline__ int action_node(const int32_t* nbr, const int32_t* cn
 // After an external placement, a new graph or a reset, everything is recomputed.
 // UIN (cov_step_host): the env batch's actions arrive in the kernel arguments (CovArgsU)
 // instead of being read from memory, one dependent round trip fewer.
-template <int NT, bool UIN = false>
-__global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<UIN, CovArgsU, CovArgs>::type p) {
-  [[maybe_unused]] CovArgs uargs;
-  if constexpr (UIN) {
-    uargs = p.a;
-    uargs.actions = p.u;
-  }
-  const CovArgs& a = *[&]() -> const CovArgs* {
-    if constexpr (UIN) return &uargs;
-    else return &p;
-  }();
+// One step of env a.env0 + blockIdx.x (the kernels below): MULTI also records the step's
+// reward and done flag at [it][b] of reward_k / done_k.
+template <int NT, bool MULTI>
+__device__ __forceinline__ void cov_step_body(const CovArgs& a, [[maybe_unused]] int it,
+                                              [[maybe_unused]] double* reward_k, [[maybe_unused]] uint8_t* done_k) {
   constexpr int RPT = kCovThreads / NT;  // robots per thread when R <= kCovThreads
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = a.env0 + blockIdx.x;
@@ -749,6 +743,8 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
     a.reward[b] = static_cast<double>(newly);
     a.done[b] = (sc0 + 1 == a.episode_length || nv == T) ? 1 : 0;
     a.dirty[b] = 0;
+    if (MULTI && reward_k) reward_k[(size_t)it * a.B + b] = static_cast<double>(newly);
+    if (MULTI && done_k) done_k[(size_t)it * a.B + b] = (sc0 + 1 == a.episode_length || nv == T) ? 1 : 0;
   }
   if (a.next_greedy) {
     // controller(greedy=True) (:800-872) on the resulting state, for the next step of an
@@ -810,11 +806,40 @@ __global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<
       if (a.h_err) a.h_err[b] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+template <int NT, bool UIN = false>
+__global__ __launch_bounds__(NT) void cov_step_kernel(typename std::conditional<UIN, CovArgsU, CovArgs>::type p) {
+  [[maybe_unused]] CovArgs uargs;
+  if constexpr (UIN) {
+    uargs = p.a;
+    uargs.actions = p.u;
+  }
+  const CovArgs& a = *[&]() -> const CovArgs* {
+    if constexpr (UIN) return &uargs;
+    else return &p;
+  }();
+  cov_step_body<NT, false>(a, 0, nullptr, nullptr);
 #ifdef GF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   GF_COV_STAMP(4);
 #endif
   signal_done(a.fin);  // cov_step_host: the host waits for this, not the stream
+}
+
+// cov_step_expert: k_steps steps of every env in one launch, each env's workgroup stepping
+// its env k_steps times (the actions come from the device: the greedy lists and the env's
+// MT19937 stream), each iteration exactly one cov_step. What an iteration reads of the
+// previous one's global writes (robots' nodes, the tail's offers, visited flags, the env's
+// words, the key) was written by this workgroup, and the barrier between iterations orders
+// it. A kernel of its own: the loop would cost the one-step kernel registers.
+template <int NT>
+__global__ __launch_bounds__(NT) void cov_step_multi_kernel(CovArgsM p) {
+  const int n = p.k_steps > 1 ? p.k_steps : 1;
+  for (int it = 0; it < n; ++it) {
+    cov_step_body<NT, true>(p.a, it, p.reward_k, p.done_k);
+    __syncthreads();
+  }
 }
 
 // reset (:405-424 after the random draws): robots onto their start targets, the
@@ -1040,6 +1065,12 @@ hipError_t launch_cov_step_uin(const CovArgs& a, const int32_t* u, hipStream_t s
   void* args[] = {&p};
   return hipLaunchKernel(reinterpret_cast<const void*>(&cov_step_kernel<kCovThreads, true>), dim3(a.B),
                          dim3(kCovThreads), args, cov_step_lds_bytes(a.R, a.M), s);
+}
+
+hipError_t launch_cov_step_multi(const CovArgsM& m, hipStream_t s) {
+  void* args[] = {const_cast<CovArgsM*>(&m)};
+  return hipLaunchKernel(reinterpret_cast<const void*>(&cov_step_multi_kernel<kCovThreads>), dim3(m.a.B),
+                         dim3(kCovThreads), args, cov_step_lds_bytes(m.a.R, m.a.M), s);
 }
 
 hipError_t launch_cov_step(const CovArgs& a, hipStream_t s) {

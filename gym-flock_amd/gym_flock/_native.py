@@ -174,6 +174,7 @@ SIGNATURES = {
     "cov_reset": [_P, _P, _P],
     "cov_reset_seeded": [_P, ctypes.c_uint64, ctypes.c_double, _P, _P],
     "cov_step": [_P, _P, _I],
+    "cov_step_expert": [_P, _I, _P, _P],
     "cov_set_actions": [_P, _P],
     "cov_set_rng": [_P, _P, _P],
     "cov_get_rng": [_P, _P, _P],
@@ -845,6 +846,16 @@ class CoverageHandle:
             return
         a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)
         check(self.lib.cov_step(self.h, ptr(a), 0))
+
+    def step_expert(self, n_steps, fetch=True):
+        """n_steps fused greedy expert steps with the device fallback draws in one launch
+        (cov_step_expert): the same as n_steps step(greedy=True, rng=True) calls. Returns
+        every step's (rewards (n_steps,B), done (n_steps,B) bool), or None with fetch=False
+        (asynchronous)."""
+        r = np.empty((int(n_steps), self.n_envs)) if fetch else None
+        d = np.empty((int(n_steps), self.n_envs), np.uint8) if fetch else None
+        check(self.lib.cov_step_expert(self.h, int(n_steps), ptr(r) if fetch else None, ptr(d) if fetch else None))
+        return (r, d.astype(bool)) if fetch else None
 
     def set_actions(self, actions):
         a = np.ascontiguousarray(np.asarray(actions).reshape(self.n_envs, self.n_robots), dtype=np.int32)

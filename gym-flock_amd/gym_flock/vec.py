@@ -267,6 +267,19 @@ class VecCoverage:
             return
         self.h.step(actions)
 
+    def expert_steps(self, n_steps, fetch=True):
+        """n_steps of the reference's greedy expert (controller(greedy=True) with its
+        np_random.choice(4) fallback draws, then step) for every env in ONE launch
+        (cov_step_expert): the same states, rewards and streams as n_steps calls of
+        step(greedy=True), for expert rollouts. Needs the streams on the device (a reset with
+        draws="device", or R <= 624 with host draws) and the greedy lists
+        (max_nodes - n_robots <= 1024). Returns (rewards (n_steps,B), done (n_steps,B)) or
+        None with fetch=False."""
+        if not self._device_draws():
+            raise RuntimeError("expert_steps needs the envs' np_random streams on the device, n_robots <= 624 "
+                               "and max_nodes - n_robots <= 1024")
+        return self.h.step_expert(n_steps, fetch=fetch)
+
     def set_actions(self, actions):
         self.h.set_actions(actions)
 

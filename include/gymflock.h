@@ -382,6 +382,15 @@ int cov_reset(cov_handle* h, const int32_t* start, const uint8_t* visited);
 int cov_reset_seeded(cov_handle* h, uint64_t seed, double frac_active, int32_t* start_out, uint8_t* visited_out);
 /* step(action) (:174-204, :234-364): actions[B][R] in [0,4). */
 int cov_step(cov_handle* h, const int32_t* actions, int flags);
+/* n_steps fused greedy expert steps (COV_ACTIONS_GREEDY | COV_GREEDY_RNG: controller(greedy=
+ * True)'s actions and the reference's np_random.choice(4) fallback draws, coverage.py:800-872,
+ * then step, :174-364) in ONE launch, each env's workgroup stepping its env n_steps times:
+ * the same result as n_steps calls of cov_step(h, NULL, COV_ACTIONS_GREEDY | COV_GREEDY_RNG)
+ * (expert rollouts: the reference's demonstrations). Needs the envs' streams on the device
+ * (cov_set_rng / cov_reset_seeded), n_robots <= 624 and max_nodes - n_robots <= 1024.
+ * rewards / done (both may be NULL; then the call returns without waiting): (n_steps, B) host
+ * arrays of every step's reward and done flag; the last step's are also cov_get_rewards'. */
+int cov_step_expert(cov_handle* h, int n_steps, double* rewards, uint8_t* done);
 int cov_set_actions(cov_handle* h, const int32_t* actions);
 /* Every env's np_random stream for COV_GREEDY_RNG steps, in the layout of numpy's
  * RandomState.get_state() (MT19937): keys[B][624] the key words, pos[B] in [0, 624] the

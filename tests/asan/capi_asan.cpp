@@ -268,6 +268,13 @@ static void coverage_session() {
   CHECK(cov_step(h, nullptr, COV_ACTIONS_GREEDY | COV_GREEDY_RNG) != 0);  // streams not set
   CHECK(cov_set_rng(h, keys.data(), pos.data()) == 0);
   for (int s = 0; s < 4; ++s) CHECK(cov_step(h, nullptr, COV_ACTIONS_GREEDY | COV_GREEDY_RNG) == 0);
+  // the same expert steps in one launch, every step's rewards and done flags to the host
+  std::vector<double> rk((size_t)5 * B);
+  std::vector<uint8_t> dk((size_t)5 * B);
+  CHECK(cov_step_expert(h, 5, rk.data(), dk.data()) == 0);
+  CHECK(cov_step_expert(h, 3, nullptr, nullptr) == 0);
+  CHECK(cov_step_expert(h, 0, nullptr, nullptr) != 0);
+  CHECK(cov_step_expert(nullptr, 1, nullptr, nullptr) != 0);
   CHECK(cov_get_rng(h, keys.data(), pos.data()) == 0);
   for (int b = 0; b < B; ++b) CHECK(pos[b] >= 0 && pos[b] <= 624);
   // the one-call drop-in step: pageable destinations, then page-locked ones

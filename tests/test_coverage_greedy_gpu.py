@@ -698,3 +698,42 @@ def test_device_reset_fraction_edges(frac):
     np.testing.assert_array_equal(vs[0].h.get_rng()[0], vs[1].h.get_rng()[0])
     for v in vs:
         v.close()
+
+
+@pytest.mark.parametrize("R", [20, 200])
+def test_expert_steps_one_launch_equals_single_steps(R):
+    """VecCoverage.expert_steps(n) (cov_step_expert: n fused greedy expert steps with the
+    device fallback draws in ONE launch) against n calls of step(greedy=True) on a twin
+    batch: 4 envs with their own device maps and streams, 75 steps (an episode) then 40 more
+    (at R=200 most robots draw once their targets are visited: several key regenerations
+    inside one launch). Every step's rewards and done flags, the final observations,
+    robots' nodes, visited flags, last actions and the streams bit-exact."""
+    B, M = 4, 1000
+    v1, v2 = VecCoverage(B, R, max_nodes=M), VecCoverage(B, R, max_nodes=M)
+    for v in (v1, v2):
+        v.reset(seed=21, new_maps=True, map_seed=5)
+    for n in (75, 40):
+        rw = np.empty((n, B))
+        dn = np.empty((n, B), bool)
+        for t in range(n):
+            v1.step(greedy=True)
+            rw[t], dn[t] = v1.rewards()
+        r2, d2 = v2.expert_steps(n)
+        np.testing.assert_array_equal(r2, rw)
+        np.testing.assert_array_equal(d2, dn)
+        for b in range(B):
+            o1, o2 = v1.obs(b), v2.obs(b)
+            for k in ("nodes", "edges", "senders", "receivers", "step"):
+                np.testing.assert_array_equal(o2[k], o1[k], err_msg="%s env %d" % (k, b))
+            np.testing.assert_array_equal(v2.h.robots(b)[1], v1.h.robots(b)[1])
+            np.testing.assert_array_equal(v2.h.visited(b), v1.h.visited(b))
+            s1, s2 = v1.np_random(b).get_state(), v2.np_random(b).get_state()
+            assert s1[2] == s2[2]
+            np.testing.assert_array_equal(s1[1], s2[1])
+        for x1, x2 in zip(v1.h.actions(), v2.h.actions()):
+            np.testing.assert_array_equal(x2, x1)
+    assert rw.sum() >= 0
+    with pytest.raises(nat.GymFlockError):
+        v2.h.step_expert(0)
+    v1.close()
+    v2.close()
