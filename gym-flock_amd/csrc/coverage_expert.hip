@@ -30,6 +30,9 @@ namespace gf {
 
 namespace {
 
+#ifndef GF_TM_DIAG
+#define GF_TM_DIAG 0  // timing ablations only (wrong results): 1 no early stop, 2 schedule window, 4 no predecessor stores
+#endif
 constexpr int kTmLanes = 64;            // sources per wave (one wave per workgroup)
 constexpr int kBatch = 8;               // independent edges per batch (16 measured slower)
 constexpr uint32_t kInf = 0xFFFF;  // uint16 cost matrix: unreachable
@@ -204,26 +207,44 @@ __global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, 
       uint32_t w[kBatch];
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt[k]);
+#if GF_TM_DIAG & 2
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) nxt[k] = sched[((j + kBatch) & 56) + k];
+#else
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) nxt[k] = sched[j + kBatch + k];  // next batch (slack in the stride)
+#endif
       uint32_t vs[kBatch], vq[kBatch];
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) {
         vs[k] = col[(w[k] & 0xFFFF) * kTmLanes + lane];
         vq[k] = col[(w[k] >> 16) * kTmLanes + lane];
       }
+      bool better[kBatch];
+      bool bany = false;
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) {
         const uint32_t via = vs[k] + 1u;  // inf + 1 never wins
-        const bool better = via < vq[k];
+        better[k] = via < vq[k];
         col[(w[k] >> 16) * kTmLanes + lane] = (V)(via < vq[k] ? via : vq[k]);
-        changed |= better ? 1 : 0;
-        // the predecessor, branch-free: a lane that did not improve stores past the end
-        // of the buffer's range, which the hardware drops (no exec-mask branch per edge:
-        // 8.63 -> 8.05-8.11 ms for 512 maps, profiles/r06/ab_tm_branchfree.txt)
-        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w[k] & 0xFFFF), prv,
-                                              better ? (int)(((w[k] >> 16) * (uint32_t)Tm + src) * 2) : (int)0x7FFFFFF0,
-                                              0, 0);
+        bany = bany || better[k];
+      }
+      changed |= bany ? 1 : 0;
+      // the predecessors, branch-free: a lane that did not improve stores past the end of
+      // the buffer's range, which the hardware drops (no exec-mask branch per edge: 8.63 ->
+      // 8.05-8.11 ms for 512 maps, profiles/r06/ab_tm_branchfree.txt); a batch no lane of
+      // the wave improved skips its 8 stores on one uniform branch (the later sweeps' usual
+      // case: 8.29 -> 7.69-7.76 ms, profiles/r06/ab_tm_store_skip.txt; a branch per edge,
+      // 8.54-8.58, and 16-edge schedule loads on top, 7.87-7.90, were slower)
+      if (__ballot(bany) != 0) {
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+#if !(GF_TM_DIAG & 4)
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w[k] & 0xFFFF), prv,
+                                                better[k] ? (int)(((w[k] >> 16) * (uint32_t)Tm + src) * 2) : (int)0x7FFFFFF0,
+                                                0, 0);
+#endif
+        }
       }
     }
     if (!PASS_B || sizeof(V) == 1) {
@@ -233,7 +254,7 @@ __global__ __launch_bounds__(kTmLanes) void cov_time_matrix_kernel(CovTmArgs a, 
         const bool any_changed = __ballot(changed) != 0;
         const bool any_inf = __ballot(any_inf_lane) != 0;
         if (lane == 0) flags[sweep] = (any_changed ? 1 : 0) | (any_inf ? 2 : 0);
-        if (!any_changed) {  // a fixed point: later sweeps change nothing
+        if (!any_changed && !(GF_TM_DIAG & 1)) {  // a fixed point: later sweeps change nothing
           for (int k = sweep + 1 + lane; k < a.kcap; k += kTmLanes) flags[k] = any_inf ? 2 : 0;
           break;
         }
