@@ -1792,8 +1792,24 @@ cut -c1-120 $O/ab_scan.txt
 timeout -k 10 400 python -u -m pytest tests/test_coverage_greedy_gpu.py tests/test_coverage_maps_gpu.py tests/test_coverage_gpu.py -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -1 $O/tests.log; exit $rc
 }
 
+r06_s20() {
+# Round 6, session 20: the drop-in greedy episode's first step (cov_time_matrix_mw_kernel)
+# with the predecessor LDS write under a per-edge branch (prod) against the branch-free
+# write to the dummy column (build/lib_plsel, -DGF_TM_MW_PL_SELECT=1 on the tree before the
+# branch-free write became the product and the switch was removed), interleaved, 8
+# episodes each; the Coverage greedy tests on the variant.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r06_s20; mkdir -p $O
+for r in 1 2 3; do for v in prod plsel; do
+  L=$PWD/build/lib_$v/libgymflock.so; [ $v = prod ] && L=$PWD/gym-flock_amd/lib/libgymflock.so
+  GYMFLOCK_LIB=$L EPISODES=8 timeout -k 10 120 python scripts/cov_first_step_probe.py > $O/probe_${v}_$r.txt 2>&1 || exit 1
+  echo "$v round $r first steps (us): $(grep 'step 0' $O/probe_${v}_$r.txt | awk '{print $5}' | tr '\n' ' ')"
+done; done
+GYMFLOCK_LIB=$PWD/build/lib_plsel/libgymflock.so timeout -k 10 300 python -u -m pytest tests/test_coverage_greedy_gpu.py -q --timeout 120 --timeout-method thread > $O/tests_plsel.log 2>&1; rc=$?; echo "plsel: $(tail -1 $O/tests_plsel.log)"; exit $rc
+}
+
 if [ $# -lt 1 ]; then
-  echo "usage: $0 <session> [args]   sessions: r03_ab1 r03_ab2 r03_profile r03_session r03_s3 r03_s4 r03_s5 r03_s6 r03_s7 r03_s8 r03_s9 r03_s10 r03_s11 r03_s12 r03_s13 r03_s14 r03_s15 r03_s16 r03_s17 r03_s18 r03_s19 r03_s20 r03_s21 r03_s22 r03_s25 r03_s26 r03_s27 r03_s28 r03_s29 r03_s30 r03_s31 r03_s32 r03_s33 r03_s34 r03_s35 r03_s36 r03_s37 r03_s38 r03_s39 r04_final r04_profile r04_session r04_s3 r04_s4 r04_s5 r04_s7 r04_s8 r04_s9 r04_s10 r04_s11 r04_s12 r04_s13 r04_s14 r04_s15 r04_s16 r04_s17 r04_s18 r04_s19 r04_s20 r04_s21 r04_s22 r04_s23 r04_s24 r04_s25 r04_s26 r04_s27 r04_s28 r04_s29 r04_s30 r04_s31 r04_s32 r04_s33 r04_s34 r05_profile r05_s1 r05_s2 r05_s3 r05_s4 r05_s5 r05_s6 r05_s7 r05_s8 r05_s9 r05_s10 r05_s11 r05_s12 r05_s13 r05_s14 r05_s15 r05_s16 r05_s17 r05_s18 r05_s19 r05_s20 r05_s21 r05_s22 r05_s23 r05_s24 r05_s25 r05_s26 r05_s27 r06_profile_a r06_profile_b r06_s1 r06_s2 r06_s3 r06_s6 r06_s10 r06_s11 r06_s12 r06_s19"
+  echo "usage: $0 <session> [args]   sessions: r03_ab1 r03_ab2 r03_profile r03_session r03_s3 r03_s4 r03_s5 r03_s6 r03_s7 r03_s8 r03_s9 r03_s10 r03_s11 r03_s12 r03_s13 r03_s14 r03_s15 r03_s16 r03_s17 r03_s18 r03_s19 r03_s20 r03_s21 r03_s22 r03_s25 r03_s26 r03_s27 r03_s28 r03_s29 r03_s30 r03_s31 r03_s32 r03_s33 r03_s34 r03_s35 r03_s36 r03_s37 r03_s38 r03_s39 r04_final r04_profile r04_session r04_s3 r04_s4 r04_s5 r04_s7 r04_s8 r04_s9 r04_s10 r04_s11 r04_s12 r04_s13 r04_s14 r04_s15 r04_s16 r04_s17 r04_s18 r04_s19 r04_s20 r04_s21 r04_s22 r04_s23 r04_s24 r04_s25 r04_s26 r04_s27 r04_s28 r04_s29 r04_s30 r04_s31 r04_s32 r04_s33 r04_s34 r05_profile r05_s1 r05_s2 r05_s3 r05_s4 r05_s5 r05_s6 r05_s7 r05_s8 r05_s9 r05_s10 r05_s11 r05_s12 r05_s13 r05_s14 r05_s15 r05_s16 r05_s17 r05_s18 r05_s19 r05_s20 r05_s21 r05_s22 r05_s23 r05_s24 r05_s25 r05_s26 r05_s27 r06_profile_a r06_profile_b r06_s1 r06_s2 r06_s3 r06_s6 r06_s10 r06_s11 r06_s12 r06_s19 r06_s20"
   exit 2
 fi
 "$@"
