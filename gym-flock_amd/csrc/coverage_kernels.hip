@@ -884,14 +884,15 @@ __global__ __launch_bounds__(kCovThreads) void cov_reset_kernel(CovArgs a, const
 // int(T * frac), replace=False) for the unvisited ones, each numpy's legacy permutation of
 // the stream (Fisher-Yates from the top, random_interval's masked rejection: oracle/
 // mt19937.py). The stream is left in mt_key / mt_pos for the fallback draws
-// (COV_GREEDY_RNG). One wave per env: the draws and swaps form one chain, which every lane
-// runs (lane 0 swaps); the key regenerations take the whole wave.
+// (COV_GREEDY_RNG). One wave per env: the draws are one chain, which every lane runs, then
+// lane 0 swaps; the key regenerations and the tempering take the whole wave.
 __global__ __launch_bounds__(64) void cov_seed_reset_kernel(CovArgs a, uint32_t seed0, double frac, int32_t* start,
                                                             uint8_t* visited0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* key = reinterpret_cast<uint32_t*>(smem);
   int32_t* perm = reinterpret_cast<int32_t*>(key + kMtN);
-  uint8_t* vis = reinterpret_cast<uint8_t*>(perm + a.Tmax);
+  int32_t* vseq = perm + a.Tmax;  // [Tm] the draws of one permutation, by i
+  uint8_t* vis = reinterpret_cast<uint8_t*>(vseq + a.Tmax);
   const int b = blockIdx.x, lane = threadIdx.x;
   const int R = a.R, Tm = a.Tmax, T = a.ntg[b];
   if (lane == 0) {
@@ -903,33 +904,40 @@ __global__ __launch_bounds__(64) void cov_seed_reset_kernel(CovArgs a, uint32_t 
   }
   __syncthreads();
   int pos = kMtN;  // wave-uniform
-  auto next = [&]() {
-    if (pos == kMtN) {
-      mt_regen<64>(key);
-      pos = 0;
-    }
-    return mt_temper(key[pos++]);
-  };
-  auto permute = [&](int n) {  // RandomState.permutation(n) into perm[0, n)
+  // RandomState.permutation(n) into perm[0, n). The draws do not depend on the permutation,
+  // so they come first: 64 tempered words per round (one LDS load per lane), consumed in
+  // stream order by a register chain (readlane; the masked rejection of each i), the
+  // accepted ones into vseq[i]; then lane 0 runs the swaps, one LDS round trip each (the
+  // draws and swaps interleaved waited on two per swap)
+  auto permute = [&](int n) {
     for (int k = lane; k < n; k += 64) perm[k] = k;
+    int i = n - 1;  // wave-uniform
+    while (i >= 1) {
+      if (pos == kMtN) {
+        mt_regen<64>(key);
+        pos = 0;
+      }
+      const int avail = min(64, kMtN - pos);
+      const uint32_t wl = lane < avail ? mt_temper(key[pos + lane]) : 0u;
+      int u = 0;
+      for (; u < avail && i >= 1; ++u) {
+        const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz(static_cast<uint32_t>(i));
+        const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wl), u)) & mask;
+        if (v <= static_cast<uint32_t>(i)) {
+          if (lane == 0) vseq[i] = static_cast<int>(v);
+          --i;
+        }
+      }
+      pos += u;
+    }
     __syncthreads();
-    for (int i = n - 1; i >= 1; --i) {
-      uint32_t mask = static_cast<uint32_t>(i);
-      mask |= mask >> 1;
-      mask |= mask >> 2;
-      mask |= mask >> 4;
-      mask |= mask >> 8;
-      mask |= mask >> 16;
-      uint32_t v;
-      do {
-        v = next() & mask;
-      } while (v > static_cast<uint32_t>(i));
-      if (lane == 0) {  // one lane: its LDS reads and writes stay in program order
-        const int t = perm[i];
-        perm[i] = perm[v];
+    if (lane == 0)  // one lane: its LDS reads and writes stay in program order
+      for (int k = n - 1; k >= 1; --k) {
+        const int v = vseq[k];
+        const int t = perm[k];
+        perm[k] = perm[v];
         perm[v] = t;
       }
-    }
     __syncthreads();
   };
   permute(T);
@@ -1045,7 +1053,7 @@ hipError_t launch_cov_graph(const CovArgs& a, const int32_t* envs, int n, hipStr
 
 hipError_t launch_cov_seed_reset(const CovArgs& a, uint32_t seed0, double frac, int32_t* start, uint8_t* visited0,
                                  hipStream_t s) {
-  const size_t lds = (size_t)kMtN * 4 + (size_t)a.Tmax * 5;
+  const size_t lds = (size_t)kMtN * 4 + (size_t)a.Tmax * 9;
   hipLaunchKernelGGL(cov_seed_reset_kernel, dim3(a.B), dim3(64), lds, s, a, seed0, frac, start, visited0);
   return hipGetLastError();
 }
