@@ -908,7 +908,7 @@ __global__ __launch_bounds__(64) void cov_seed_reset_kernel(CovArgs a, uint32_t 
   // so they come first: 64 tempered words per round (one LDS load per lane), consumed in
   // stream order by a register chain (readlane; the masked rejection of each i), the
   // accepted ones into vseq[i]; then lane 0 runs the swaps, one LDS round trip each (the
-  // draws and swaps interleaved waited on two per swap)
+  // draws and swaps interleaved waited on two per swap; profiles/r06/ab_seed_reset_draws.txt)
   auto permute = [&](int n) {
     for (int k = lane; k < n; k += 64) perm[k] = k;
     int i = n - 1;  // wave-uniform
@@ -931,13 +931,19 @@ __global__ __launch_bounds__(64) void cov_seed_reset_kernel(CovArgs a, uint32_t 
       pos += u;
     }
     __syncthreads();
-    if (lane == 0)  // one lane: its LDS reads and writes stay in program order
+    if (lane == 0 && n > 1) {  // one lane: its LDS reads and writes stay in program order
+      // the next swap's draw is read with this swap's entries (vseq is not written here),
+      // so a swap waits on one LDS round trip, not two
+      int v = vseq[n - 1];
       for (int k = n - 1; k >= 1; --k) {
-        const int v = vseq[k];
+        const int vnext = vseq[k - 1];  // vseq[0]: read, never used
         const int t = perm[k];
-        perm[k] = perm[v];
+        const int pv = perm[v];
+        perm[k] = pv;
         perm[v] = t;
+        v = vnext;
       }
+    }
     __syncthreads();
   };
   permute(T);
